@@ -1,0 +1,86 @@
+"""Fixture configurations shared by the golden generator and the parity tests.
+
+Each entry is a set of reference CLI flags (GLI:17-62).  Sizes are reduced (h=8,
+z=16, B=8, S=32) so the oracle replays them in seconds.  Large tensors are stored
+as sha1 + sums + sampled elements: the sha1 pins the oracle bitwise (CPU tests),
+the samples/sums let a GPU result be compared within tolerance.  The full-size
+configs of BASELINE.json are covered by size-independent property tests.
+"""
+import hashlib
+
+import numpy as np
+import torch
+
+FULL_LIMIT = 1024  # tensors above this many elements are stored as summaries (sha1 + stats + samples)
+
+_SMALL = {"image_size": 32, "batch_size": 8, "z_size": 16, "G_h_size": 8, "D_h_size": 8,
+          "n_iter": 3}
+
+
+def _cfg(**kw):
+    args = dict(_SMALL)
+    args.update(kw)
+    return {"args": args, "seed": 1, "n_images": 64}
+
+
+CONFIGS = {
+    "sgan": _cfg(loss_D=1),
+    "lsgan": _cfg(loss_D=2),
+    "wgangp": _cfg(loss_D=3),
+    "hinge": _cfg(loss_D=4),
+    "rsgan": _cfg(loss_D=5),
+    "rasgan": _cfg(loss_D=6),
+    "ralsgan": _cfg(loss_D=7),
+    "rahinge": _cfg(loss_D=8),
+    "ralsgan64": _cfg(loss_D=7, image_size=64),
+    "rahinge_spectral": _cfg(loss_D=8, spectral="True"),
+    "ralsgan_gp": _cfg(loss_D=7, grad_penalty="True"),
+    "rasgan_spectralG": _cfg(loss_D=6, spectral_G="True"),
+    "ralsgan_nobn": _cfg(loss_D=7, no_batch_norm_G="True", no_batch_norm_D="True"),
+    "ralsgan_tanh": _cfg(loss_D=7, Tanh_GD="True"),
+    "ralsgan_selu": _cfg(loss_D=7, SELU="True"),
+    "ralsgan_wd": _cfg(loss_D=7, weight_decay=0.01, decay=0.1),
+    "wgangp_arch1": {"args": {"image_size": 32, "batch_size": 8, "z_size": 16, "loss_D": 3,
+                              "arch": 1, "n_iter": 2}, "seed": 1, "n_images": 64},
+    "rahinge_arch1": {"args": {"image_size": 32, "batch_size": 8, "z_size": 16, "loss_D": 8,
+                               "arch": 1, "n_iter": 2}, "seed": 1, "n_images": 64},
+}
+
+
+def summarize_indices(numel, count=64, seed=97):
+    """Positions sampled from a large tensor (same on every machine)."""
+    rng = np.random.default_rng(seed + numel)
+    return np.sort(rng.choice(numel, size=min(count, numel), replace=False))
+
+
+class Recorder:
+    def __init__(self):
+        self.store = {}
+
+    def put(self, key, t):
+        t = t.detach().to(torch.float32).contiguous().cpu() if t.is_floating_point() else t.detach().cpu()
+        arr = t.numpy()
+        if arr.size <= FULL_LIMIT:
+            self.store[key] = arr.copy()
+        else:
+            flat = arr.reshape(-1).astype(np.float32)
+            idx = summarize_indices(flat.size)
+            self.store[key + "@sample"] = flat[idx].copy()
+            self.store[key + "@shape"] = np.array(arr.shape, dtype=np.int64)
+            self.store[key + "@sum"] = np.array([flat.astype(np.float64).sum(),
+                                                 (flat.astype(np.float64) ** 2).sum()])
+            self.store[key + "@sha1"] = np.frombuffer(
+                hashlib.sha1(flat.tobytes()).hexdigest().encode(), dtype=np.uint8).copy()
+
+    def state(self, prefix, module):
+        for k, v in module.state_dict().items():
+            self.put(f"{prefix}.{k}", v)
+
+    def optim(self, prefix, opt, module):
+        names = [n for n, _ in module.named_parameters()]
+        for p, n in zip(module.parameters(), names):
+            st = opt.state.get(p, {})
+            if st:
+                self.put(f"{prefix}.{n}.exp_avg", st["exp_avg"])
+                self.put(f"{prefix}.{n}.exp_avg_sq", st["exp_avg_sq"])
+                self.store[f"{prefix}.{n}.step"] = np.array([float(st["step"])])

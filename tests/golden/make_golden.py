@@ -1,0 +1,205 @@
+#!/usr/bin/env python3
+"""Golden-vector generator: runs the UNMODIFIED reference training script on CPU.
+
+Test infrastructure only (runs in the build container, never on the GPU box, never
+imported by the product).  It executes ``/root/reference/code/GAN_losses_iter.py``
+(referred to as GLI below) with ``runpy`` after injecting stub modules for the
+third-party packages the script imports but this image lacks (torchvision,
+IPython, fid, pytorch_visualize; GLI:121-143).  The stubs only replace I/O:
+
+* ``torchvision.datasets.ImageFolder`` -> a synthetic uint8 image set mapped by
+  ``(u8/255 - 0.5)/0.5`` (what ToTensor+Normalize does, GLI:160-166);
+* ``torchvision.utils.save_image`` -> no-op (GLI:565, 768);
+* ``fid.calculate_fid_given_paths`` / ``pytorch_visualize`` / ``IPython`` -> unused.
+
+Capture points: ``torch.optim.Adam.__init__`` (state after ``weights_init``,
+GLI:476-477, and ``z_test``, GLI:497) and ``torch.optim.Adam.step`` (GLI:659 and
+GLI:712).  At each step the harness reads the loop's module-level variables
+(``x``, ``z``, ``u``, ``y_pred``, ``y_pred_fake``, ``errD``, ``errG``) from the
+script's frame, the parameter gradients before the update and the full module and
+optimizer state after it.
+
+Output: one ``.npz`` per config under ``tests/golden/`` (``allow_pickle=False``
+loadable).  Tensors above ``FULL_LIMIT`` elements are stored as a summary
+(sampled elements at seeded positions + sum + sum of squares + sha1) so the arch-1
+fixtures stay small.
+
+Usage:  python tests/golden/make_golden.py [config-name ...]
+"""
+import json
+import os
+import runpy
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+REF_SCRIPT = "/root/reference/code/GAN_losses_iter.py"
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+from tests.golden.configs import CONFIGS, Recorder  # noqa: E402
+
+THREADS = 1
+
+
+def synthetic_dataset(n, size, seed=1234, n_colors=3):
+    """uint8 images -> float in [-1,1] on the 1/127.5 grid."""
+    g = torch.Generator().manual_seed(seed)
+    u8 = torch.randint(0, 256, (n, n_colors, size, size), generator=g, dtype=torch.uint8)
+    return (u8.float() / 255.0 - 0.5) / 0.5
+
+
+def install_stubs(dataset):
+    tv = types.ModuleType("torchvision")
+    dset = types.ModuleType("torchvision.datasets")
+    transf = types.ModuleType("torchvision.transforms")
+    models = types.ModuleType("torchvision.models")
+    vutils = types.ModuleType("torchvision.utils")
+
+    class _Folder:
+        def __init__(self, *a, **k):
+            self.images = dataset
+
+        def __len__(self):
+            return self.images.shape[0]
+
+        def __getitem__(self, i):
+            return self.images[i], 0
+
+    dset.ImageFolder = _Folder
+    dset.CIFAR10 = _Folder
+
+    class _Identity:
+        def __init__(self, *a, **k):
+            pass
+
+        def __call__(self, x):
+            return x
+
+    for name in ("Compose", "Resize", "ToTensor", "Normalize", "ToPILImage"):
+        setattr(transf, name, _Identity)
+    vutils.save_image = lambda *a, **k: None
+    tv.datasets, tv.transforms, tv.models, tv.utils = dset, transf, models, vutils
+    sys.modules.update({"torchvision": tv, "torchvision.datasets": dset,
+                        "torchvision.transforms": transf, "torchvision.models": models,
+                        "torchvision.utils": vutils})
+    ipy = types.ModuleType("IPython")
+    ipyd = types.ModuleType("IPython.display")
+    ipyd.Image = lambda *a, **k: None
+    ipy.display = ipyd
+    sys.modules.update({"IPython": ipy, "IPython.display": ipyd})
+    pv = types.ModuleType("pytorch_visualize")
+    pv.make_dot = lambda *a, **k: None
+    sys.modules["pytorch_visualize"] = pv
+    fid = types.ModuleType("fid")
+    fid.calculate_fid_given_paths = lambda *a, **k: 0.0
+    sys.modules["fid"] = fid
+
+
+def _script_globals():
+    f = sys._getframe(1)
+    while f is not None:
+        if "optimizerD" in f.f_globals and "param" in f.f_globals:
+            return f.f_globals
+        f = f.f_back
+    return None
+
+
+def run_config(name, cfg):
+    torch.set_num_threads(THREADS)
+    args = cfg["args"]
+    S = args.get("image_size", 64)
+    dataset = synthetic_dataset(cfg.get("n_images", 64), S)
+    install_stubs(dataset)
+    rec = Recorder()
+    n_iter = args.get("n_iter", 3)
+
+    orig_init = torch.optim.Adam.__init__
+    orig_step = torch.optim.Adam.step
+    n_init = [0]
+
+    def init_hook(self, params, *a, **k):
+        orig_init(self, params, *a, **k)
+        n_init[0] += 1
+        if n_init[0] == 2:  # optimizerG: G and D fully initialised (GLI:529-530)
+            g = sys._getframe(1).f_globals
+            rec.state("init.G", g["G"])
+            rec.state("init.D", g["D"])
+            rec.put("init.z_test", g["z_test"])
+
+    def step_hook(self, *a, **k):
+        g = _script_globals()
+        i = g["i"]
+        if self is g["optimizerD"]:
+            tag = f"it{i}.D"
+            rec.put(tag + ".x", g["x"])
+            rec.put(tag + ".z", g["z"])
+            if g["param"].loss_D == 3 or g["param"].grad_penalty:
+                rec.put(tag + ".u", g["u"])
+                rec.put(tag + ".gp", g["grad_penalty"].reshape(1))
+            rec.put(tag + ".y_pred", g["y_pred"])
+            rec.put(tag + ".y_pred_fake", g["y_pred_fake"])
+            rec.put(tag + ".errD", g["errD"].reshape(1))
+            for n, p in g["D"].named_parameters():
+                rec.put(f"{tag}.grad.{n}", p.grad)
+            out = orig_step(self, *a, **k)
+            rec.state(tag + ".post", g["D"])
+            rec.state(tag + ".postG", g["G"])
+            rec.optim(tag + ".adam", self, g["D"])
+        else:
+            tag = f"it{i}.G"
+            rec.put(tag + ".z", g["z"])
+            if g["param"].loss_D not in (1, 2, 3, 4):
+                rec.put(tag + ".x", g["x"])
+                rec.put(tag + ".y_pred", g["y_pred"])
+            rec.put(tag + ".y_pred_fake", g["y_pred_fake"])
+            rec.put(tag + ".errG", g["errG"].reshape(1))
+            for n, p in g["G"].named_parameters():
+                rec.put(f"{tag}.grad.{n}", p.grad)
+            out = orig_step(self, *a, **k)
+            rec.state(tag + ".post", g["G"])
+            rec.state(tag + ".postD", g["D"])
+            rec.optim(tag + ".adam", self, g["G"])
+        return out
+
+    torch.optim.Adam.__init__ = init_hook
+    torch.optim.Adam.step = step_hook
+    tmp = tempfile.mkdtemp(prefix="rgan_golden_")
+    argv = [REF_SCRIPT, "--cuda", "False", "--seed", str(cfg.get("seed", 1)),
+            "--n_iter", str(n_iter), "--gen_extra_images", "0", "--print_every", "1000",
+            "--output_folder", tmp, "--extra_folder", tmp + "/extra", "--input_folder", tmp]
+    for k, v in args.items():
+        if k == "n_iter":
+            continue
+        argv += ["--" + k, str(v)]
+    old_argv, old_cwd = sys.argv, os.getcwd()
+    sys.argv = argv
+    os.chdir(tmp)
+    try:
+        runpy.run_path(REF_SCRIPT, run_name="__main__")
+    finally:
+        sys.argv = old_argv
+        os.chdir(old_cwd)
+        torch.optim.Adam.__init__ = orig_init
+        torch.optim.Adam.step = orig_step
+    rec.store["meta.json"] = np.frombuffer(json.dumps({
+        "config": name, "args": args, "seed": cfg.get("seed", 1), "n_iter": n_iter,
+        "n_images": cfg.get("n_images", 64), "threads": THREADS,
+        "torch": torch.__version__}).encode(), dtype=np.uint8).copy()
+    out = os.path.join(HERE, f"{name}.npz")
+    np.savez_compressed(out, **rec.store)
+    return out
+
+
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(CONFIGS)
+    if len(names) == 1:
+        print(names[0], "->", run_config(names[0], CONFIGS[names[0]]), flush=True)
+    else:  # one fresh interpreter per config: the reference mutates global torch state
+        import subprocess
+        for n in names:
+            r = subprocess.run([sys.executable, os.path.abspath(__file__), n],
+                               capture_output=True, text=True)
+            print(n, "ok" if r.returncode == 0 else "FAILED\n" + r.stderr[-2000:], flush=True)
