@@ -1,0 +1,164 @@
+/*
+ * rgan.h — C-ABI of the MI355X (gfx950) RelativisticGAN training core.
+ *
+ * The reference has no FFI of its own: its hot path is the module-level PyTorch
+ * training loop of code/GAN_losses_iter.py (GLI).  Each entry point below replaces
+ * the PyTorch op(s) that loop reaches, cited per function.
+ *
+ * Conventions:
+ *   - plain device pointers (fp32 unless stated) and sizes; no torch types;
+ *   - the caller allocates every output and every workspace; kernels never allocate;
+ *   - return 0 on success, a hipError_t-compatible code otherwise
+ *     (RGAN_EINVAL = invalid descriptor / sizes, checked on the host before launch);
+ *   - every launch goes on `stream` (hipStream_t passed as void*); no host syncs, so
+ *     every entry point is hipGraph-capturable.
+ */
+#ifndef RGAN_H
+#define RGAN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RGAN_EINVAL 1001
+
+/* Activation codes fused into epilogues (GLI:345,370,388,417,437,450; SELU GLI:338). */
+enum {
+  RGAN_ACT_NONE = 0, RGAN_ACT_RELU = 1, RGAN_ACT_LRELU = 2, RGAN_ACT_TANH = 3,
+  RGAN_ACT_SIGMOID = 4, RGAN_ACT_SELU = 5
+};
+
+/* One 2-D convolution as the reference's torch.nn.Conv2d / ConvTranspose2d sees it.
+ * "x" is the op's input image, "y" its output.  Element strides are given for
+ * (batch, channel, h, w) so NCHW (reference layout) and NHWC (internal layout,
+ * torch channels_last) tensors are both accepted.  Weights are in torch layout:
+ * Conv2d [cout][cin][kh][kw], ConvTranspose2d [cin][cout][kh][kw], contiguous. */
+typedef struct RganConv {
+  int batch;
+  int cin, hin, win;
+  int cout, hout, wout;
+  int kh, kw, stride, pad;
+  int transposed;          /* 0: Conv2d, 1: ConvTranspose2d */
+  long long xs[4];         /* x strides (b, c, h, w) in elements */
+  long long ys[4];         /* y strides (b, c, h, w) in elements */
+} RganConv;
+
+/* Workspace bytes needed by rgan_conv_{fwd,dgrad,wgrad}; `which` = 0 fwd, 1 dgrad, 2 wgrad. */
+size_t rgan_conv_workspace(const RganConv* d, int which);
+
+/* y = act(conv(x, w) * wscale + bias).  Replaces Conv2d/ConvTranspose2d.forward
+ * (GLI:336,361,387,410,428,448; arch 1 GLI:202-223,260-302) fused with the
+ * following activation when no BatchNorm sits between them.  wscale: nullable device
+ * scalar (spectral norm's 1/sigma, torch/nn/utils/spectral_norm.py:115-116). */
+int rgan_conv_fwd(const RganConv* d, const float* x, const float* w, const float* wscale,
+                  const float* bias, float* y, int act, float act_alpha,
+                  void* ws, size_t ws_bytes, void* stream);
+
+/* dx = d conv / d x applied to dy  (aten convolution_backward, grad_input). */
+int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* w, const float* wscale,
+                    float* dx, void* ws, size_t ws_bytes, void* stream);
+
+/* dw = d conv / d w applied to dy (aten convolution_backward, grad_weight), written
+ * in torch weight layout; dbias (nullable) = per-output-channel sum of dy. */
+int rgan_conv_wgrad(const RganConv* d, const float* x, const float* dy, float* dw, float* dbias,
+                    void* ws, size_t ws_bytes, void* stream);
+
+/* ---- BatchNorm2d, train mode (GLI:341,366,433; arch 1 GLI:204-218,262-297) ----
+ * Tensors are [batch*h*w][C] with element strides (sp = pixel stride, sc = channel
+ * stride); P = batch*h*w.  stats = float[2*C] workspace slot receiving (mean, invstd).
+ * Running stats follow torch: r = (1-m) r + m * stat, unbiased var for running_var;
+ * num_batches_tracked (int64, nullable) += 1.  `partial` workspace: rgan_bn_partial_bytes. */
+size_t rgan_bn_partial_bytes(long long P, int C);
+int rgan_bn_stats(const float* y, long long P, int C, long long sp, long long sc,
+                  float eps, float momentum, float* running_mean, float* running_var,
+                  long long* num_batches_tracked, float* stats, void* partial, void* stream);
+/* a = act(gamma * (y - mean) * invstd + beta)  (torch's alpha/beta form) */
+int rgan_bn_apply(const float* y, long long P, int C, long long sp, long long sc,
+                  const float* stats, const float* gamma, const float* beta,
+                  int act, float act_alpha, float* a, long long asp, long long asc, void* stream);
+/* Backward through act(BN(y)): given da, produce dy, dgamma, dbeta. */
+int rgan_bn_backward(const float* da, long long dsp, long long dsc,
+                     const float* y, long long P, int C, long long sp, long long sc,
+                     const float* stats, const float* gamma, const float* beta,
+                     int act, float act_alpha, float* dy, long long ysp, long long ysc,
+                     float* dgamma, float* dbeta, void* partial, void* stream);
+
+/* ---- elementwise ---- */
+/* dx = da * act'(a) where a = act(x) is the saved activation output. */
+int rgan_act_backward(const float* da, const float* a, long long n, int act, float act_alpha,
+                      float* dx, void* stream);
+/* out[n] = sum over pixels of t (per channel; bias gradient), strided like bn. */
+int rgan_channel_sum(const float* t, long long P, int C, long long sp, long long sc,
+                     float* out, void* partial, void* stream);
+
+/* ---- loss heads (GLI:481-484, 592-644, 686-709) ----
+ * kind = --loss_D (1..8); side 0 = D-real (heads 1-4) / D (heads 5-8), 1 = D-fake
+ * (heads 1-4), 2 = G.  r, f: [n] (either nullable per head).  loss: device float[1];
+ * dr, df: [n] gradients of loss w.r.t. r and f (nullable).  n <= 65536. */
+int rgan_loss_head(int kind, int side, const float* r, const float* f, int n,
+                   float* loss, float* dr, float* df, void* stream);
+/* Distributed form: the three phases of the same head with the cross-rank sums done by
+ * the caller between them.  phase 0: sums[0..1] = (sum r, sum f) local;
+ * phase 1: given global means in gsum[0..1] (sum r, sum f over n_global), sums[0..3] =
+ * local (sum a, sum b, sum a', sum b'); phase 2: loss and grads from global gsum[0..5]. */
+int rgan_loss_head_dist(int kind, int side, int phase, const float* r, const float* f, int n,
+                        int n_global, const float* gsum, float* sums, float* loss,
+                        float* dr, float* df, void* stream);
+/* out = in * (*scale) (device scalar), used to apply an upstream gradient. */
+int rgan_scale(const float* in, const float* scale, long long n, float* out, void* stream);
+
+/* ---- WGAN-GP (GLI:646-658) ---- */
+/* xb[b] = x[b]*u[b] + xf[b]*(1-u[b]) over per-sample blocks of `per` elements. */
+int rgan_gp_interp(const float* x, const float* xf, const float* u, int batch, long long per,
+                   float* xb, void* stream);
+/* norms[b] = ||g_b||_2 ; loss = lam * mean_b (norms-1)^2 over n_global samples. */
+int rgan_gp_penalty(const float* g, int batch, long long per, float lam, int n_global,
+                    float* norms, float* loss, void* stream);
+/* dg = (*gscale) * lam * 2 (norm_b - 1)/n_global * g_b / norm_b (0 where norm_b == 0). */
+int rgan_gp_penalty_backward(const float* g, const float* norms, int batch, long long per,
+                             float lam, int n_global, const float* gscale, float* dg,
+                             void* stream);
+
+/* ---- spectral norm (torch/nn/utils/spectral_norm.py:62-139; GLI call sites 334-446) ----
+ * W viewed as [rows][cols]; element (r, c) sits at r*rs + (c / lo)*hs + (c % lo).
+ * Conv2d weight (dim 0): rs = cin*kk, hs = kk, lo = kk.  ConvTranspose2d (dim 1, the
+ * permute(1,0,2,3) view): rs = kk, hs = cout*kk, lo = kk.
+ * One power iteration: v = normalize(W^T u), u = normalize(W v), sigma = u.(W v);
+ * writes u, v in place and inv_sigma[0] = 1/sigma.  do_iter = 0 only recomputes sigma.
+ * ws: rgan_spectral_ws_bytes(rows, cols). */
+size_t rgan_spectral_ws_bytes(int rows, int cols);
+int rgan_spectral_power(const float* W, int rows, int cols, long long rs, long long hs, int lo,
+                        float eps, float* u, float* v, float* inv_sigma, int do_iter,
+                        void* ws, void* stream);
+/* dW_orig = dW_eff/sigma - (<dW_eff, W_orig>/sigma^2) u v^T (u, v constants); ws >= 1 KiB. */
+int rgan_spectral_backward(const float* W, const float* dWeff, int rows, int cols,
+                           long long rs, long long hs, int lo, const float* u, const float* v,
+                           const float* inv_sigma, float* dW, void* ws, void* stream);
+
+/* ---- Adam (torch/optim/adam.py:347-547, _single_tensor_adam semantics) ----
+ * Updates `ntensors` tensors (any count; launched in chunks).  hyper = device double[8]:
+ * {lr, beta1, beta2, eps, weight_decay, 0, 0, 0} (doubles, as torch keeps them in
+ * Python floats); step = device float[1], incremented once per call before use, like
+ * state['step'].  Pointer arrays are host arrays of device pointers. */
+int rgan_adam(int ntensors, float* const* params, const float* const* grads,
+              float* const* exp_avg, float* const* exp_avg_sq, const long long* numel,
+              const double* hyper, float* step, void* stream);
+/* hyper[0] *= gamma (ExponentialLR.step, GLI:533-534,713-714). */
+int rgan_lr_decay(double* hyper, double gamma, void* stream);
+
+/* ---- data movement ---- */
+/* out[b] = images[idx[b]] for per-image blocks of `per` floats (the real-batch draw,
+ * GLI:176-178, 581-583, on a dataset resident in HBM). */
+int rgan_gather_images(const float* images, const long long* idx, int batch, long long per,
+                       float* out, void* stream);
+
+/* Library self-description: number of exported compute entry points, version string. */
+const char* rgan_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

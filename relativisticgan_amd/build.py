@@ -1,0 +1,63 @@
+"""Build the gfx950 HIP library in-tree: relativisticgan_amd/librgan.so.
+
+One hipcc invocation per translation unit (compiled in parallel), then one link.  The
+.so is plain C-ABI (include/rgan.h) with no torch dependency; Python loads it with
+ctypes (relativisticgan_amd/_lib.py).
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "librgan.so")
+BUILD = os.path.join(HERE, "build")
+ARCH = os.environ.get("RGAN_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I" + os.path.join(ROOT, "include"),
+         "-Wno-unused-result", "-munsafe-fp-atomics"]
+SOURCES = ["conv_gemm.hip", "bn_act.hip", "heads_optim.hip"]
+
+
+def _stale(obj, src):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    deps = [src] + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    deps.append(os.path.join(ROOT, "include", "rgan.h"))
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose=False, force=False):
+    os.makedirs(BUILD, exist_ok=True)
+    jobs = []
+    for s in SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(BUILD, s.replace(".hip", ".o"))
+        if force or _stale(obj, src):
+            jobs.append([HIPCC, *FLAGS, "-c", src, "-o", obj])
+
+    def run(cmd):
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        return cmd, r
+
+    with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
+        for cmd, r in ex.map(run, jobs):
+            if verbose or r.returncode:
+                sys.stderr.write(r.stdout + r.stderr)
+            if r.returncode:
+                raise RuntimeError(f"hipcc failed: {' '.join(cmd)}")
+    objs = [os.path.join(BUILD, s.replace(".hip", ".o")) for s in SOURCES]
+    if force or jobs or not os.path.exists(OUT) or any(os.path.getmtime(o) > os.path.getmtime(OUT) for o in objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode:
+            sys.stderr.write(r.stdout + r.stderr)
+            raise RuntimeError("link failed")
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(verbose="-v" in sys.argv, force="-f" in sys.argv))

@@ -1,0 +1,107 @@
+// Shared device helpers for the gfx950 kernels (wave64, CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/rgan.h"
+
+#define RGAN_CHECK_LAUNCH()                         \
+  do {                                              \
+    hipError_t _e = hipGetLastError();              \
+    if (_e != hipSuccess) return (int)_e;           \
+  } while (0)
+
+#define RGAN_REQUIRE(cond)                          \
+  do {                                              \
+    if (!(cond)) return RGAN_EINVAL;                \
+  } while (0)
+
+namespace rgan {
+
+constexpr int WAVE = 64;
+
+__device__ __forceinline__ float act_fwd(float v, int act, float alpha) {
+  switch (act) {
+    case RGAN_ACT_RELU: return v > 0.f ? v : 0.f;
+    case RGAN_ACT_LRELU: return v > 0.f ? v : v * alpha;
+    case RGAN_ACT_TANH: return tanhf(v);
+    case RGAN_ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+    case RGAN_ACT_SELU: {
+      const float scale = 1.0507009873554804934193349852946f;
+      const float a = 1.6732632423543772848170429916717f;
+      return v > 0.f ? scale * v : scale * (a * (expf(v) - 1.f));
+    }
+    default: return v;
+  }
+}
+
+// derivative of act expressed through the activation OUTPUT a = act(x)
+__device__ __forceinline__ float act_grad_from_out(float a, int act, float alpha) {
+  switch (act) {
+    case RGAN_ACT_RELU: return a > 0.f ? 1.f : 0.f;
+    case RGAN_ACT_LRELU: return a > 0.f ? 1.f : alpha;
+    case RGAN_ACT_TANH: return 1.f - a * a;
+    case RGAN_ACT_SIGMOID: return a * (1.f - a);
+    case RGAN_ACT_SELU: {
+      const float scale = 1.0507009873554804934193349852946f;
+      const float sa = 1.7580993408473768599402175208123f;  // scale * alpha
+      return a > 0.f ? scale : a + sa;
+    }
+    default: return 1.f;
+  }
+}
+
+// derivative of act expressed through the activation INPUT x
+__device__ __forceinline__ float act_grad_from_in(float x, int act, float alpha) {
+  switch (act) {
+    case RGAN_ACT_RELU: return x > 0.f ? 1.f : 0.f;
+    case RGAN_ACT_LRELU: return x > 0.f ? 1.f : alpha;
+    case RGAN_ACT_TANH: { float t = tanhf(x); return 1.f - t * t; }
+    case RGAN_ACT_SIGMOID: { float s = 1.f / (1.f + expf(-x)); return s * (1.f - s); }
+    case RGAN_ACT_SELU: {
+      const float scale = 1.0507009873554804934193349852946f;
+      const float sa = 1.7580993408473768599402175208123f;
+      return x > 0.f ? scale : sa * expf(x);
+    }
+    default: return 1.f;
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide sum (blockDim.x multiple of 64, <= 1024).  `red` >= 16 floats of LDS.
+// Result valid in every thread.  Fixed order: deterministic.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum_d(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+}  // namespace rgan

@@ -1,0 +1,894 @@
+// Implicit-GEMM convolutions on fp32 MFMA (v_mfma_f32_32x32x2_f32) for gfx950.
+//
+// Replaces torch.nn.Conv2d / ConvTranspose2d forward and aten::convolution_backward
+// on the reference's hot path (GLI:336,361,387,410,428,448; arch 1 GLI:202-223,260-302).
+//
+// Three GEMM modes, one kernel template:
+//   MODE_CONV   C[m][n] = sum_k im2col(x)[m][k] * Wp[k][n]       (Conv2d fwd, ConvT dgrad,
+//               stride-1 ConvT fwd / Conv dgrad with a flipped kernel, 1x1 "GEMM" layers)
+//   MODE_CONVT2 the same per output phase (oh%2, ow%2) of a k4 s2 p1 ConvTranspose2d
+//               (ConvT fwd, Conv dgrad): 4 sub-pixel GEMMs with K = 4*Cin, no zero taps
+//   MODE_WGRAD  C[m][n] = sum_p G[p][m] * im2col(img)[p][n]       (weight gradients)
+// Activations are NHWC (torch channels_last) inside the path; any (b,c,h,w) strides are
+// accepted (NCHW images at the boundary take the scalar gather).  fp32 in, fp32 MFMA
+// accumulate: no reduced precision anywhere.
+//
+// Tiling: 256 threads = 4 waves; block tile BM x BN x BK(32); each wave owns a
+// (BM/WM) x (BN/WN) sub-tile of 32x32 MFMA accumulators.  LDS is double buffered with
+// register-staged global loads (next tile's loads in flight while the current tile's
+// MFMAs run).  LDS images keep every MFMA operand read a conflict-free ds_read_b32:
+// m-major tiles use row stride BK+1, k-major tiles BM+4 / BN+4.  Split-K writes fp32
+// slabs reduced in fixed order (deterministic) by splitk_reduce.
+#include "common.h"
+
+namespace rgan {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+enum { MODE_CONV = 0, MODE_CONVT2 = 1, MODE_WGRAD = 2 };
+constexpr int BK = 32;
+
+// n / d for 0 <= n < 2^31 via multiply-high (host-computed magic numbers)
+struct FastDiv {
+  uint32_t d, m, l;
+  FastDiv() = default;
+  explicit FastDiv(uint32_t div) {
+    d = div;
+    l = 0;
+    while ((1u << l) < d) ++l;
+    uint64_t one = 1;
+    m = (uint32_t)(((one << 32) * ((one << l) - d)) / d + 1);
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    uint32_t hi = __umulhi(n, m);
+    return (uint32_t)(((uint64_t)hi + n) >> l);
+  }
+};
+
+struct Img {
+  const float* p;
+  long long sb, sc, sh, sw;
+  int H, W, C;
+};
+
+struct OutMap {
+  FastDiv fgw, fghw;      // row m -> (b, i, j) over (gh, gw)
+  int step;
+  long long sb, sh, sw;
+  FastDiv fnc, fnkw;      // col n -> (nh, nw, c) over (nkh, nkw, nc)
+  long long th, tw, tc;
+};
+
+struct GemmArgs {
+  int M, N, K;
+  int ksplit, splits, tiles_n;
+  Img a;                  // CONV/CONVT2: x.  WGRAD: gradient image (channel = m)
+  Img im;                 // WGRAD: image expanded by im2col
+  int KH, KW, stride, pad;
+  FastDiv fgw, fghw;      // decomposition of m (CONV/CONVT2) or p (WGRAD)
+  FastDiv fC, fKW;        // k (CONV/CONVT2) or n (WGRAD) -> (kh, kw, ci)
+  const float* Bw;        // packed weights [phase][K][N]
+  float* C;
+  OutMap out;
+  const float* bias;
+  int act;
+  float alpha;
+  float* slab;
+};
+
+__device__ __forceinline__ long long row_offset(const OutMap& o, int m, int phase) {
+  uint32_t b = o.fghw.div(m);
+  uint32_t rem = m - b * o.fghw.d;
+  uint32_t i = o.fgw.div(rem);
+  uint32_t j = rem - i * o.fgw.d;
+  int ph = phase >> 1, pw = phase & 1;
+  return (long long)b * o.sb + (long long)(i * o.step + ph) * o.sh + (long long)(j * o.step + pw) * o.sw;
+}
+
+__device__ __forceinline__ long long col_offset(const OutMap& o, int n) {
+  uint32_t t = o.fnc.div(n);
+  uint32_t c = n - t * o.fnc.d;
+  uint32_t nh = o.fnkw.div(t);
+  uint32_t nw = t - nh * o.fnkw.d;
+  return (long long)nh * o.th + (long long)nw * o.tw + (long long)c * o.tc;
+}
+
+template <int MODE, int BM, int BN, int WM, int WN, bool AV, bool BV>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
+  constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
+  static_assert(TM >= 1 && TN >= 1 && WM * WN == 4, "tile config");
+  constexpr bool AK = (MODE == MODE_WGRAD);          // A staged k-major
+  constexpr int A_LD = AK ? (BM + 4) : (BK + 1);
+  constexpr int A_SZ = AK ? BK * (BM + 4) : BM * (BK + 1);
+  constexpr int B_LD = BN + 4;
+  constexpr int B_SZ = BK * B_LD;
+  constexpr int STAGE = A_SZ + B_SZ;
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = (wid / WN) * (BM / WM), wn = (wid % WN) * (BN / WN);
+  const int tile = blockIdx.x;
+  const int tm_i = tile / g.tiles_n, tn_i = tile - tm_i * g.tiles_n;
+  const int m0 = tm_i * BM, n0 = tn_i * BN;
+  const int z = blockIdx.z;
+  const int phase = z / g.splits, split = z - phase * g.splits;
+  const int kbeg = split * g.ksplit;
+  const int kend = min(g.K, kbeg + g.ksplit);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+  const int ph = phase >> 1, pw = phase & 1;
+  const float* __restrict__ Bw = g.Bw + (size_t)phase * g.K * g.N;
+
+  // ---------------- per-thread load geometry ----------------
+  // A (CONV/CONVT2, vector): rows (tid>>3)+32i, quad tid&7
+  constexpr int AR = BM / 32;
+  long long abase[(MODE != MODE_WGRAD && AV) ? AR : 1];
+  int aih[(MODE != MODE_WGRAD && AV) ? AR : 1], aiw[(MODE != MODE_WGRAD && AV) ? AR : 1];
+  if constexpr (MODE != MODE_WGRAD && AV) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      int m = m0 + (tid >> 3) + 32 * i;
+      if (m < g.M) {
+        uint32_t b = g.fghw.div(m);
+        uint32_t rem = m - b * g.fghw.d;
+        uint32_t oi = g.fgw.div(rem);
+        uint32_t oj = rem - oi * g.fgw.d;
+        abase[i] = (long long)b * g.a.sb;
+        if constexpr (MODE == MODE_CONV) {
+          aih[i] = (int)oi * g.stride - g.pad;
+          aiw[i] = (int)oj * g.stride - g.pad;
+        } else {
+          aih[i] = (int)oi;
+          aiw[i] = (int)oj;
+        }
+      } else {
+        abase[i] = 0;
+        aih[i] = -(1 << 28);
+        aiw[i] = 0;
+      }
+    }
+  }
+  // WGRAD B (vector): fixed column quad n = n0 + 4*(tid % (BN/4)) -> (kh, kw, ci)
+  int wb_kh = 0, wb_kw = 0, wb_ci = 0;
+  bool wb_nok = false;
+  if constexpr (MODE == MODE_WGRAD && BV) {
+    int n = n0 + 4 * (tid % (BN / 4));
+    wb_nok = n < g.N;
+    uint32_t t = g.fC.div(n);
+    wb_ci = n - t * g.fC.d;
+    wb_kh = g.fKW.div(t);
+    wb_kw = t - wb_kh * g.fKW.d;
+  }
+
+  // register staging
+  constexpr int A_ELEMS = BM * BK / 256;   // floats per thread
+  constexpr int B_ELEMS = BK * BN / 256;
+  float ra[A_ELEMS];
+  float rb[B_ELEMS];
+
+  auto load_tiles = [&](int k0) {
+    // ---------------- A ----------------
+    if constexpr (MODE != MODE_WGRAD) {
+      if constexpr (AV) {
+        const int q = tid & 7;
+        const int k = k0 + 4 * q;
+        int dh = 0, dw = 0, ci = 0;
+        const bool kok = k < kend;
+        if (kok) {
+          uint32_t t = g.fC.div(k);
+          ci = k - t * g.fC.d;
+          if constexpr (MODE == MODE_CONV) {
+            uint32_t kh = g.fKW.div(t);
+            dh = kh;
+            dw = t - kh * g.fKW.d;
+          } else {
+            int th = t >> 1, tw = t & 1;
+            dh = ph - th;
+            dw = pw - tw;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+          int ih = aih[i] + dh, iw = aiw[i] + dw;
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (kok && (unsigned)ih < (unsigned)g.a.H && (unsigned)iw < (unsigned)g.a.W)
+            v = *reinterpret_cast<const float4*>(g.a.p + abase[i] + (long long)ih * g.a.sh +
+                                                 (long long)iw * g.a.sw + ci);
+          ra[4 * i + 0] = v.x; ra[4 * i + 1] = v.y; ra[4 * i + 2] = v.z; ra[4 * i + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < A_ELEMS; ++j) {
+          int e = tid + 256 * j;
+          int row = e >> 5, col = e & 31;
+          int m = m0 + row, k = k0 + col;
+          float v = 0.f;
+          if (m < g.M && k < kend) {
+            uint32_t b = g.fghw.div(m);
+            uint32_t rem = m - b * g.fghw.d;
+            uint32_t oi = g.fgw.div(rem);
+            uint32_t oj = rem - oi * g.fgw.d;
+            uint32_t t = g.fC.div(k);
+            int ci = k - t * g.fC.d;
+            int ih, iw;
+            if constexpr (MODE == MODE_CONV) {
+              uint32_t kh = g.fKW.div(t);
+              ih = (int)oi * g.stride - g.pad + (int)kh;
+              iw = (int)oj * g.stride - g.pad + (int)(t - kh * g.fKW.d);
+            } else {
+              ih = (int)oi + ph - (int)(t >> 1);
+              iw = (int)oj + pw - (int)(t & 1);
+            }
+            if ((unsigned)ih < (unsigned)g.a.H && (unsigned)iw < (unsigned)g.a.W)
+              v = g.a.p[(long long)b * g.a.sb + (long long)ih * g.a.sh + (long long)iw * g.a.sw +
+                        (long long)ci * g.a.sc];
+          }
+          ra[j] = v;
+        }
+      }
+    } else {
+      // WGRAD A: rows p (k dim), cols m (gradient channel)
+      if constexpr (AV) {
+        constexpr int TPR = BM / 4, RPP = 256 / TPR, PASSES = BK / RPP;
+        const int q = tid % TPR, r = tid / TPR;
+        const int m = m0 + 4 * q;
+#pragma unroll
+        for (int i = 0; i < PASSES; ++i) {
+          int p = k0 + r + RPP * i;
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (p < kend && m < g.M) {
+            uint32_t b = g.fghw.div(p);
+            uint32_t rem = p - b * g.fghw.d;
+            uint32_t oi = g.fgw.div(rem);
+            uint32_t oj = rem - oi * g.fgw.d;
+            v = *reinterpret_cast<const float4*>(g.a.p + (long long)b * g.a.sb + (long long)oi * g.a.sh +
+                                                 (long long)oj * g.a.sw + m);
+          }
+          ra[4 * i + 0] = v.x; ra[4 * i + 1] = v.y; ra[4 * i + 2] = v.z; ra[4 * i + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < A_ELEMS; ++j) {
+          int e = tid + 256 * j;
+          int row = e / BM, col = e - (e / BM) * BM;
+          int p = k0 + row, m = m0 + col;
+          float v = 0.f;
+          if (p < kend && m < g.M) {
+            uint32_t b = g.fghw.div(p);
+            uint32_t rem = p - b * g.fghw.d;
+            uint32_t oi = g.fgw.div(rem);
+            uint32_t oj = rem - oi * g.fgw.d;
+            v = g.a.p[(long long)b * g.a.sb + (long long)oi * g.a.sh + (long long)oj * g.a.sw +
+                      (long long)m * g.a.sc];
+          }
+          ra[j] = v;
+        }
+      }
+    }
+    // ---------------- B ----------------
+    if constexpr (MODE != MODE_WGRAD) {
+      if constexpr (BV) {
+        constexpr int TPR = BN / 4, RPP = 256 / TPR, PASSES = BK / RPP;
+        const int q = tid % TPR, r = tid / TPR;
+        const int n = n0 + 4 * q;
+#pragma unroll
+        for (int i = 0; i < PASSES; ++i) {
+          int k = k0 + r + RPP * i;
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (k < kend && n < g.N) v = *reinterpret_cast<const float4*>(Bw + (size_t)k * g.N + n);
+          rb[4 * i + 0] = v.x; rb[4 * i + 1] = v.y; rb[4 * i + 2] = v.z; rb[4 * i + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < B_ELEMS; ++j) {
+          int e = tid + 256 * j;
+          int row = e / BN, col = e - (e / BN) * BN;
+          int k = k0 + row, n = n0 + col;
+          rb[j] = (k < kend && n < g.N) ? Bw[(size_t)k * g.N + n] : 0.f;
+        }
+      }
+    } else {
+      // WGRAD B: im2col(img)[p][n]
+      if constexpr (BV) {
+        constexpr int TPR = BN / 4, RPP = 256 / TPR, PASSES = BK / RPP;
+        const int r = tid / TPR;
+#pragma unroll
+        for (int i = 0; i < PASSES; ++i) {
+          int p = k0 + r + RPP * i;
+          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (p < kend && wb_nok) {
+            uint32_t b = g.fghw.div(p);
+            uint32_t rem = p - b * g.fghw.d;
+            uint32_t oi = g.fgw.div(rem);
+            uint32_t oj = rem - oi * g.fgw.d;
+            int ih = (int)oi * g.stride - g.pad + wb_kh;
+            int iw = (int)oj * g.stride - g.pad + wb_kw;
+            if ((unsigned)ih < (unsigned)g.im.H && (unsigned)iw < (unsigned)g.im.W)
+              v = *reinterpret_cast<const float4*>(g.im.p + (long long)b * g.im.sb + (long long)ih * g.im.sh +
+                                                   (long long)iw * g.im.sw + wb_ci);
+          }
+          rb[4 * i + 0] = v.x; rb[4 * i + 1] = v.y; rb[4 * i + 2] = v.z; rb[4 * i + 3] = v.w;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < B_ELEMS; ++j) {
+          int e = tid + 256 * j;
+          int row = e / BN, col = e - (e / BN) * BN;
+          int p = k0 + row, n = n0 + col;
+          float v = 0.f;
+          if (p < kend && n < g.N) {
+            uint32_t b = g.fghw.div(p);
+            uint32_t rem = p - b * g.fghw.d;
+            uint32_t oi = g.fgw.div(rem);
+            uint32_t oj = rem - oi * g.fgw.d;
+            uint32_t t = g.fC.div(n);
+            int ci = n - t * g.fC.d;
+            uint32_t kh = g.fKW.div(t);
+            int kw = t - kh * g.fKW.d;
+            int ih = (int)oi * g.stride - g.pad + (int)kh;
+            int iw = (int)oj * g.stride - g.pad + kw;
+            if ((unsigned)ih < (unsigned)g.im.H && (unsigned)iw < (unsigned)g.im.W)
+              v = g.im.p[(long long)b * g.im.sb + (long long)ih * g.im.sh + (long long)iw * g.im.sw +
+                         (long long)ci * g.im.sc];
+          }
+          rb[j] = v;
+        }
+      }
+    }
+  };
+
+  auto store_tiles = [&](int buf) {
+    float* As = smem + buf * STAGE;
+    float* Bs = As + A_SZ;
+    if constexpr (MODE != MODE_WGRAD) {
+      if constexpr (AV) {
+        const int q = tid & 7;
+#pragma unroll
+        for (int i = 0; i < AR; ++i) {
+          float* dst = As + ((tid >> 3) + 32 * i) * A_LD + 4 * q;
+          dst[0] = ra[4 * i + 0]; dst[1] = ra[4 * i + 1]; dst[2] = ra[4 * i + 2]; dst[3] = ra[4 * i + 3];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < A_ELEMS; ++j) {
+          int e = tid + 256 * j;
+          As[(e >> 5) * A_LD + (e & 31)] = ra[j];
+        }
+      }
+    } else {
+      if constexpr (AV) {
+        constexpr int TPR = BM / 4, RPP = 256 / TPR, PASSES = BK / RPP;
+        const int q = tid % TPR, r = tid / TPR;
+#pragma unroll
+        for (int i = 0; i < PASSES; ++i)
+          *reinterpret_cast<float4*>(As + (r + RPP * i) * A_LD + 4 * q) =
+              make_float4(ra[4 * i], ra[4 * i + 1], ra[4 * i + 2], ra[4 * i + 3]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < A_ELEMS; ++j) {
+          int e = tid + 256 * j;
+          int row = e / BM;
+          As[row * A_LD + (e - row * BM)] = ra[j];
+        }
+      }
+    }
+    if constexpr (BV) {
+      constexpr int TPR = BN / 4, RPP = 256 / TPR, PASSES = BK / RPP;
+      const int q = tid % TPR, r = tid / TPR;
+#pragma unroll
+      for (int i = 0; i < PASSES; ++i)
+        *reinterpret_cast<float4*>(Bs + (r + RPP * i) * B_LD + 4 * q) =
+            make_float4(rb[4 * i], rb[4 * i + 1], rb[4 * i + 2], rb[4 * i + 3]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < B_ELEMS; ++j) {
+        int e = tid + 256 * j;
+        int row = e / BN;
+        Bs[row * B_LD + (e - row * BN)] = rb[j];
+      }
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (nk > 0) {
+    load_tiles(kbeg);
+    store_tiles(0);
+  }
+  __syncthreads();
+  const int l32 = lane & 31, lk = lane >> 5;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK);
+    const float* As = smem + cur * STAGE;
+    const float* Bs = As + A_SZ;
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      const int k = 2 * kk + lk;
+      float af[TM], bf[TN];
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+        af[t] = AK ? As[k * A_LD + wm + 32 * t + l32] : As[(wm + 32 * t + l32) * A_LD + k];
+#pragma unroll
+      for (int t = 0; t < TN; ++t) bf[t] = Bs[k * B_LD + wn + 32 * t + l32];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_tiles(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------
+  if (g.splits > 1) {
+    float* slab = g.slab + (size_t)z * g.M * g.N;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn + 32 * j + l32;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          if (row < g.M && col < g.N) slab[(size_t)row * g.N + col] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+  long long* moff = reinterpret_cast<long long*>(smem);
+  long long* noff = moff + BM;
+  for (int i = tid; i < BM; i += 256) {
+    int m = m0 + i;
+    moff[i] = m < g.M ? row_offset(g.out, m, MODE == MODE_CONVT2 ? phase : 0) : 0;
+  }
+  for (int i = tid; i < BN; i += 256) {
+    int n = n0 + i;
+    noff[i] = n < g.N ? col_offset(g.out, n) : 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cl = wn + 32 * j + l32;
+      const int col = n0 + cl;
+      const float bv = (g.bias && col < g.N) ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rl = wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (m0 + rl < g.M && col < g.N) {
+          float v = acc[i][j][r] + bv;
+          g.C[moff[rl] + noff[cl]] = act_fwd(v, g.act, g.alpha);
+        }
+      }
+    }
+}
+
+template <int MODE>
+__global__ void splitk_reduce(GemmArgs g, int phases) {
+  const size_t MN = (size_t)g.M * g.N;
+  const size_t total = MN * phases;
+  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (size_t)gridDim.x * blockDim.x) {
+    const int phase = (int)(idx / MN);
+    const size_t e = idx - (size_t)phase * MN;
+    const int m = (int)(e / g.N), n = (int)(e - (size_t)m * g.N);
+    const float* s = g.slab + (size_t)phase * g.splits * MN + e;
+    float v = 0.f;
+    for (int sp = 0; sp < g.splits; ++sp) v += s[(size_t)sp * MN];
+    if (g.bias) v += g.bias[n];
+    g.C[row_offset(g.out, m, MODE == MODE_CONVT2 ? phase : 0) + col_offset(g.out, n)] =
+        act_fwd(v, g.act, g.alpha);
+  }
+}
+
+// ---------------------------------------------------------------- weight packing
+struct PackArgs {
+  const float* W;
+  float* out;
+  const float* scale;
+  int K, N, phases;
+  FastDiv fpci, fpkw;      // k -> (kh, kw, ci)
+  FastDiv fnco, fnkw;      // n -> (nh, nw, co)
+  long long s_in, s_out, s_kh, s_kw;
+  int KH, KW, flip, convt2;
+};
+
+__global__ void pack_weights(PackArgs a) {
+  const size_t KN = (size_t)a.K * a.N, total = KN * a.phases;
+  const float sc = a.scale ? a.scale[0] : 1.f;
+  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (size_t)gridDim.x * blockDim.x) {
+    const int phase = (int)(idx / KN);
+    const size_t e = idx - (size_t)phase * KN;
+    const int k = (int)(e / a.N), n = (int)(e - (size_t)k * a.N);
+    uint32_t t = a.fpci.div(k);
+    const int ci = k - t * a.fpci.d;
+    int kh, kw, co;
+    if (a.convt2) {
+      const int th = t >> 1, tw = t & 1;
+      kh = 2 * th + 1 - (phase >> 1);
+      kw = 2 * tw + 1 - (phase & 1);
+      co = n;
+    } else {
+      uint32_t kkh = a.fpkw.div(t);
+      int kkw = t - kkh * a.fpkw.d;
+      uint32_t tn = a.fnco.div(n);
+      co = n - tn * a.fnco.d;
+      uint32_t nh = a.fnkw.div(tn);
+      int nw = tn - nh * a.fnkw.d;
+      kh = kkh + nh;
+      kw = kkw + nw;
+      if (a.flip) {
+        kh = a.KH - 1 - kh;
+        kw = a.KW - 1 - kw;
+      }
+    }
+    a.out[idx] = a.W[ci * a.s_in + co * a.s_out + kh * a.s_kh + kw * a.s_kw] * sc;
+  }
+}
+
+// ---------------------------------------------------------------- host planning
+enum { CFG_L = 0, CFG_M = 1, CFG_N = 2 };
+
+struct Plan {
+  int mode = MODE_CONV;
+  GemmArgs g{};
+  int phases = 1;
+  int cfg = CFG_L;
+  bool av = false, bv = false;
+  // packing
+  bool pack = false;
+  PackArgs pk{};
+  size_t pack_floats = 0, slab_floats = 0;
+};
+
+static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+static void tile_dims(int cfg, int& bm, int& bn) {
+  bm = cfg == CFG_N ? 256 : 128;
+  bn = cfg == CFG_L ? 128 : (cfg == CFG_M ? 64 : 32);
+}
+
+static void choose_tiling(Plan& p) {
+  GemmArgs& g = p.g;
+  p.cfg = g.N <= 32 ? CFG_N : (g.N <= 64 ? CFG_M : CFG_L);
+  int bm, bn;
+  tile_dims(p.cfg, bm, bn);
+  const int tiles_m = ceil_div(g.M, bm), tiles_n = ceil_div(g.N, bn);
+  g.tiles_n = tiles_n;
+  const long long tiles = (long long)tiles_m * tiles_n * p.phases;
+  const int nk = ceil_div(g.K, BK);
+  int splits = 1;
+  const long long target = 512;  // two resident 256-thread blocks per CU on 256 CUs
+  if (tiles < target) {
+    splits = (int)((target + tiles - 1) / tiles);
+    splits = std::min(splits, std::max(1, nk / 4));
+    splits = std::min(splits, 256);
+    // bound the slab to 256 MiB
+    while (splits > 1 && (size_t)splits * g.M * g.N * p.phases > (size_t)64 << 20) --splits;
+  }
+  const int per = ceil_div(nk, splits);
+  g.ksplit = per * BK;
+  g.splits = ceil_div(g.K, g.ksplit);
+  if (g.splits < 1) g.splits = 1;
+  p.slab_floats = g.splits > 1 ? (size_t)g.splits * g.M * g.N * p.phases : 0;
+}
+
+static OutMap make_out(int gh, int gw, int step, long long sb, long long sh, long long sw, int nkh,
+                       int nkw, int nc, long long th, long long tw, long long tc) {
+  OutMap o;
+  o.fgw = FastDiv(gw);
+  o.fghw = FastDiv((uint32_t)gh * gw);
+  o.step = step;
+  o.sb = sb; o.sh = sh; o.sw = sw;
+  o.fnc = FastDiv(nc);
+  o.fnkw = FastDiv(nkw);
+  (void)nkh;
+  o.th = th; o.tw = tw; o.tc = tc;
+  return o;
+}
+
+static Img make_img(const float* p, int H, int W, int C, const long long* s /* b,c,h,w */) {
+  Img im;
+  im.p = p; im.H = H; im.W = W; im.C = C;
+  im.sb = s[0]; im.sc = s[1]; im.sh = s[2]; im.sw = s[3];
+  return im;
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+static bool vec_img_ok(const Img& im) {
+  return im.sc == 1 && im.C % 4 == 0 && im.sh % 4 == 0 && im.sw % 4 == 0 && im.sb % 4 == 0 &&
+         aligned16(im.p);
+}
+
+static void set_pack(Plan& p, const float* W, const float* scale, int K, int N, int pci, int pkw,
+                     int nco, int nkw, long long s_in, long long s_out, long long s_kh, long long s_kw,
+                     int KH, int KW, int flip, int convt2) {
+  p.pack = true;
+  PackArgs& a = p.pk;
+  a.W = W; a.scale = scale; a.K = K; a.N = N; a.phases = p.phases;
+  a.fpci = FastDiv(pci); a.fpkw = FastDiv(pkw);
+  a.fnco = FastDiv(nco); a.fnkw = FastDiv(nkw);
+  a.s_in = s_in; a.s_out = s_out; a.s_kh = s_kh; a.s_kw = s_kw;
+  a.KH = KH; a.KW = KW; a.flip = flip; a.convt2 = convt2;
+  p.pack_floats = (size_t)K * N * p.phases;
+}
+
+static bool desc_ok(const RganConv* d) {
+  if (!d) return false;
+  if (d->batch <= 0 || d->cin <= 0 || d->cout <= 0 || d->kh <= 0 || d->kw <= 0 || d->stride <= 0 ||
+      d->pad < 0)
+    return false;
+  if (!d->transposed) {
+    if (d->hout != (d->hin + 2 * d->pad - d->kh) / d->stride + 1) return false;
+    if (d->wout != (d->win + 2 * d->pad - d->kw) / d->stride + 1) return false;
+  } else {
+    if (d->hout != (d->hin - 1) * d->stride - 2 * d->pad + d->kh) return false;
+    if (d->wout != (d->win - 1) * d->stride - 2 * d->pad + d->kw) return false;
+  }
+  // 32-bit index space for the GEMM dims
+  if ((long long)d->batch * d->hout * d->wout >= (1LL << 31)) return false;
+  if ((long long)d->batch * d->hin * d->win >= (1LL << 31)) return false;
+  return true;
+}
+
+static bool is_k4s2p1(const RganConv* d) {
+  return d->kh == 4 && d->kw == 4 && d->stride == 2 && d->pad == 1;
+}
+
+// forward GEMM over the conv's input x producing y (conv or transposed conv)
+static int plan_fwd(const RganConv* d, const float* x, const float* w, const float* wscale,
+                    const float* bias, float* y, int act, float alpha, Plan& p) {
+  if (!desc_ok(d)) return RGAN_EINVAL;
+  GemmArgs& g = p.g;
+  const int KK = d->kh * d->kw;
+  g.a = make_img(x, d->hin, d->win, d->cin, d->xs);
+  g.C = y; g.bias = bias; g.act = act; g.alpha = alpha;
+  if (!d->transposed) {
+    p.mode = MODE_CONV;
+    g.M = d->batch * d->hout * d->wout; g.N = d->cout; g.K = KK * d->cin;
+    g.KH = d->kh; g.KW = d->kw; g.stride = d->stride; g.pad = d->pad;
+    g.fgw = FastDiv(d->wout); g.fghw = FastDiv((uint32_t)d->hout * d->wout);
+    g.fC = FastDiv(d->cin); g.fKW = FastDiv(d->kw);
+    g.out = make_out(d->hout, d->wout, 1, d->ys[0], d->ys[2], d->ys[3], 1, 1, d->cout, 0, 0, d->ys[1]);
+    // Wp[(kh,kw,ci)][co] = W[co][ci][kh][kw]
+    set_pack(p, w, wscale, g.K, g.N, d->cin, d->kw, d->cout, 1, KK, (long long)d->cin * KK, d->kw, 1,
+             d->kh, d->kw, 0, 0);
+  } else if (is_k4s2p1(d) && d->hout == 2 * d->hin && d->wout == 2 * d->win) {
+    p.mode = MODE_CONVT2;
+    p.phases = 4;
+    g.M = d->batch * d->hin * d->win; g.N = d->cout; g.K = 4 * d->cin;
+    g.KH = 4; g.KW = 4; g.stride = 2; g.pad = 1;
+    g.fgw = FastDiv(d->win); g.fghw = FastDiv((uint32_t)d->hin * d->win);
+    g.fC = FastDiv(d->cin); g.fKW = FastDiv(2);
+    g.out = make_out(d->hin, d->win, 2, d->ys[0], d->ys[2], d->ys[3], 1, 1, d->cout, 0, 0, d->ys[1]);
+    // ConvT weight [ci][co][kh][kw]
+    set_pack(p, w, wscale, g.K, g.N, d->cin, 2, d->cout, 1, (long long)d->cout * 16, 16, 4, 1, 4, 4, 0, 1);
+  } else if (d->hin == 1 && d->win == 1 && d->stride == 1 && d->pad == 0) {
+    // 1x1 -> kh x kw expansion (G's first layer, GLI:336): plain GEMM, N = (oh, ow, co)
+    p.mode = MODE_CONV;
+    g.M = d->batch; g.N = KK * d->cout; g.K = d->cin;
+    g.KH = 1; g.KW = 1; g.stride = 1; g.pad = 0;
+    g.fgw = FastDiv(1); g.fghw = FastDiv(1);
+    g.fC = FastDiv(d->cin); g.fKW = FastDiv(1);
+    g.out = make_out(1, 1, 1, d->ys[0], 0, 0, d->kh, d->kw, d->cout, d->ys[2], d->ys[3], d->ys[1]);
+    // Wp[ci][(oh,ow,co)] = W[ci][co][oh][ow]
+    set_pack(p, w, wscale, g.K, g.N, d->cin, 1, d->cout, d->kw, (long long)d->cout * KK, KK, d->kw, 1,
+             d->kh, d->kw, 0, 0);
+  } else if (d->stride == 1) {
+    // stride-1 transposed conv == conv with the flipped kernel and pad k-1-p
+    p.mode = MODE_CONV;
+    g.M = d->batch * d->hout * d->wout; g.N = d->cout; g.K = KK * d->cin;
+    g.KH = d->kh; g.KW = d->kw; g.stride = 1; g.pad = d->kh - 1 - d->pad;
+    if (d->kh != d->kw) return RGAN_EINVAL;
+    g.fgw = FastDiv(d->wout); g.fghw = FastDiv((uint32_t)d->hout * d->wout);
+    g.fC = FastDiv(d->cin); g.fKW = FastDiv(d->kw);
+    g.out = make_out(d->hout, d->wout, 1, d->ys[0], d->ys[2], d->ys[3], 1, 1, d->cout, 0, 0, d->ys[1]);
+    set_pack(p, w, wscale, g.K, g.N, d->cin, d->kw, d->cout, 1, (long long)d->cout * KK, KK, d->kw, 1,
+             d->kh, d->kw, 1, 0);
+  } else {
+    return RGAN_EINVAL;
+  }
+  p.av = vec_img_ok(g.a);
+  p.bv = g.N % 4 == 0;
+  choose_tiling(p);
+  return 0;
+}
+
+// data gradient: input dy (cout, hout, wout) -> dx (cin, hin, win)
+static int plan_dgrad(const RganConv* d, const float* dy, const float* w, const float* wscale,
+                      float* dx, Plan& p) {
+  if (!desc_ok(d)) return RGAN_EINVAL;
+  GemmArgs& g = p.g;
+  const int KK = d->kh * d->kw;
+  g.a = make_img(dy, d->hout, d->wout, d->cout, d->ys);
+  g.C = dx; g.bias = nullptr; g.act = RGAN_ACT_NONE; g.alpha = 0.f;
+  g.out = make_out(d->hin, d->win, 1, d->xs[0], d->xs[2], d->xs[3], 1, 1, d->cin, 0, 0, d->xs[1]);
+  if (!d->transposed) {
+    if (is_k4s2p1(d) && d->hin == 2 * d->hout && d->win == 2 * d->wout) {
+      p.mode = MODE_CONVT2;
+      p.phases = 4;
+      g.M = d->batch * d->hout * d->wout; g.N = d->cin; g.K = 4 * d->cout;
+      g.KH = 4; g.KW = 4; g.stride = 2; g.pad = 1;
+      g.fgw = FastDiv(d->wout); g.fghw = FastDiv((uint32_t)d->hout * d->wout);
+      g.fC = FastDiv(d->cout); g.fKW = FastDiv(2);
+      g.out = make_out(d->hout, d->wout, 2, d->xs[0], d->xs[2], d->xs[3], 1, 1, d->cin, 0, 0, d->xs[1]);
+      // W[co][ci][kh][kw] read as a ConvT weight [in=co][out=ci]
+      set_pack(p, w, wscale, g.K, g.N, d->cout, 2, d->cin, 1, (long long)d->cin * 16, 16, 4, 1, 4, 4, 0, 1);
+    } else if (d->stride == 1 && d->kh == d->kw) {
+      p.mode = MODE_CONV;
+      g.M = d->batch * d->hin * d->win; g.N = d->cin; g.K = KK * d->cout;
+      g.KH = d->kh; g.KW = d->kw; g.stride = 1; g.pad = d->kh - 1 - d->pad;
+      g.fgw = FastDiv(d->win); g.fghw = FastDiv((uint32_t)d->hin * d->win);
+      g.fC = FastDiv(d->cout); g.fKW = FastDiv(d->kw);
+      // Wp[(kh,kw,co)][ci] = W[co][ci][k-1-kh][k-1-kw]
+      set_pack(p, w, wscale, g.K, g.N, d->cout, d->kw, d->cin, 1, (long long)d->cin * KK, KK, d->kw, 1,
+               d->kh, d->kw, 1, 0);
+    } else {
+      return RGAN_EINVAL;
+    }
+  } else {
+    // transposed conv's dgrad is the direct conv (same k, s, p) with W[ci][co] as [out=ci][in=co]
+    p.mode = MODE_CONV;
+    g.M = d->batch * d->hin * d->win; g.N = d->cin; g.K = KK * d->cout;
+    g.KH = d->kh; g.KW = d->kw; g.stride = d->stride; g.pad = d->pad;
+    g.fgw = FastDiv(d->win); g.fghw = FastDiv((uint32_t)d->hin * d->win);
+    g.fC = FastDiv(d->cout); g.fKW = FastDiv(d->kw);
+    set_pack(p, w, wscale, g.K, g.N, d->cout, d->kw, d->cin, 1, KK, (long long)d->cout * KK, d->kw, 1,
+             d->kh, d->kw, 0, 0);
+  }
+  p.av = vec_img_ok(g.a);
+  p.bv = g.N % 4 == 0;
+  choose_tiling(p);
+  return 0;
+}
+
+// weight gradient, written in torch weight layout
+static int plan_wgrad(const RganConv* d, const float* x, const float* dy, float* dw, Plan& p) {
+  if (!desc_ok(d)) return RGAN_EINVAL;
+  GemmArgs& g = p.g;
+  const int KK = d->kh * d->kw;
+  p.mode = MODE_WGRAD;
+  g.KH = d->kh; g.KW = d->kw; g.stride = d->stride; g.pad = d->pad;
+  g.C = dw; g.bias = nullptr; g.act = RGAN_ACT_NONE; g.alpha = 0.f;
+  if (!d->transposed) {
+    // C[co][(kh,kw,ci)] = sum_p dy[p][co] * im2col(x)[p][(kh,kw,ci)]
+    g.a = make_img(dy, d->hout, d->wout, d->cout, d->ys);
+    g.im = make_img(x, d->hin, d->win, d->cin, d->xs);
+    g.M = d->cout; g.N = KK * d->cin; g.K = d->batch * d->hout * d->wout;
+    g.fgw = FastDiv(d->wout); g.fghw = FastDiv((uint32_t)d->hout * d->wout);
+    g.fC = FastDiv(d->cin); g.fKW = FastDiv(d->kw);
+    g.out = make_out(1, 1, 1, (long long)d->cin * KK, 0, 0, d->kh, d->kw, d->cin, d->kw, 1, KK);
+  } else {
+    // ConvT weight [ci][co][kh][kw]: the adjoint conv maps dy (hout) -> x (hin)
+    g.a = make_img(x, d->hin, d->win, d->cin, d->xs);
+    g.im = make_img(dy, d->hout, d->wout, d->cout, d->ys);
+    g.M = d->cin; g.N = KK * d->cout; g.K = d->batch * d->hin * d->win;
+    g.fgw = FastDiv(d->win); g.fghw = FastDiv((uint32_t)d->hin * d->win);
+    g.fC = FastDiv(d->cout); g.fKW = FastDiv(d->kw);
+    g.out = make_out(1, 1, 1, (long long)d->cout * KK, 0, 0, d->kh, d->kw, d->cout, d->kw, 1, KK);
+  }
+  p.av = g.a.sc == 1 && g.M % 4 == 0 && g.a.sh % 4 == 0 && g.a.sw % 4 == 0 && g.a.sb % 4 == 0 &&
+         aligned16(g.a.p);
+  p.bv = vec_img_ok(g.im);
+  choose_tiling(p);
+  return 0;
+}
+
+static size_t plan_ws_bytes(const Plan& p) {
+  return align_up(p.pack_floats * 4, 256) + align_up(p.slab_floats * 4, 256);
+}
+
+template <int MODE, int BM, int BN, int WM, int WN>
+static void launch_cfg(const Plan& p, dim3 grid, hipStream_t s) {
+  if (p.av && p.bv) gemm_kernel<MODE, BM, BN, WM, WN, true, true><<<grid, 256, 0, s>>>(p.g);
+  else if (p.av) gemm_kernel<MODE, BM, BN, WM, WN, true, false><<<grid, 256, 0, s>>>(p.g);
+  else if (p.bv) gemm_kernel<MODE, BM, BN, WM, WN, false, true><<<grid, 256, 0, s>>>(p.g);
+  else gemm_kernel<MODE, BM, BN, WM, WN, false, false><<<grid, 256, 0, s>>>(p.g);
+}
+
+template <int MODE>
+static void launch_mode(const Plan& p, dim3 grid, hipStream_t s) {
+  switch (p.cfg) {
+    case CFG_L: launch_cfg<MODE, 128, 128, 2, 2>(p, grid, s); break;
+    case CFG_M: launch_cfg<MODE, 128, 64, 2, 2>(p, grid, s); break;
+    default: launch_cfg<MODE, 256, 32, 4, 1>(p, grid, s); break;
+  }
+}
+
+static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
+  if (ws_bytes < plan_ws_bytes(p)) return RGAN_EINVAL;
+  if (p.g.M <= 0 || p.g.N <= 0 || p.g.K <= 0) return RGAN_EINVAL;
+  char* w = (char*)ws;
+  if (p.pack) {
+    if (!ws) return RGAN_EINVAL;
+    p.pk.out = (float*)w;
+    p.g.Bw = p.pk.out;
+    w += align_up(p.pack_floats * 4, 256);
+    const size_t total = p.pack_floats;
+    const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
+    pack_weights<<<blocks, 256, 0, s>>>(p.pk);
+    RGAN_CHECK_LAUNCH();
+  }
+  p.g.slab = p.slab_floats ? (float*)w : nullptr;
+  int bm, bn;
+  tile_dims(p.cfg, bm, bn);
+  dim3 grid(ceil_div(p.g.M, bm) * p.g.tiles_n, 1, p.phases * p.g.splits);
+  switch (p.mode) {
+    case MODE_CONV: launch_mode<MODE_CONV>(p, grid, s); break;
+    case MODE_CONVT2: launch_mode<MODE_CONVT2>(p, grid, s); break;
+    default: launch_mode<MODE_WGRAD>(p, grid, s); break;
+  }
+  RGAN_CHECK_LAUNCH();
+  if (p.g.splits > 1) {
+    const size_t total = (size_t)p.g.M * p.g.N * p.phases;
+    const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
+    switch (p.mode) {
+      case MODE_CONV: splitk_reduce<MODE_CONV><<<blocks, 256, 0, s>>>(p.g, p.phases); break;
+      case MODE_CONVT2: splitk_reduce<MODE_CONVT2><<<blocks, 256, 0, s>>>(p.g, p.phases); break;
+      default: splitk_reduce<MODE_WGRAD><<<blocks, 256, 0, s>>>(p.g, p.phases); break;
+    }
+    RGAN_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+}  // namespace rgan
+
+using namespace rgan;
+
+extern "C" size_t rgan_conv_workspace(const RganConv* d, int which) {
+  Plan p;
+  static const float dummy[4] = {0, 0, 0, 0};
+  int rc;
+  if (which == 0) rc = plan_fwd(d, dummy, dummy, nullptr, nullptr, (float*)dummy, 0, 0.f, p);
+  else if (which == 1) rc = plan_dgrad(d, dummy, dummy, nullptr, (float*)dummy, p);
+  else rc = plan_wgrad(d, dummy, dummy, (float*)dummy, p);
+  if (rc) return 0;
+  return plan_ws_bytes(p) + 256;  // never 0 for a valid descriptor (0 signals "unsupported")
+}
+
+extern "C" int rgan_conv_fwd(const RganConv* d, const float* x, const float* w, const float* wscale,
+                             const float* bias, float* y, int act, float act_alpha, void* ws,
+                             size_t ws_bytes, void* stream) {
+  if (!x || !w || !y) return RGAN_EINVAL;
+  Plan p;
+  int rc = plan_fwd(d, x, w, wscale, bias, y, act, act_alpha, p);
+  if (rc) return rc;
+  return run_plan(p, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* w, const float* wscale,
+                               float* dx, void* ws, size_t ws_bytes, void* stream) {
+  if (!dy || !w || !dx) return RGAN_EINVAL;
+  Plan p;
+  int rc = plan_dgrad(d, dy, w, wscale, dx, p);
+  if (rc) return rc;
+  return run_plan(p, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int rgan_conv_wgrad(const RganConv* d, const float* x, const float* dy, float* dw,
+                               float* dbias, void* ws, size_t ws_bytes, void* stream) {
+  if (!x || !dy || !dw) return RGAN_EINVAL;
+  Plan p;
+  int rc = plan_wgrad(d, x, dy, dw, p);
+  if (rc) return rc;
+  rc = run_plan(p, ws, ws_bytes, (hipStream_t)stream);
+  if (rc) return rc;
+  if (dbias) {
+    // per-output-channel sum of dy: for Conv2d dy has cout channels, for ConvT too
+    const long long P = (long long)d->batch * d->hout * d->wout;
+    if (d->ys[1] != 1 || d->ys[3] != d->cout || d->ys[2] != (long long)d->wout * d->cout) return RGAN_EINVAL;
+    return rgan_channel_sum(dy, P, d->cout, d->cout, 1, dbias, nullptr, stream);
+  }
+  return 0;
+}

@@ -1,0 +1,542 @@
+// Loss heads, gradient penalty, spectral norm, Adam and data movement for gfx950.
+//
+//  * loss heads: the eight --loss_D variants (GLI:481-484, 592-644, 686-709; algebra in
+//    SURVEY Appendix D) as ONE single-workgroup kernel computing loss and dL/dr, dL/df;
+//  * WGAN-GP: interpolation + per-sample norm/penalty and its backward (GLI:646-658);
+//  * spectral norm power iteration and the sigma-gradient correction
+//    (torch/nn/utils/spectral_norm.py:62-139 as reached from GLI:126,334-446);
+//  * fused multi-tensor Adam (torch/optim/adam.py _single_tensor_adam, GLI:529-530,659,712);
+//  * real-batch gather from a dataset resident in HBM (GLI:176-178, 581-583).
+#include "common.h"
+
+namespace rgan {
+
+// ------------------------------------------------------------------ loss heads
+__device__ __forceinline__ float softplus(float x) { return fmaxf(x, 0.f) + log1pf(expf(-fabsf(x))); }
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+// relativistic-average pair (a on r - m_f, b on f - m_r); returns value, writes derivative
+__device__ __forceinline__ float ra_a(int kind, bool gside, float d, float& der) {
+  if (kind == 6) {
+    if (!gside) { der = sigm(d) - 1.f; return softplus(-d); }
+    der = sigm(d); return softplus(d);
+  }
+  if (kind == 7) {
+    const float s = gside ? d + 1.f : d - 1.f;
+    der = 2.f * s; return s * s;
+  }
+  // 8: hinge
+  if (!gside) { const float h = 1.f - d; der = h > 0.f ? -1.f : 0.f; return h > 0.f ? h : 0.f; }
+  const float h = 1.f + d; der = h > 0.f ? 1.f : 0.f; return h > 0.f ? h : 0.f;
+}
+__device__ __forceinline__ float ra_b(int kind, bool gside, float d, float& der) {
+  if (kind == 6) {
+    if (!gside) { der = sigm(d); return softplus(d); }
+    der = sigm(d) - 1.f; return softplus(-d);
+  }
+  if (kind == 7) {
+    const float s = gside ? d - 1.f : d + 1.f;
+    der = 2.f * s; return s * s;
+  }
+  if (!gside) { const float h = 1.f + d; der = h > 0.f ? 1.f : 0.f; return h > 0.f ? h : 0.f; }
+  const float h = 1.f - d; der = h > 0.f ? -1.f : 0.f; return h > 0.f ? h : 0.f;
+}
+
+// heads 1-4 on one tensor t; side 0 D-real, 1 D-fake, 2 G
+__device__ __forceinline__ float single_term(int kind, int side, float t, float& der) {
+  if (kind == 1) {
+    const float y = side == 1 ? 0.f : 1.f;
+    const float lv = y > 0.5f ? fmaxf(logf(t), -100.f) : fmaxf(logf(1.f - t), -100.f);
+    der = (t - y) / fmaxf((1.f - t) * t, 1e-12f);
+    return -lv;
+  }
+  if (kind == 2) {
+    const float s = side == 1 ? t : t - 1.f;
+    der = 2.f * s; return s * s;
+  }
+  if (kind == 3 || (kind == 4 && side == 2)) {
+    const float sg = side == 1 ? 1.f : -1.f;
+    der = sg; return sg * t;
+  }
+  // hinge D
+  if (side == 0) { const float h = 1.f - t; der = h > 0.f ? -1.f : 0.f; return h > 0.f ? h : 0.f; }
+  const float h = 1.f + t; der = h > 0.f ? 1.f : 0.f; return h > 0.f ? h : 0.f;
+}
+
+// phase < 0: everything in one launch (single process).  Otherwise the distributed phases
+// of rgan_loss_head_dist.  One workgroup of 1024 threads.
+__global__ __launch_bounds__(1024) void loss_head_kernel(int kind, int side, int phase, const float* r,
+                                                         const float* f, int n, int n_global,
+                                                         const float* gsum, float* sums, float* loss,
+                                                         float* dr, float* df) {
+  __shared__ float red[16];
+  const int tid = threadIdx.x;
+  const float ng = (float)n_global;
+  if (kind <= 4) {
+    const float* t = side == 0 ? r : f;
+    float* dt = side == 0 ? dr : df;
+    float s = 0.f;
+    for (int i = tid; i < n; i += blockDim.x) {
+      float der;
+      s += single_term(kind, side, t[i], der);
+      if (dt && phase != 0) dt[i] = der / ng;
+    }
+    s = block_sum(s, red);
+    if (tid == 0) {
+      if (phase < 0) loss[0] = s / ng;
+      else if (phase == 0) sums[0] = s;
+      else if (loss) loss[0] = gsum[0] / ng;
+    }
+    return;
+  }
+  if (kind == 5) {
+    // RSGAN: BCEwL(r - f, 1) for D, BCEwL(f - r, 1) for G (elementwise pairs)
+    float s = 0.f;
+    for (int i = tid; i < n; i += blockDim.x) {
+      const float d = side == 2 ? f[i] - r[i] : r[i] - f[i];
+      s += softplus(-d);
+      const float g = (sigm(d) - 1.f) / ng;
+      if (phase != 0) {
+        if (side == 2) { if (df) df[i] = g; if (dr) dr[i] = -g; }
+        else { if (dr) dr[i] = g; if (df) df[i] = -g; }
+      }
+    }
+    s = block_sum(s, red);
+    if (tid == 0) {
+      if (phase < 0) loss[0] = s / ng;
+      else if (phase == 0) sums[0] = s;
+      else if (loss) loss[0] = gsum[0] / ng;
+    }
+    return;
+  }
+  // relativistic average heads 6-8
+  const bool gside = side == 2;
+  float mr, mf;
+  if (phase < 0 || phase == 0) {
+    float sr = 0.f, sf = 0.f;
+    for (int i = tid; i < n; i += blockDim.x) { sr += r[i]; sf += f[i]; }
+    sr = block_sum(sr, red);
+    sf = block_sum(sf, red);
+    if (phase == 0) {
+      if (tid == 0) { sums[0] = sr; sums[1] = sf; }
+      return;
+    }
+    mr = sr / ng; mf = sf / ng;
+  } else {
+    mr = gsum[0] / ng; mf = gsum[1] / ng;
+  }
+  if (phase < 0 || phase == 1) {
+    float sa = 0.f, sb = 0.f, sda = 0.f, sdb = 0.f;
+    for (int i = tid; i < n; i += blockDim.x) {
+      float da, db;
+      sa += ra_a(kind, gside, r[i] - mf, da);
+      sb += ra_b(kind, gside, f[i] - mr, db);
+      sda += da; sdb += db;
+    }
+    sa = block_sum(sa, red); sb = block_sum(sb, red);
+    sda = block_sum(sda, red); sdb = block_sum(sdb, red);
+    if (phase == 1) {
+      if (tid == 0) { sums[0] = sa; sums[1] = sb; sums[2] = sda; sums[3] = sdb; }
+      return;
+    }
+    // single-process: fall through with local == global sums
+    if (tid == 0) loss[0] = (sa / ng + sb / ng) / 2.f;
+    const float inv2 = 0.5f / ng;
+    for (int i = tid; i < n; i += blockDim.x) {
+      float da, db;
+      ra_a(kind, gside, r[i] - mf, da);
+      ra_b(kind, gside, f[i] - mr, db);
+      if (dr) dr[i] = inv2 * (da - sdb / ng);
+      if (df) df[i] = inv2 * (db - sda / ng);
+    }
+    return;
+  }
+  // phase 2: gsum = (sum r, sum f, sum a, sum b, sum a', sum b') global
+  if (tid == 0 && loss) loss[0] = (gsum[2] / ng + gsum[3] / ng) / 2.f;
+  const float inv2 = 0.5f / ng;
+  for (int i = tid; i < n; i += blockDim.x) {
+    float da, db;
+    ra_a(kind, gside, r[i] - mf, da);
+    ra_b(kind, gside, f[i] - mr, db);
+    if (dr) dr[i] = inv2 * (da - gsum[5] / ng);
+    if (df) df[i] = inv2 * (db - gsum[4] / ng);
+  }
+}
+
+static bool head_args_ok(int kind, int side, const float* r, const float* f, int n) {
+  if (kind < 1 || kind > 8 || n <= 0 || n > 65536) return false;
+  if (kind <= 4) return side >= 0 && side <= 2 && (side == 0 ? r != nullptr : f != nullptr);
+  return (side == 0 || side == 2) && r && f;
+}
+
+extern "C" int rgan_loss_head(int kind, int side, const float* r, const float* f, int n, float* loss,
+                              float* dr, float* df, void* stream) {
+  RGAN_REQUIRE(head_args_ok(kind, side, r, f, n) && loss);
+  loss_head_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(kind, side, -1, r, f, n, n, nullptr, nullptr, loss,
+                                                       dr, df);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int rgan_loss_head_dist(int kind, int side, int phase, const float* r, const float* f, int n,
+                                   int n_global, const float* gsum, float* sums, float* loss, float* dr,
+                                   float* df, void* stream) {
+  RGAN_REQUIRE(head_args_ok(kind, side, r, f, n) && n_global >= n && phase >= 0 && phase <= 2);
+  if (kind <= 5) RGAN_REQUIRE(phase != 1);
+  if (phase == 0 || phase == 1) RGAN_REQUIRE(sums != nullptr);
+  if (phase >= 1) RGAN_REQUIRE(gsum != nullptr);
+  loss_head_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(kind, side, phase, r, f, n, n_global, gsum, sums,
+                                                       loss, dr, df);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void scale_kernel(const float* __restrict__ in, const float* __restrict__ sc, long long n,
+                             float* __restrict__ out) {
+  const float s = sc[0];
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
+       i += (long long)gridDim.x * blockDim.x)
+    out[i] = in[i] * s;
+}
+
+static int grid1(long long n) {
+  return (int)std::max<long long>(1, std::min<long long>((n + 255) / 256, 8192));
+}
+
+extern "C" int rgan_scale(const float* in, const float* scale, long long n, float* out, void* stream) {
+  RGAN_REQUIRE(in && scale && out && n >= 0);
+  if (n == 0) return 0;
+  scale_kernel<<<grid1(n), 256, 0, (hipStream_t)stream>>>(in, scale, n, out);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------ gradient penalty
+__global__ void gp_interp_kernel(const float* __restrict__ x, const float* __restrict__ xf,
+                                 const float* __restrict__ u, int batch, long long per, float* __restrict__ xb) {
+  const long long total = (long long)batch * per;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const float uu = u[i / per];
+    xb[i] = x[i] * uu + xf[i] * (1.f - uu);
+  }
+}
+
+extern "C" int rgan_gp_interp(const float* x, const float* xf, const float* u, int batch, long long per,
+                              float* xb, void* stream) {
+  RGAN_REQUIRE(x && xf && u && xb && batch > 0 && per > 0);
+  gp_interp_kernel<<<grid1(batch * per), 256, 0, (hipStream_t)stream>>>(x, xf, u, batch, per, xb);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ __launch_bounds__(1024) void gp_norm_kernel(const float* __restrict__ g, long long per,
+                                                       float* __restrict__ norms) {
+  __shared__ float red[16];
+  const float* gb = g + blockIdx.x * per;
+  float s = 0.f;
+  for (long long i = threadIdx.x; i < per; i += blockDim.x) s += gb[i] * gb[i];
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) norms[blockIdx.x] = sqrtf(s);
+}
+
+__global__ __launch_bounds__(1024) void gp_loss_kernel(const float* __restrict__ norms, int batch, float lam,
+                                                       int n_global, float* loss) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < batch; i += blockDim.x) {
+    const float d = norms[i] - 1.f;
+    s += d * d;
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) loss[0] = lam * (s / (float)n_global);
+}
+
+extern "C" int rgan_gp_penalty(const float* g, int batch, long long per, float lam, int n_global, float* norms,
+                               float* loss, void* stream) {
+  RGAN_REQUIRE(g && norms && loss && batch > 0 && per > 0 && n_global >= batch);
+  hipStream_t s = (hipStream_t)stream;
+  gp_norm_kernel<<<batch, 1024, 0, s>>>(g, per, norms);
+  RGAN_CHECK_LAUNCH();
+  gp_loss_kernel<<<1, 1024, 0, s>>>(norms, batch, lam, n_global, loss);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+__global__ void gp_bwd_kernel(const float* __restrict__ g, const float* __restrict__ norms, int batch,
+                              long long per, float lam, int n_global, const float* gscale,
+                              float* __restrict__ dg) {
+  const long long total = (long long)batch * per;
+  const float gs = gscale ? gscale[0] : 1.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const float nb = norms[i / per];
+    const float coef = nb > 0.f ? gs * lam * 2.f * (nb - 1.f) / (float)n_global / nb : 0.f;
+    dg[i] = coef * g[i];
+  }
+}
+
+extern "C" int rgan_gp_penalty_backward(const float* g, const float* norms, int batch, long long per, float lam,
+                                        int n_global, const float* gscale, float* dg, void* stream) {
+  RGAN_REQUIRE(g && norms && dg && batch > 0 && per > 0 && n_global >= batch);
+  gp_bwd_kernel<<<grid1(batch * per), 256, 0, (hipStream_t)stream>>>(g, norms, batch, per, lam, n_global,
+                                                                     gscale, dg);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------ spectral norm
+// W viewed [rows][cols]; element (r, c) at r*rs + (c / lo)*hs + (c % lo)
+struct SnView {
+  const float* W;
+  int rows, cols, lo;
+  long long rs, hs;
+  __device__ __forceinline__ long long off(int r, int c) const {
+    const int ch = c / lo;
+    return (long long)r * rs + (long long)ch * hs + (c - ch * lo);
+  }
+};
+
+constexpr int SN_RCHUNK = 64;
+
+// partial[k][c] = sum_{r in chunk k} W(r,c) u[r]
+__global__ __launch_bounds__(256) void sn_wtu_kernel(SnView w, const float* __restrict__ u,
+                                                     float* __restrict__ part) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (c >= w.cols) return;
+  const int r0 = k * SN_RCHUNK, r1 = min(w.rows, r0 + SN_RCHUNK);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += w.W[w.off(r, c)] * u[r];
+  part[(size_t)k * w.cols + c] = s;
+}
+
+// v = t / max(||t||, eps), t[c] = sum_k part[k][c]
+__global__ __launch_bounds__(1024) void sn_norm_v_kernel(const float* __restrict__ part, int nchunks, int cols,
+                                                         float eps, float* __restrict__ v, float* __restrict__ t) {
+  __shared__ float red[16];
+  float s = 0.f;
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) {
+    float a = 0.f;
+    for (int k = 0; k < nchunks; ++k) a += part[(size_t)k * cols + c];
+    t[c] = a;
+    s += a * a;
+  }
+  s = block_sum(s, red);
+  const float den = fmaxf(sqrtf(s), eps);
+  __syncthreads();
+  for (int c = threadIdx.x; c < cols; c += blockDim.x) v[c] = t[c] / den;
+}
+
+// w[r] = sum_c W(r,c) v[c]; one wave per row
+__global__ __launch_bounds__(256) void sn_wv_kernel(SnView w, const float* __restrict__ v, float* __restrict__ out) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= w.rows) return;
+  float s = 0.f;
+  for (int c = lane; c < w.cols; c += 64) s += w.W[w.off(row, c)] * v[c];
+  s = wave_sum(s);
+  if (lane == 0) out[row] = s;
+}
+
+// u = w/max(||w||,eps) (if do_iter); sigma = u . w; inv_sigma = 1/sigma
+__global__ __launch_bounds__(1024) void sn_norm_u_kernel(const float* __restrict__ wv, int rows, float eps,
+                                                         int do_iter, float* __restrict__ u,
+                                                         float* __restrict__ inv_sigma) {
+  __shared__ float red[16];
+  float den = 1.f;
+  if (do_iter) {
+    float s = 0.f;
+    for (int r = threadIdx.x; r < rows; r += blockDim.x) s += wv[r] * wv[r];
+    s = block_sum(s, red);
+    den = fmaxf(sqrtf(s), eps);
+    for (int r = threadIdx.x; r < rows; r += blockDim.x) u[r] = wv[r] / den;
+    __syncthreads();
+  }
+  float d = 0.f;
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) d += u[r] * wv[r];
+  d = block_sum(d, red);
+  if (threadIdx.x == 0) inv_sigma[0] = 1.f / d;
+}
+
+static int sn_nchunks(int rows) { return ceil_div(rows, SN_RCHUNK); }
+
+extern "C" size_t rgan_spectral_ws_bytes(int rows, int cols) {
+  return ((size_t)sn_nchunks(rows) * cols + cols + rows + 64) * sizeof(float);
+}
+
+extern "C" int rgan_spectral_power(const float* W, int rows, int cols, long long rs, long long hs, int lo,
+                                   float eps, float* u, float* v, float* inv_sigma, int do_iter, void* ws,
+                                   void* stream) {
+  RGAN_REQUIRE(W && u && v && inv_sigma && ws && rows > 0 && cols > 0 && lo > 0);
+  hipStream_t s = (hipStream_t)stream;
+  SnView w{W, rows, cols, lo, rs, hs};
+  const int nch = sn_nchunks(rows);
+  float* part = (float*)ws;
+  float* t = part + (size_t)nch * cols;
+  float* wv = t + cols;
+  if (do_iter) {
+    sn_wtu_kernel<<<dim3(ceil_div(cols, 256), nch), 256, 0, s>>>(w, u, part);
+    RGAN_CHECK_LAUNCH();
+    sn_norm_v_kernel<<<1, 1024, 0, s>>>(part, nch, cols, eps, v, t);
+    RGAN_CHECK_LAUNCH();
+  }
+  sn_wv_kernel<<<ceil_div(rows, 4), 256, 0, s>>>(w, v, wv);
+  RGAN_CHECK_LAUNCH();
+  sn_norm_u_kernel<<<1, 1024, 0, s>>>(wv, rows, eps, do_iter, u, inv_sigma);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+// <dWeff, W> over the view, per-block partials then one block reduces
+__global__ __launch_bounds__(256) void sn_dot_kernel(SnView w, const float* __restrict__ dWe,
+                                                     float* __restrict__ part) {
+  __shared__ float red[16];
+  const long long total = (long long)w.rows * w.cols;
+  float s = 0.f;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / w.cols), c = (int)(i - (long long)r * w.cols);
+    const long long o = w.off(r, c);
+    s += dWe[o] * w.W[o];
+  }
+  s = block_sum(s, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void sn_bwd_kernel(SnView w, const float* __restrict__ dWe,
+                                                     const float* __restrict__ part, int nparts,
+                                                     const float* __restrict__ u, const float* __restrict__ v,
+                                                     const float* __restrict__ inv_sigma, float* __restrict__ dW) {
+  __shared__ float kk;
+  if (threadIdx.x == 0) {
+    float d = 0.f;
+    for (int i = 0; i < nparts; ++i) d += part[i];
+    const float is = inv_sigma[0];
+    kk = d * is * is;
+  }
+  __syncthreads();
+  const float is = inv_sigma[0], k = kk;
+  const long long total = (long long)w.rows * w.cols;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / w.cols), c = (int)(i - (long long)r * w.cols);
+    const long long o = w.off(r, c);
+    dW[o] = dWe[o] * is - k * u[r] * v[c];
+  }
+}
+
+extern "C" int rgan_spectral_backward(const float* W, const float* dWeff, int rows, int cols, long long rs,
+                                      long long hs, int lo, const float* u, const float* v,
+                                      const float* inv_sigma, float* dW, void* ws, void* stream) {
+  RGAN_REQUIRE(W && dWeff && u && v && inv_sigma && dW && ws && rows > 0 && cols > 0 && lo > 0);
+  hipStream_t s = (hipStream_t)stream;
+  SnView w{W, rows, cols, lo, rs, hs};
+  const long long total = (long long)rows * cols;
+  const int nparts = (int)std::min<long long>(256, (total + 255) / 256);
+  float* part = (float*)ws;
+  sn_dot_kernel<<<nparts, 256, 0, s>>>(w, dWeff, part);
+  RGAN_CHECK_LAUNCH();
+  sn_bwd_kernel<<<grid1(total), 256, 0, s>>>(w, dWeff, part, nparts, u, v, inv_sigma, dW);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------ Adam
+struct AdamTensor {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  long long n;
+};
+constexpr int ADAM_CHUNK = 48;
+struct AdamBatch {
+  AdamTensor t[ADAM_CHUNK];
+};
+
+__global__ void adam_step_inc(float* step) { step[0] += 1.f; }
+
+__global__ __launch_bounds__(256) void adam_kernel(AdamBatch b, const double* __restrict__ hyper,
+                                                   const float* __restrict__ step) {
+  const AdamTensor T = b.t[blockIdx.y];
+  const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
+  const double st = (double)step[0];
+  const double bc1 = 1.0 - pow(b1, st), bc2 = 1.0 - pow(b2, st);
+  const float neg_step = (float)(-(lr / bc1));
+  const float bc2s = (float)sqrt(bc2);
+  const float w = (float)(1.0 - b1);
+  const float fb2 = (float)b2, f1mb2 = (float)(1.0 - b2), feps = (float)eps, fwd = (float)wd;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < T.n;
+       i += (long long)gridDim.x * blockDim.x) {
+    float g = T.g[i];
+    float p = T.p[i];
+    if (wd != 0.0) g = g + fwd * p;
+    float m = T.m[i];
+    const float diff = g - m;
+    m = w < 0.5f ? m + w * diff : g - diff * (1.f - w);
+    float v = T.v[i] * fb2;
+    v = v + f1mb2 * g * g;
+    const float denom = sqrtf(v) / bc2s + feps;
+    p = p + neg_step * (m / denom);
+    T.m[i] = m;
+    T.v[i] = v;
+    T.p[i] = p;
+  }
+}
+
+extern "C" int rgan_adam(int ntensors, float* const* params, const float* const* grads, float* const* exp_avg,
+                         float* const* exp_avg_sq, const long long* numel, const double* hyper, float* step,
+                         void* stream) {
+  RGAN_REQUIRE(ntensors >= 0 && hyper && step);
+  hipStream_t s = (hipStream_t)stream;
+  adam_step_inc<<<1, 1, 0, s>>>(step);
+  RGAN_CHECK_LAUNCH();
+  for (int base = 0; base < ntensors; base += ADAM_CHUNK) {
+    const int cnt = std::min(ADAM_CHUNK, ntensors - base);
+    AdamBatch b{};
+    long long maxn = 1;
+    for (int i = 0; i < cnt; ++i) {
+      const int j = base + i;
+      RGAN_REQUIRE(params[j] && grads[j] && exp_avg[j] && exp_avg_sq[j] && numel[j] >= 0);
+      b.t[i] = AdamTensor{params[j], grads[j], exp_avg[j], exp_avg_sq[j], numel[j]};
+      maxn = std::max(maxn, numel[j]);
+    }
+    const int bx = (int)std::max<long long>(1, std::min<long long>((maxn + 1023) / 1024, 2048));
+    adam_kernel<<<dim3(bx, cnt), 256, 0, s>>>(b, hyper, step);
+    RGAN_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+__global__ void lr_decay_kernel(double* hyper, double gamma) { hyper[0] *= gamma; }
+
+extern "C" int rgan_lr_decay(double* hyper, double gamma, void* stream) {
+  RGAN_REQUIRE(hyper);
+  lr_decay_kernel<<<1, 1, 0, (hipStream_t)stream>>>(hyper, gamma);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------ data movement
+__global__ void gather_kernel(const float* __restrict__ images, const long long* __restrict__ idx, int batch,
+                              long long per, float* __restrict__ out) {
+  const long long total = (long long)batch * per;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long b = i / per, e = i - b * per;
+    out[i] = images[idx[b] * per + e];
+  }
+}
+
+extern "C" int rgan_gather_images(const float* images, const long long* idx, int batch, long long per,
+                                  float* out, void* stream) {
+  RGAN_REQUIRE(images && idx && out && batch > 0 && per > 0);
+  gather_kernel<<<grid1(batch * per), 256, 0, (hipStream_t)stream>>>(images, idx, batch, per, out);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" const char* rgan_version(void) { return "rgan-mi355x 0.1 gfx950 fp32-mfma"; }
+
+}  // namespace rgan

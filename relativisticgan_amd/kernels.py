@@ -1,0 +1,301 @@
+"""Tensor-level wrappers over the C-ABI (no autograd here; see autograd.py).
+
+Every function takes CUDA (HIP) tensors, allocates outputs with torch's caching
+allocator and launches on the current stream.  Internal activations are NHWC
+(torch channels_last strides on a [B, C, H, W] tensor); NCHW tensors are accepted
+wherever the reference hands them over (images into D, out of G).
+"""
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from . import _lib as L
+
+
+@dataclass(frozen=True)
+class ConvGeom:
+    """One conv layer as the reference declares it (k, stride, pad, transposed)."""
+    k: int
+    stride: int
+    pad: int
+    transposed: bool
+
+    def out_hw(self, h, w):
+        if self.transposed:
+            return ((h - 1) * self.stride - 2 * self.pad + self.k, (w - 1) * self.stride - 2 * self.pad + self.k)
+        return ((h + 2 * self.pad - self.k) // self.stride + 1, (w + 2 * self.pad - self.k) // self.stride + 1)
+
+    def in_hw(self, ho, wo):
+        if self.transposed:
+            return ((ho + 2 * self.pad - self.k) // self.stride + 1, (wo + 2 * self.pad - self.k) // self.stride + 1)
+        return ((ho - 1) * self.stride - 2 * self.pad + self.k, (wo - 1) * self.stride - 2 * self.pad + self.k)
+
+
+def empty_nhwc(B, C, H, W, device):
+    return torch.empty_strided((B, C, H, W), (H * W * C, 1, W * C, C), dtype=torch.float32, device=device)
+
+
+def is_nhwc(t):
+    B, C, H, W = t.shape
+    return t.stride() == (H * W * C, 1, W * C, C) or (H == 1 and W == 1 and t.stride()[1] == 1)
+
+
+def _desc(x_shape, x_stride, y_shape, y_stride, geom):
+    d = L.RganConv()
+    B, cin, hin, win = x_shape
+    _, cout, hout, wout = y_shape
+    d.batch, d.cin, d.hin, d.win = B, cin, hin, win
+    d.cout, d.hout, d.wout = cout, hout, wout
+    d.kh = d.kw = geom.k
+    d.stride, d.pad, d.transposed = geom.stride, geom.pad, int(geom.transposed)
+    for i in range(4):
+        d.xs[i] = x_stride[i]
+        d.ys[i] = y_stride[i]
+    return d
+
+
+def _f32(*ts):
+    for t in ts:
+        if t is not None and t.dtype != torch.float32:
+            raise L.RganError(f"expected float32 tensors, got {t.dtype}")
+
+
+def conv_fwd(x, w, geom, bias=None, act="none", alpha=0.0, wscale=None, out=None, nchw_out=False):
+    """y = act(conv(x, w*wscale) + bias); x [B,Cin,H,W] any strides; w torch layout."""
+    L.require_cuda(x, w, bias, wscale)
+    _f32(x, w, bias)
+    B, cin, H, W = x.shape
+    cout = w.shape[1] if geom.transposed else w.shape[0]
+    Ho, Wo = geom.out_hw(H, W)
+    if out is None:
+        out = (torch.empty((B, cout, Ho, Wo), dtype=torch.float32, device=x.device) if nchw_out
+               else empty_nhwc(B, cout, Ho, Wo, x.device))
+    d = _desc(x.shape, x.stride(), out.shape, out.stride(), geom)
+    lib = L.lib()
+    nbytes = lib.rgan_conv_workspace(ctypes.byref(d), 0)
+    if nbytes == 0:
+        raise L.RganError(f"unsupported conv {geom} for input {tuple(x.shape)}")
+    ws = L.workspace(nbytes, x.device)
+    L.check(lib.rgan_conv_fwd(ctypes.byref(d), L.ptr(x), L.ptr(w), L.ptr(wscale), L.ptr(bias), L.ptr(out),
+                              L.ACT[act], float(alpha), L.ptr(ws), ws.numel(), L.stream()), "rgan_conv_fwd")
+    return out
+
+
+def conv_dgrad(dy, w, geom, x_shape, wscale=None, out=None, like=None):
+    """dx of the conv (input grad), NHWC unless `like` (a tensor whose strides to copy) is given."""
+    L.require_cuda(dy, w, wscale)
+    _f32(dy, w)
+    B, cin, H, W = x_shape
+    if out is None:
+        if like is not None and not is_nhwc(like):
+            out = torch.empty(x_shape, dtype=torch.float32, device=dy.device)
+        else:
+            out = empty_nhwc(B, cin, H, W, dy.device)
+    d = _desc(out.shape, out.stride(), dy.shape, dy.stride(), geom)
+    lib = L.lib()
+    nbytes = lib.rgan_conv_workspace(ctypes.byref(d), 1)
+    if nbytes == 0:
+        raise L.RganError(f"unsupported conv dgrad {geom} for {tuple(x_shape)}")
+    ws = L.workspace(nbytes, dy.device)
+    L.check(lib.rgan_conv_dgrad(ctypes.byref(d), L.ptr(dy), L.ptr(w), L.ptr(wscale), L.ptr(out), L.ptr(ws),
+                                ws.numel(), L.stream()), "rgan_conv_dgrad")
+    return out
+
+
+def conv_wgrad(x, dy, geom, w_shape, with_bias=False):
+    """(dw in torch layout, dbias or None)."""
+    L.require_cuda(x, dy)
+    _f32(x, dy)
+    dw = torch.empty(w_shape, dtype=torch.float32, device=x.device)
+    db = None
+    if with_bias:
+        db = torch.empty(dy.shape[1], dtype=torch.float32, device=x.device)
+        if not is_nhwc(dy):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+    d = _desc(x.shape, x.stride(), dy.shape, dy.stride(), geom)
+    lib = L.lib()
+    nbytes = lib.rgan_conv_workspace(ctypes.byref(d), 2)
+    if nbytes == 0:
+        raise L.RganError(f"unsupported conv wgrad {geom} for {tuple(x.shape)}")
+    ws = L.workspace(nbytes, x.device)
+    L.check(lib.rgan_conv_wgrad(ctypes.byref(d), L.ptr(x), L.ptr(dy), L.ptr(dw), L.ptr(db), L.ptr(ws),
+                                ws.numel(), L.stream()), "rgan_conv_wgrad")
+    return dw, db
+
+
+# ------------------------------------------------------------------ BatchNorm
+def _pc(t):
+    """[P][C] view parameters of an NHWC tensor."""
+    B, C, H, W = t.shape
+    if not is_nhwc(t):
+        raise L.RganError("BatchNorm kernels expect NHWC (channels_last) activations")
+    return B * H * W, C, C, 1
+
+
+def bn_stats(y, eps, momentum, running_mean=None, running_var=None, num_batches_tracked=None):
+    """Batch (mean, invstd) as float[2C]; updates running buffers when given."""
+    P, C, sp, sc = _pc(y)
+    lib = L.lib()
+    stats = torch.empty(2 * C, dtype=torch.float32, device=y.device)
+    part = L.workspace(lib.rgan_bn_partial_bytes(P, C), y.device)
+    L.check(lib.rgan_bn_stats(L.ptr(y), P, C, sp, sc, float(eps), float(momentum), L.ptr(running_mean),
+                              L.ptr(running_var), L.ptr(num_batches_tracked), L.ptr(stats), L.ptr(part),
+                              L.stream()), "rgan_bn_stats")
+    return stats
+
+
+def bn_apply(y, stats, gamma, beta, act="none", alpha=0.0, out=None):
+    P, C, sp, sc = _pc(y)
+    if out is None:
+        out = torch.empty_like(y)
+    Pa, Ca, asp, asc = _pc(out)
+    L.check(L.lib().rgan_bn_apply(L.ptr(y), P, C, sp, sc, L.ptr(stats), L.ptr(gamma), L.ptr(beta), L.ACT[act],
+                                  float(alpha), L.ptr(out), asp, asc, L.stream()), "rgan_bn_apply")
+    return out
+
+
+def bn_backward(da, y, stats, gamma, beta, act="none", alpha=0.0, need_affine=True):
+    if not is_nhwc(da):
+        da = da.contiguous(memory_format=torch.channels_last)
+    P, C, sp, sc = _pc(y)
+    _, _, dsp, dsc = _pc(da)
+    dy = torch.empty_like(y)
+    dgamma = torch.empty(C, dtype=torch.float32, device=y.device) if need_affine and gamma is not None else None
+    dbeta = torch.empty(C, dtype=torch.float32, device=y.device) if need_affine and beta is not None else None
+    lib = L.lib()
+    part = L.workspace(lib.rgan_bn_partial_bytes(P, C), y.device)
+    L.check(lib.rgan_bn_backward(L.ptr(da), dsp, dsc, L.ptr(y), P, C, sp, sc, L.ptr(stats), L.ptr(gamma),
+                                 L.ptr(beta), L.ACT[act], float(alpha), L.ptr(dy), sp, sc, L.ptr(dgamma),
+                                 L.ptr(dbeta), L.ptr(part), L.stream()), "rgan_bn_backward")
+    return dy, dgamma, dbeta
+
+
+def act_backward(da, a, act, alpha=0.0):
+    """dx = da * act'(x) from the activation output a (same strides required)."""
+    if da.stride() != a.stride():
+        da = da.contiguous(memory_format=torch.channels_last) if is_nhwc(a) else da.contiguous()
+    dx = torch.empty_like(a)
+    L.check(L.lib().rgan_act_backward(L.ptr(da), L.ptr(a), a.numel(), L.ACT[act], float(alpha), L.ptr(dx),
+                                      L.stream()), "rgan_act_backward")
+    return dx
+
+
+# ------------------------------------------------------------------ loss heads / GP
+def loss_head(kind, side, r, f, need_dr=True, need_df=True):
+    t = r if r is not None else f
+    n = t.numel()
+    loss = torch.empty((), dtype=torch.float32, device=t.device)
+    dr = torch.empty_like(r) if (r is not None and need_dr) else None
+    df = torch.empty_like(f) if (f is not None and need_df) else None
+    L.check(L.lib().rgan_loss_head(int(kind), int(side), L.ptr(r), L.ptr(f), n, L.ptr(loss), L.ptr(dr),
+                                   L.ptr(df), L.stream()), "rgan_loss_head")
+    return loss, dr, df
+
+
+def loss_head_dist(kind, side, phase, r, f, n_global, gsum=None, need_dr=True, need_df=True):
+    t = r if r is not None else f
+    n = t.numel()
+    sums = torch.zeros(4, dtype=torch.float32, device=t.device)
+    loss = torch.empty((), dtype=torch.float32, device=t.device)
+    dr = torch.empty_like(r) if (phase == 2 and r is not None and need_dr) else None
+    df = torch.empty_like(f) if (phase == 2 and f is not None and need_df) else None
+    L.check(L.lib().rgan_loss_head_dist(int(kind), int(side), int(phase), L.ptr(r), L.ptr(f), n, int(n_global),
+                                        L.ptr(gsum), L.ptr(sums), L.ptr(loss), L.ptr(dr), L.ptr(df), L.stream()),
+            "rgan_loss_head_dist")
+    return sums, loss, dr, df
+
+
+def scale(t, s):
+    out = torch.empty_like(t)
+    L.check(L.lib().rgan_scale(L.ptr(t), L.ptr(s), t.numel(), L.ptr(out), L.stream()), "rgan_scale")
+    return out
+
+
+def gp_interp(x, xf, u):
+    B = x.shape[0]
+    x = x.contiguous()
+    xf = xf.contiguous()
+    out = torch.empty_like(x)
+    L.check(L.lib().rgan_gp_interp(L.ptr(x), L.ptr(xf), L.ptr(u.contiguous()), B, x[0].numel(), L.ptr(out),
+                                   L.stream()), "rgan_gp_interp")
+    return out
+
+
+def gp_penalty(g, lam, n_global):
+    g = g.contiguous()
+    B = g.shape[0]
+    norms = torch.empty(B, dtype=torch.float32, device=g.device)
+    loss = torch.empty((), dtype=torch.float32, device=g.device)
+    L.check(L.lib().rgan_gp_penalty(L.ptr(g), B, g[0].numel(), float(lam), int(n_global), L.ptr(norms),
+                                    L.ptr(loss), L.stream()), "rgan_gp_penalty")
+    return loss, norms, g
+
+
+def gp_penalty_backward(g, norms, lam, n_global, gscale):
+    B = g.shape[0]
+    dg = torch.empty_like(g)
+    L.check(L.lib().rgan_gp_penalty_backward(L.ptr(g), L.ptr(norms), B, g[0].numel(), float(lam), int(n_global),
+                                             L.ptr(gscale), L.ptr(dg), L.stream()), "rgan_gp_penalty_backward")
+    return dg
+
+
+# ------------------------------------------------------------------ spectral norm
+def sn_view(w, transposed):
+    """(rows, cols, rs, hs, lo) of torch's reshape_weight_to_matrix (dim 0 conv, dim 1 convT)."""
+    if w.dim() == 2:
+        w = w.view(w.shape[0], w.shape[1], 1, 1)
+    a, b, kh, kw = w.shape
+    kk = kh * kw
+    if transposed:  # [cin][cout][kh][kw] -> rows = cout
+        return b, a * kk, kk, b * kk, kk
+    return a, b * kk, b * kk, kk, kk
+
+
+def spectral_power(w, u, v, transposed, eps=1e-12, do_iter=True):
+    rows, cols, rs, hs, lo = sn_view(w, transposed)
+    lib = L.lib()
+    inv_sigma = torch.empty(1, dtype=torch.float32, device=w.device)
+    ws = L.workspace(lib.rgan_spectral_ws_bytes(rows, cols), w.device)
+    L.check(lib.rgan_spectral_power(L.ptr(w), rows, cols, rs, hs, lo, float(eps), L.ptr(u), L.ptr(v),
+                                     L.ptr(inv_sigma), int(bool(do_iter)), L.ptr(ws), L.stream()),
+            "rgan_spectral_power")
+    return inv_sigma
+
+
+def spectral_backward(w, dw_eff, u, v, inv_sigma, transposed):
+    rows, cols, rs, hs, lo = sn_view(w, transposed)
+    dw = torch.empty_like(w)
+    ws = L.workspace(4096, w.device)
+    L.check(L.lib().rgan_spectral_backward(L.ptr(w), L.ptr(dw_eff), rows, cols, rs, hs, lo, L.ptr(u), L.ptr(v),
+                                           L.ptr(inv_sigma), L.ptr(dw), L.ptr(ws), L.stream()),
+            "rgan_spectral_backward")
+    return dw
+
+
+# ------------------------------------------------------------------ Adam / data
+def adam(params, grads, exp_avgs, exp_avg_sqs, hyper, step):
+    n = len(params)
+    arr = ctypes.c_void_p * max(n, 1)
+    P = arr(*[p.data_ptr() for p in params])
+    G = arr(*[g.data_ptr() for g in grads])
+    M = arr(*[m.data_ptr() for m in exp_avgs])
+    V = arr(*[v.data_ptr() for v in exp_avg_sqs])
+    N = (ctypes.c_longlong * max(n, 1))(*[p.numel() for p in params])
+    L.check(L.lib().rgan_adam(n, ctypes.cast(P, ctypes.c_void_p), ctypes.cast(G, ctypes.c_void_p),
+                              ctypes.cast(M, ctypes.c_void_p), ctypes.cast(V, ctypes.c_void_p),
+                              ctypes.cast(N, ctypes.c_void_p), L.ptr(hyper), L.ptr(step), L.stream()), "rgan_adam")
+
+
+def lr_decay(hyper, gamma):
+    L.check(L.lib().rgan_lr_decay(L.ptr(hyper), float(gamma), L.stream()), "rgan_lr_decay")
+
+
+def gather_images(images, idx, out=None):
+    B = idx.numel()
+    per = images[0].numel()
+    if out is None:
+        out = torch.empty((B,) + tuple(images.shape[1:]), dtype=torch.float32, device=images.device)
+    L.check(L.lib().rgan_gather_images(L.ptr(images), L.ptr(idx), B, per, L.ptr(out), L.stream()),
+            "rgan_gather_images")
+    return out

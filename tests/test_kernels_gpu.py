@@ -1,0 +1,318 @@
+"""Kernel-level numerics: every HIP kernel vs a plain PyTorch reference of the same op.
+
+GPU-only (marked ``gpu``).  References are torch fp64 on the CPU for small shapes and
+torch fp32 on the device (MIOpen/ATen) for the full-size layer shapes of BASELINE's
+configs.  Tolerances are stated per test (fp32 accumulation over K terms).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _nhwc(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+@pytest.fixture(scope="module")
+def K():
+    from relativisticgan_amd import kernels
+    return kernels
+
+
+def _ref_conv(x, w, g, bias=None):
+    x64, w64 = x.double().cpu(), w.double().cpu()
+    b64 = bias.double().cpu() if bias is not None else None
+    if g.transposed:
+        return F.conv_transpose2d(x64, w64, b64, stride=g.stride, padding=g.pad)
+    return F.conv2d(x64, w64, b64, stride=g.stride, padding=g.pad)
+
+
+# (B, cin, cout, H, k, s, p, transposed)
+SMALL = [
+    (2, 8, 16, 16, 4, 2, 1, False),
+    (3, 3, 8, 16, 4, 2, 1, False),      # first D layer, Cin=3 (scalar gather)
+    (2, 16, 8, 8, 4, 2, 1, True),       # ConvT k4s2p1
+    (2, 8, 3, 8, 4, 2, 1, True),        # last G layer, Cout=3
+    (5, 16, 32, 1, 4, 1, 0, True),      # G start 1x1 -> 4x4
+    (5, 32, 1, 4, 4, 1, 0, False),      # D end 4x4 -> 1x1
+    (2, 12, 20, 8, 3, 1, 1, False),     # arch-1 3x3
+    (2, 64, 128, 8, 4, 2, 1, False),
+    (2, 128, 64, 4, 4, 2, 1, True),
+    (7, 20, 36, 10, 4, 2, 1, False),    # ragged sizes
+]
+
+
+@pytest.mark.parametrize("case", SMALL)
+@pytest.mark.parametrize("layout", ["nhwc", "nchw"])
+def test_conv_fwd_dgrad_wgrad_small(K, case, layout):
+    B, cin, cout, H, k, s, p, tr = case
+    g = K.ConvGeom(k, s, p, tr)
+    torch.manual_seed(0)
+    x = torch.randn(B, cin, H, H, device=DEV)
+    w = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k), device=DEV) * 0.1
+    if layout == "nhwc":
+        x = _nhwc(x)
+    y = K.conv_fwd(x, w, g)
+    ref = _ref_conv(x, w, g)
+    assert y.shape == ref.shape
+    assert _rel(y, ref) < 2e-6
+    dy = torch.randn_like(ref, dtype=torch.float32).to(DEV)
+    if layout == "nhwc":
+        dy = _nhwc(dy)
+    x64 = x.double().cpu().requires_grad_(True)
+    w64 = w.double().cpu().requires_grad_(True)
+    out64 = (F.conv_transpose2d if tr else F.conv2d)(x64, w64, stride=s, padding=p)
+    out64.backward(dy.double().cpu())
+    dx = K.conv_dgrad(dy, w, g, x.shape)
+    assert _rel(dx, x64.grad) < 2e-6
+    dw, _ = K.conv_wgrad(x, dy, g, w.shape)
+    assert _rel(dw, w64.grad) < 2e-6
+
+
+def test_conv_bias_act(K):
+    g = K.ConvGeom(3, 1, 1, False)
+    x = _nhwc(torch.randn(2, 12, 8, 8, device=DEV))
+    w = torch.randn(20, 12, 3, 3, device=DEV) * 0.1
+    b = torch.randn(20, device=DEV)
+    for act, fn in [("lrelu", lambda t: F.leaky_relu(t, 0.1)), ("relu", F.relu), ("tanh", torch.tanh),
+                    ("sigmoid", torch.sigmoid), ("selu", F.selu)]:
+        y = K.conv_fwd(x, w, g, bias=b, act=act, alpha=0.1)
+        assert _rel(y, fn(_ref_conv(x, w, g, b))) < 3e-6, act
+    dy = _nhwc(torch.randn(2, 20, 8, 8, device=DEV))
+    _, db = K.conv_wgrad(x, dy, g, w.shape, with_bias=True)
+    assert _rel(db, dy.double().sum((0, 2, 3))) < 1e-6
+
+
+def test_conv_wscale(K):
+    g = K.ConvGeom(4, 2, 1, False)
+    x = _nhwc(torch.randn(2, 8, 8, 8, device=DEV))
+    w = torch.randn(16, 8, 4, 4, device=DEV)
+    s = torch.tensor([0.25], device=DEV)
+    assert _rel(K.conv_fwd(x, w, g, wscale=s), _ref_conv(x, w * 0.25, g)) < 2e-6
+    dy = _nhwc(torch.randn(2, 16, 4, 4, device=DEV))
+    dx = K.conv_dgrad(dy, w, g, x.shape, wscale=s)
+    dx_ref = K.conv_dgrad(dy, w * 0.25, g, x.shape)
+    assert _rel(dx, dx_ref) < 1e-6
+
+
+# full-size layer shapes of C2 (RaSGAN 128^2, B=64, h=128): a few representative ones
+BIG = [
+    (64, 128, 256, 64, 4, 2, 1, False),
+    (64, 1024, 2048, 8, 4, 2, 1, False),
+    (64, 2048, 1024, 4, 4, 2, 1, True),
+    (64, 256, 128, 32, 4, 2, 1, True),
+    (64, 128, 3, 64, 4, 2, 1, True),
+    (64, 3, 128, 128, 4, 2, 1, False),
+    (64, 128, 2048, 1, 4, 1, 0, True),
+    (64, 2048, 1, 4, 4, 1, 0, False),
+]
+
+
+@pytest.mark.parametrize("case", BIG)
+def test_conv_full_size(K, case):
+    B, cin, cout, H, k, s, p, tr = case
+    g = K.ConvGeom(k, s, p, tr)
+    torch.manual_seed(1)
+    x = torch.randn(B, cin, H, H, device=DEV)
+    if cin != 3:
+        x = _nhwc(x)
+    w = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k), device=DEV) * 0.02
+    xr = x.detach().clone().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    with torch.backends.cudnn.flags(enabled=False):
+        ref = (F.conv_transpose2d if tr else F.conv2d)(xr, wr, stride=s, padding=p)
+        dy = torch.randn_like(ref)
+        ref.backward(dy)
+    y = K.conv_fwd(x, w, g)
+    assert _rel(y, ref.detach()) < 2e-5
+    dyk = dy if cout == 3 else _nhwc(dy)
+    assert _rel(K.conv_dgrad(dyk, w, g, x.shape, like=x), xr.grad) < 2e-5
+    assert _rel(K.conv_wgrad(x, dyk, g, w.shape)[0], wr.grad) < 2e-5
+
+
+def _bn_ref(y, gamma, beta, eps=1e-5):
+    y64 = y.double().cpu()
+    mean = y64.mean((0, 2, 3))
+    var = y64.var((0, 2, 3), unbiased=False)
+    xh = (y64 - mean[None, :, None, None]) / torch.sqrt(var + eps)[None, :, None, None]
+    return xh * gamma.double().cpu()[None, :, None, None] + beta.double().cpu()[None, :, None, None], mean, var
+
+
+@pytest.mark.parametrize("shape", [(4, 8, 5, 5), (64, 256, 32, 32), (2, 2048, 4, 4), (3, 3, 1, 1)])
+@pytest.mark.parametrize("act", ["relu", "lrelu", "none", "tanh"])
+def test_batchnorm_train(K, shape, act):
+    torch.manual_seed(2)
+    B, C, H, W = shape
+    y = _nhwc(torch.randn(shape, device=DEV) * 3 + 1.5)
+    gamma = 1 + 0.1 * torch.randn(C, device=DEV)
+    beta = 0.1 * torch.randn(C, device=DEV)
+    rm = torch.zeros(C, device=DEV)
+    rv = torch.ones(C, device=DEV)
+    nbt = torch.zeros((), dtype=torch.long, device=DEV)
+    stats = K.bn_stats(y, 1e-5, 0.1, rm, rv, nbt)
+    a = K.bn_apply(y, stats, gamma, beta, act, 0.2)
+    z, mean, var = _bn_ref(y, gamma, beta)
+    fn = {"relu": F.relu, "lrelu": lambda t: F.leaky_relu(t, 0.2), "none": lambda t: t, "tanh": torch.tanh}[act]
+    assert _rel(a, fn(z)) < 1e-5
+    n = B * H * W
+    assert _rel(rm, 0.1 * mean) < 1e-5
+    assert _rel(rv, 0.9 + 0.1 * var * n / max(n - 1, 1)) < 1e-5
+    assert int(nbt.item()) == 1
+    # backward vs torch autograd in fp64
+    da = _nhwc(torch.randn(shape, device=DEV))
+    y64 = y.double().cpu().requires_grad_(True)
+    g64 = gamma.double().cpu().requires_grad_(True)
+    b64 = beta.double().cpu().requires_grad_(True)
+    out = fn(F.batch_norm(y64, None, None, g64, b64, training=True, eps=1e-5))
+    out.backward(da.double().cpu())
+    dy, dg, db = K.bn_backward(da, y, stats, gamma, beta, act, 0.2)
+    tol = 1e-4 if n == 1 else 2e-5
+    assert _rel(dy, y64.grad) < tol
+    assert _rel(dg, g64.grad) < 2e-5
+    assert _rel(db, b64.grad) < 2e-5
+
+
+def _torch_head(kind, side, r, f):
+    """The reference's expressions (GLI:592-709) in fp64 with torch autograd."""
+    ones = torch.ones_like(r if r is not None else f)
+    zeros = torch.zeros_like(ones)
+    bce, bcel = torch.nn.BCELoss(), torch.nn.BCEWithLogitsLoss()
+    relu = torch.nn.ReLU()
+    if kind <= 4:
+        t = r if side == 0 else f
+        if kind == 1:
+            return bce(t, zeros if side == 1 else ones)
+        if kind == 2:
+            return torch.mean(t ** 2) if side == 1 else torch.mean((t - ones) ** 2)
+        if kind == 3 or side == 2:
+            return torch.mean(t) if side == 1 else -torch.mean(t)
+        return torch.mean(relu(1.0 - t)) if side == 0 else torch.mean(relu(1.0 + t))
+    if kind == 5:
+        return bcel(r - f, ones) if side == 0 else bcel(f - r, ones)
+    if kind == 6:
+        if side == 0:
+            return (bcel(r - torch.mean(f), ones) + bcel(f - torch.mean(r), zeros)) / 2
+        return (bcel(r - torch.mean(f), zeros) + bcel(f - torch.mean(r), ones)) / 2
+    if kind == 7:
+        if side == 0:
+            return (torch.mean((r - torch.mean(f) - ones) ** 2) + torch.mean((f - torch.mean(r) + ones) ** 2)) / 2
+        return (torch.mean((r - torch.mean(f) + ones) ** 2) + torch.mean((f - torch.mean(r) - ones) ** 2)) / 2
+    if side == 0:
+        return (torch.mean(relu(1.0 - (r - torch.mean(f)))) + torch.mean(relu(1.0 + (f - torch.mean(r))))) / 2
+    return (torch.mean(relu(1.0 + (r - torch.mean(f)))) + torch.mean(relu(1.0 - (f - torch.mean(r))))) / 2
+
+
+HEAD_CASES = [(k, s) for k in (1, 2, 3, 4) for s in (0, 1, 2)] + [(k, s) for k in (5, 6, 7, 8) for s in (0, 2)]
+
+
+@pytest.mark.parametrize("kind,side", HEAD_CASES)
+@pytest.mark.parametrize("n", [1, 8, 64, 3000])
+def test_loss_heads(K, kind, side, n):
+    torch.manual_seed(kind * 10 + side)
+    if kind == 1:
+        r = torch.rand(n, device=DEV) * 0.98 + 0.01
+        f = torch.rand(n, device=DEV) * 0.98 + 0.01
+    else:
+        r = torch.randn(n, device=DEV) * 2
+        f = torch.randn(n, device=DEV) * 2
+    needs_r = kind > 4 or side == 0
+    needs_f = kind > 4 or side != 0
+    loss, dr, df = K.loss_head(kind, side, r if needs_r else None, f if needs_f else None)
+    r64 = r.double().cpu().requires_grad_(True)
+    f64 = f.double().cpu().requires_grad_(True)
+    ref = _torch_head(kind, side, r64 if needs_r else None, f64 if needs_f else None)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) <= 1e-5 * max(1.0, abs(ref.item()))
+    if needs_r:
+        assert _rel(dr, r64.grad) < 1e-5 or r64.grad.abs().max() < 1e-12
+    if needs_f:
+        assert _rel(df, f64.grad) < 1e-5 or f64.grad.abs().max() < 1e-12
+
+
+def test_gp_kernels(K):
+    torch.manual_seed(3)
+    x = torch.randn(8, 3, 16, 16, device=DEV)
+    xf = torch.randn(8, 3, 16, 16, device=DEV)
+    u = torch.rand(8, 1, 1, 1, device=DEV)
+    xb = K.gp_interp(x, xf, u)
+    assert _rel(xb, x * u + xf * (1 - u)) < 1e-6
+    g = torch.randn(8, 3, 16, 16, device=DEV)
+    loss, norms, gc = K.gp_penalty(g, 10.0, 8)
+    g64 = g.double().cpu().requires_grad_(True)
+    ref = 10.0 * ((g64.norm(2, 1).norm(2, 1).norm(2, 1) - 1) ** 2).mean()
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-5 * ref.item()
+    one = torch.ones((), device=DEV)
+    dg = K.gp_penalty_backward(gc, norms, 10.0, 8, one)
+    assert _rel(dg, g64.grad) < 1e-5
+
+
+@pytest.mark.parametrize("transposed", [False, True])
+def test_spectral_norm(K, transposed):
+    torch.manual_seed(4)
+    conv = (torch.nn.ConvTranspose2d(24, 16, 4, 2, 1, bias=False) if transposed
+            else torch.nn.Conv2d(24, 16, 4, 2, 1, bias=False))
+    sn = torch.nn.utils.spectral_norm(conv)
+    w = sn.weight_orig.detach().to(DEV)
+    u = sn.weight_u.detach().clone().to(DEV)
+    v = sn.weight_v.detach().clone().to(DEV)
+    inv_sigma = K.spectral_power(w, u, v, transposed)
+    # reference: one power iteration in fp64
+    dim = 1 if transposed else 0
+    W = sn.weight_orig.detach().double()
+    if dim == 1:
+        W = W.permute(1, 0, 2, 3)
+    Wm = W.reshape(W.shape[0], -1)
+    u0 = sn.weight_u.double()
+    v1 = F.normalize(Wm.t() @ u0, dim=0, eps=1e-12)
+    u1 = F.normalize(Wm @ v1, dim=0, eps=1e-12)
+    sigma = torch.dot(u1, Wm @ v1)
+    assert _rel(u, u1) < 1e-5 and _rel(v, v1) < 1e-5
+    assert abs(1 / inv_sigma.item() - sigma.item()) < 1e-5 * sigma.item()
+    # backward of W_eff = W / sigma(W) with u, v held constant
+    Wt = sn.weight_orig.detach().double().requires_grad_(True)
+    W2 = Wt.permute(1, 0, 2, 3) if dim == 1 else Wt
+    sig = torch.dot(u1, W2.reshape(W2.shape[0], -1) @ v1)
+    G = torch.randn_like(Wt)
+    (Wt / sig).backward(G)
+    dw = K.spectral_backward(w, G.float().to(DEV), u, v, inv_sigma, transposed)
+    assert _rel(dw, Wt.grad) < 1e-5
+
+
+def test_adam_matches_torch(K):
+    torch.manual_seed(5)
+    shapes = [(64, 3, 4, 4), (128,), (7, 9)]
+    params = [torch.randn(s, device=DEV) for s in shapes]
+    ref = [p.detach().cpu().clone().requires_grad_(True) for p in params]
+    opt = torch.optim.Adam(ref, lr=1e-4, betas=(0.5, 0.999), weight_decay=0.01)
+    m = [torch.zeros_like(p) for p in params]
+    v = [torch.zeros_like(p) for p in params]
+    hyper = torch.tensor([1e-4, 0.5, 0.999, 1e-8, 0.01, 0, 0, 0], dtype=torch.float64, device=DEV)
+    step = torch.zeros(1, device=DEV)
+    for it in range(3):
+        grads = [torch.randn(s, device=DEV) for s in shapes]
+        for r, g in zip(ref, grads):
+            r.grad = g.cpu()
+        opt.step()
+        K.adam(params, grads, m, v, hyper, step)
+    for p, r in zip(params, ref):
+        assert torch.allclose(p.cpu(), r.detach(), rtol=1e-6, atol=1e-7)
+    assert step.item() == 3
+
+
+def test_gather(K):
+    imgs = torch.randn(10, 3, 4, 4, device=DEV)
+    idx = torch.tensor([3, 0, 9], dtype=torch.long, device=DEV)
+    assert torch.equal(K.gather_images(imgs, idx), imgs[idx])
