@@ -79,12 +79,31 @@ int rgan_bn_stats(const float* y, long long P, int C, long long sp, long long sc
 int rgan_bn_apply(const float* y, long long P, int C, long long sp, long long sc,
                   const float* stats, const float* gamma, const float* beta,
                   int act, float act_alpha, float* a, long long asp, long long asc, void* stream);
+/* Staged form for data parallelism (SyncBN): local moments (count, mean, M2) as
+ * float[3][C]; the caller gathers them from all ranks into [nranks][3][C] and merges
+ * in rank order with rgan_bn_finalize (Chan's parallel variance; deterministic). */
+int rgan_bn_moments(const float* y, long long P, int C, long long sp, long long sc,
+                    float* moments, void* partial, void* stream);
+int rgan_bn_finalize(const float* moments, int nranks, int C, float eps, float momentum,
+                     float* running_mean, float* running_var, long long* num_batches_tracked,
+                     float* stats, void* stream);
 /* Backward through act(BN(y)): given da, produce dy, dgamma, dbeta. */
 int rgan_bn_backward(const float* da, long long dsp, long long dsc,
                      const float* y, long long P, int C, long long sp, long long sc,
                      const float* stats, const float* gamma, const float* beta,
                      int act, float act_alpha, float* dy, long long ysp, long long ysc,
                      float* dgamma, float* dbeta, void* partial, void* stream);
+/* Staged backward: local sums[2][C] = (sum g, sum g*(y-mean)), g = da*act'; the caller
+ * all-reduces them over ranks, then apply with the global pixel count P_global. */
+int rgan_bn_backward_sums(const float* da, long long dsp, long long dsc, const float* y,
+                          long long P, int C, long long sp, long long sc, const float* stats,
+                          const float* gamma, const float* beta, int act, float act_alpha,
+                          float* sums, void* partial, void* stream);
+int rgan_bn_backward_apply(const float* da, long long dsp, long long dsc, const float* y,
+                           long long P, int C, long long sp, long long sc, const float* stats,
+                           const float* gamma, const float* beta, int act, float act_alpha,
+                           const float* sums, long long P_global, float* dy, long long ysp,
+                           long long ysc, float* dgamma, float* dbeta, void* stream);
 
 /* ---- elementwise ---- */
 /* dx = da * act'(a) where a = act(x) is the saved activation output. */
@@ -154,6 +173,15 @@ int rgan_lr_decay(double* hyper, double gamma, void* stream);
  * GLI:176-178, 581-583, on a dataset resident in HBM). */
 int rgan_gather_images(const float* images, const long long* idx, int batch, long long per,
                        float* out, void* stream);
+
+/* ---- live launch timing (bench.py roofline) ----
+ * rgan_profile_begin(capacity): bracket each subsequent conv GEMM launch with HIP events
+ * on its stream (up to `capacity` launches).  rgan_profile_end: wait, stop, return
+ * summed GEMM time, summed algorithmic FLOPs (2*B*Cin*Cout*k*k*pixels per conv op) and
+ * the launch count.  rgan_profile_kernel(i in [0,36)): the same per kernel symbol. */
+int rgan_profile_begin(int capacity);
+int rgan_profile_end(double* total_ms, double* total_flops, long long* launches);
+int rgan_profile_kernel(int idx, char* name, int name_len, double* ms, double* flops, long long* n);
 
 /* Library self-description: number of exported compute entry points, version string. */
 const char* rgan_version(void);

@@ -370,7 +370,9 @@ class Trainer:
     right after it, mirroring the golden capture points.
     """
 
-    def __init__(self, param, images, hooks=None, seed_all=True):
+    def __init__(self, param, images, hooks=None, seed_all=True, dtype=torch.float32):
+        """``dtype`` != float32 (test envelope only): modules and buffers are cast after the
+        fp32 initialisation, so the same initial values are used at higher precision."""
         self.p = p = param
         self.hooks = hooks
         if seed_all:
@@ -393,6 +395,11 @@ class Trainer:
         self.u = torch.FloatTensor(B, 1, 1, 1)
         self.z_test = torch.FloatTensor(B, p.z_size, 1, 1).normal_(0, 1)
         self.grad_outputs = torch.ones(B)
+        if dtype != torch.float32:
+            self.G.to(dtype)
+            self.D.to(dtype)
+            for name in ("x", "x_fake", "y", "y2", "z", "u", "z_test", "grad_outputs"):
+                setattr(self, name, getattr(self, name).to(dtype))
         self.optD = torch.optim.Adam(self.D.parameters(), lr=p.lr_D, betas=(p.beta1, p.beta2),
                                      weight_decay=p.weight_decay)
         self.optG = torch.optim.Adam(self.G.parameters(), lr=p.lr_G, betas=(p.beta1, p.beta2),
@@ -411,15 +418,18 @@ class Trainer:
             q.requires_grad = flag
 
     # -- one iteration (GLI:560-714)
-    def iteration(self, i):
+    def iteration(self, i, feed=None):
+        """One reference iteration.  ``feed`` (test teacher-forcing only) supplies the
+        random inputs {x_D, z_D, u, z_G, x_G} instead of drawing them."""
         p, D, G = self.p, self.D, self.G
+        draw_real = (lambda key: feed[key]) if feed else (lambda key: self.next_real())
         rec = StepRecord()
         if i % p.print_every == 0:
             G(self.z_test)  # sample image; mutates G's BN running statistics (GLI:564)
         self._set_D_grad(True)
         for _ in range(p.Diters):
             D.zero_grad()
-            real = self.next_real()
+            real = draw_real("x_D")
             B = real.size(0)
             self.x.data.resize_as_(real).copy_(real)
             y_pred = D(self.x)
@@ -427,7 +437,7 @@ class Trainer:
                 self.y.data.resize_(B).fill_(1)
                 err_real = head_real(p.loss_D, y_pred, self.y)
                 err_real.backward()
-                self.z.data.resize_(B, p.z_size, 1, 1).normal_(0, 1)
+                self._draw_z(B, feed, "z_D")
                 fake = G(self.z)
                 self.x_fake.data.resize_(fake.data.size()).copy_(fake.data)
                 self.y.data.resize_(B).fill_(0)
@@ -438,7 +448,7 @@ class Trainer:
             else:
                 self.y.data.resize_(B).fill_(1)
                 self.y2.data.resize_(B).fill_(0)
-                self.z.data.resize_(B, p.z_size, 1, 1).normal_(0, 1)
+                self._draw_z(B, feed, "z_D")
                 fake = G(self.z)
                 self.x_fake.data.resize_(fake.data.size()).copy_(fake.data)
                 y_pred_fake = D(self.x_fake.detach())
@@ -448,7 +458,10 @@ class Trainer:
                          y_pred_fake=y_pred_fake.detach(), errD=errD.detach())
             if p.loss_D == 3 or p.grad_penalty:
                 self.u.data.resize_(B, 1, 1, 1)
-                self.u.uniform_(0, 1)
+                if feed:
+                    self.u.data.copy_(feed["u"])
+                else:
+                    self.u.uniform_(0, 1)
                 gp = gradient_penalty(D, self.x, self.x_fake, self.u, p.penalty, self.grad_outputs)
                 gp.backward()
                 rec.D.update(u=self.u.clone(), gp=gp.detach())
@@ -462,12 +475,12 @@ class Trainer:
         for _ in range(p.Giters):
             G.zero_grad()
             self.y.data.resize_(B).fill_(1)
-            self.z.data.resize_(B, p.z_size, 1, 1).normal_(0, 1)
+            self._draw_z(B, feed, "z_G")
             fake = G(self.z)
             y_pred_fake = D(fake)
             y_pred = None
             if p.loss_D not in (1, 2, 3, 4):
-                real = self.next_real()
+                real = draw_real("x_G")
                 B = real.size(0)
                 self.x.data.resize_as_(real).copy_(real)
                 if p.loss_D == 6:
@@ -489,6 +502,12 @@ class Trainer:
         self.decayD.step()
         self.decayG.step()
         return rec
+
+    def _draw_z(self, B, feed, key):
+        if feed:
+            self.z.data.resize_(B, self.p.z_size, 1, 1).copy_(feed[key])
+        else:
+            self.z.data.resize_(B, self.p.z_size, 1, 1).normal_(0, 1)
 
     def log_line(self, i, elapsed):
         """The reference's progress line format (GLI:723)."""

@@ -33,6 +33,12 @@ _SIGS = {
     "rgan_conv_wgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "rgan_bn_partial_bytes": (c_sz, [c_ll, c_int]),
     "rgan_bn_stats": (c_int, [c_vp, c_ll, c_int, c_ll, c_ll, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rgan_bn_moments": (c_int, [c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp]),
+    "rgan_bn_finalize": (c_int, [c_vp, c_int, c_int, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rgan_bn_backward_sums": (c_int, [c_vp, c_ll, c_ll, c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp, c_int,
+                                      c_f, c_vp, c_vp, c_vp]),
+    "rgan_bn_backward_apply": (c_int, [c_vp, c_ll, c_ll, c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp, c_int,
+                                       c_f, c_vp, c_ll, c_vp, c_ll, c_ll, c_vp, c_vp, c_vp]),
     "rgan_bn_apply": (c_int, [c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp, c_int, c_f, c_vp, c_ll, c_ll,
                               c_vp]),
     "rgan_bn_backward": (c_int, [c_vp, c_ll, c_ll, c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp, c_int, c_f,
@@ -54,6 +60,9 @@ _SIGS = {
     "rgan_adam": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rgan_lr_decay": (c_int, [c_vp, c_d, c_vp]),
     "rgan_gather_images": (c_int, [c_vp, c_vp, c_int, c_ll, c_vp, c_vp]),
+    "rgan_profile_begin": (c_int, [c_int]),
+    "rgan_profile_end": (c_int, [c_vp, c_vp, c_vp]),
+    "rgan_profile_kernel": (c_int, [c_int, ctypes.c_char_p, c_int, c_vp, c_vp, c_vp]),
     "rgan_version": (ctypes.c_char_p, []),
 }
 

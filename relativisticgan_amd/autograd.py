@@ -1,0 +1,236 @@
+"""Autograd Functions over the HIP kernels.
+
+``ConvLayerFn`` is one fused layer of the reference's Sequentials: Conv2d /
+ConvTranspose2d (+bias) (+BatchNorm2d in train mode) (+activation), optionally with
+spectral norm on the weight (GLI:326-452 arch 0, GLI:190-307 arch 1).  Forward:
+implicit-GEMM conv with the activation fused in the epilogue (no BN) or conv -> BN
+moments -> fused normalise+activation (BN).  Backward: fused act'+BN backward, conv
+dgrad and wgrad GEMMs, spectral sigma correction.
+
+Double backward (WGAN-GP, ``torch.autograd.grad(..., create_graph=True)`` at GLI:655):
+when the backward itself runs with grad mode on, the layer is re-expressed with
+differentiable pieces -- ``ConvPrim``/``ConvDgradPrim``/``ConvWgradPrim`` (HIP GEMMs
+whose backwards are each other, so any order of derivative stays on the MFMA kernels)
+plus torch tensor algebra for the per-channel BN normalisation and the activation --
+and differentiated with ``torch.autograd.grad``; ``gp.backward()`` then runs through
+those pieces.
+"""
+import torch
+import torch.nn.functional as F
+
+from . import dp
+from . import kernels as K
+
+
+class LayerSpec:
+    """Static description of one fused layer."""
+
+    __slots__ = ("geom", "act", "alpha", "bn", "eps", "momentum", "spectral", "nchw_out")
+
+    def __init__(self, geom, act="none", alpha=0.0, bn=False, eps=1e-5, momentum=0.1, spectral=False,
+                 nchw_out=False):
+        self.geom, self.act, self.alpha, self.bn = geom, act, alpha, bn
+        self.eps, self.momentum, self.spectral, self.nchw_out = eps, momentum, spectral, nchw_out
+
+
+# ---------------------------------------------------------------- differentiable conv primitives
+class ConvPrim(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, geom):
+        ctx.geom = geom
+        ctx.save_for_backward(x, w)
+        return K.conv_fwd(x, w, geom)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dx = ConvDgradPrim.apply(dy, w, ctx.geom, tuple(x.shape)) if ctx.needs_input_grad[0] else None
+        dw = ConvWgradPrim.apply(x, dy, ctx.geom, tuple(w.shape)) if ctx.needs_input_grad[1] else None
+        return dx, dw, None
+
+
+class ConvDgradPrim(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, dy, w, geom, x_shape):
+        ctx.geom = geom
+        ctx.save_for_backward(dy, w)
+        return K.conv_dgrad(dy, w, geom, x_shape)
+
+    @staticmethod
+    def backward(ctx, ddx):
+        dy, w = ctx.saved_tensors
+        d_dy = ConvPrim.apply(ddx, w, ctx.geom) if ctx.needs_input_grad[0] else None
+        d_w = ConvWgradPrim.apply(ddx, dy, ctx.geom, tuple(w.shape)) if ctx.needs_input_grad[1] else None
+        return d_dy, d_w, None, None
+
+
+class ConvWgradPrim(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dy, geom, w_shape):
+        ctx.geom = geom
+        ctx.save_for_backward(x, dy)
+        return K.conv_wgrad(x, dy, geom, w_shape)[0]
+
+    @staticmethod
+    def backward(ctx, ddw):
+        x, dy = ctx.saved_tensors
+        d_x = ConvDgradPrim.apply(dy, ddw, ctx.geom, tuple(x.shape)) if ctx.needs_input_grad[0] else None
+        d_dy = ConvPrim.apply(x, ddw, ctx.geom) if ctx.needs_input_grad[1] else None
+        return d_x, d_dy, None, None
+
+
+def _torch_act(t, act, alpha):
+    if act == "relu":
+        return F.relu(t)
+    if act == "lrelu":
+        return F.leaky_relu(t, alpha)
+    if act == "tanh":
+        return torch.tanh(t)
+    if act == "sigmoid":
+        return torch.sigmoid(t)
+    if act == "selu":
+        return F.selu(t)
+    return t
+
+
+def _sn_sigma(w, u, v, transposed):
+    wm = w.permute(1, 0, 2, 3) if (transposed and w.dim() == 4) else w
+    wm = wm.reshape(wm.shape[0], -1)
+    return torch.dot(u, torch.mv(wm, v))
+
+
+def composite_layer(x, w, bias, gamma, beta, spec, stats_mode, sn):
+    """The layer as differentiable pieces (used for create_graph backward)."""
+    if spec.spectral:
+        u, v, _ = sn
+        w = w / _sn_sigma(w, u, v, spec.geom.transposed)
+    y = ConvPrim.apply(x, w, spec.geom)
+    if bias is not None:
+        y = y + bias.view(1, -1, 1, 1)
+    if spec.bn:
+        if stats_mode is None:  # train mode: batch statistics (global batch under SyncBN)
+            if dp.sync_bn():
+                n_loc = torch.tensor([y.shape[0] * y.shape[2] * y.shape[3]], dtype=y.dtype, device=y.device)
+                s = torch.cat([y.sum((0, 2, 3)), n_loc])
+                s = _AllReduceSum.apply(s)
+                mean = (s[:-1] / s[-1]).view(1, -1, 1, 1)
+                c = y - mean
+                q = _AllReduceSum.apply(torch.cat([(c * c).sum((0, 2, 3)), n_loc]))
+                var = (q[:-1] / q[-1]).view(1, -1, 1, 1)
+            else:
+                mean = y.mean((0, 2, 3), keepdim=True)
+                c = y - mean
+                var = (c * c).mean((0, 2, 3), keepdim=True)
+            y = c / torch.sqrt(var + spec.eps)
+        else:
+            mean, invstd = stats_mode
+            y = (y - mean.view(1, -1, 1, 1)) * invstd.view(1, -1, 1, 1)
+        y = y * gamma.view(1, -1, 1, 1) + beta.view(1, -1, 1, 1)
+    return _torch_act(y, spec.act, spec.alpha)
+
+
+class _AllReduceSum(torch.autograd.Function):
+    """Differentiable SUM over ranks (the backward of a sum-all-reduce is a sum-all-reduce)."""
+
+    @staticmethod
+    def forward(ctx, t):
+        return dp.all_reduce_sum(t.clone())
+
+    @staticmethod
+    def backward(ctx, g):
+        return dp.all_reduce_sum(g.clone())
+
+
+# ---------------------------------------------------------------- fused layer
+class ConvLayerFn(torch.autograd.Function):
+    """a = act(BN(conv(x, w_eff) + bias)); see module docstring."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, gamma, beta, spec, bufs, sn):
+        # bufs = (running_mean, running_var, num_batches_tracked, training)
+        # sn   = (u, v, inv_sigma) clones for spectral layers, else None
+        wscale = sn[2] if spec.spectral else None
+        stats_eval = None
+        if spec.bn:
+            y = K.conv_fwd(x, w, spec.geom, bias=bias, wscale=wscale)
+            rm, rv, nbt, training = bufs
+            C = y.shape[1]
+            if training:
+                if dp.sync_bn():
+                    mom = dp.all_gather_cat(K.bn_moments(y))
+                    stats = K.bn_finalize(mom, dp.world(), C, spec.eps, spec.momentum, rm, rv, nbt)
+                else:
+                    stats = K.bn_stats(y, spec.eps, spec.momentum, rm, rv, nbt)
+            else:
+                stats = torch.cat([rm, torch.rsqrt(rv + spec.eps)])
+                stats_eval = (rm, stats[C:])
+            a = K.bn_apply(y, stats, gamma, beta, spec.act, spec.alpha)
+            ctx.save_for_backward(x, w, bias, gamma, beta, y, stats, *(sn if spec.spectral else ()))
+        else:
+            a = K.conv_fwd(x, w, spec.geom, bias=bias, act=spec.act, alpha=spec.alpha, wscale=wscale,
+                           nchw_out=spec.nchw_out)
+            ctx.save_for_backward(x, w, bias, gamma, beta, a, None, *(sn if spec.spectral else ()))
+        ctx.spec = spec
+        ctx.stats_eval = stats_eval
+        ctx.training = bufs[3] if bufs is not None else True
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        spec = ctx.spec
+        saved = ctx.saved_tensors
+        x, w, bias, gamma, beta, t5, stats = saved[:7]
+        sn = saved[7:10] if spec.spectral else None
+        nx, nw, nb, ng, nbeta = ctx.needs_input_grad[:5]
+        if torch.is_grad_enabled():
+            return ConvLayerFn._create_graph_backward(ctx, da, x, w, bias, gamma, beta, sn)
+        wscale = sn[2] if spec.spectral else None
+        dgamma = dbeta = None
+        if spec.bn:
+            y = t5
+            P = y.shape[0] * y.shape[2] * y.shape[3]
+            if ctx.stats_eval is not None:
+                # eval-mode BN is a per-channel affine map: dy = da * act' * gamma * invstd
+                dy, _, _ = K.bn_backward(da, y, stats, gamma, beta, spec.act, spec.alpha, need_affine=False)
+                raise NotImplementedError("backward through eval-mode BatchNorm is not on the training path")
+            if dp.sync_bn():
+                sums, da_c = K.bn_backward_sums(da, y, stats, gamma, beta, spec.act, spec.alpha)
+                dp.all_reduce_sum(sums)
+                dy, dgamma, dbeta = K.bn_backward_apply(da_c, y, stats, gamma, beta, spec.act, spec.alpha, sums,
+                                                        P * dp.world(), need_affine=ng or nbeta)
+            else:
+                dy, dgamma, dbeta = K.bn_backward(da, y, stats, gamma, beta, spec.act, spec.alpha,
+                                                  need_affine=ng or nbeta)
+        elif spec.act != "none":
+            dy = K.act_backward(da, t5, spec.act, spec.alpha)
+        else:
+            dy = da
+        dx = K.conv_dgrad(dy, w, spec.geom, tuple(x.shape), wscale=wscale, like=x) if nx else None
+        dw = db = None
+        if nw or nb:
+            dw, db = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), with_bias=bias is not None and nb)
+            if spec.spectral and nw:
+                u, v, inv_sigma = sn
+                dw = K.spectral_backward(w, dw, u, v, inv_sigma, spec.geom.transposed)
+            if not nw:
+                dw = None
+        return dx, dw, db, dgamma, dbeta, None, None, None
+
+    @staticmethod
+    def _create_graph_backward(ctx, da, x, w, bias, gamma, beta, sn):
+        """Differentiable backward: rebuild the layer from its REAL inputs (x keeps its
+        history, w is the Parameter) and let autograd differentiate the composite, so the
+        returned gradients are functions of (da, x, w, ...) that gp.backward() can follow."""
+        spec = ctx.spec
+        slots = [i for i, t in enumerate((x, w, bias, gamma, beta))
+                 if t is not None and ctx.needs_input_grad[i]]
+        out = [None] * 8
+        if not slots:
+            return tuple(out)
+        src = (x, w, bias, gamma, beta)
+        with torch.enable_grad():
+            a = composite_layer(x, w, bias, gamma, beta, spec, ctx.stats_eval, sn)
+            grads = torch.autograd.grad(a, [src[i] for i in slots], da, create_graph=True, allow_unused=True)
+        for i, g in zip(slots, grads):
+            out[i] = g
+        return tuple(out)

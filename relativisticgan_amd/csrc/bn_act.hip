@@ -64,11 +64,9 @@ __global__ __launch_bounds__(256) void bn_stats_partial(const float* __restrict_
   }
 }
 
-__global__ void bn_stats_final(const float* __restrict__ part, int chunks, int C, long long P, float eps,
-                               float momentum, float* running_mean, float* running_var,
-                               long long* nbt, float* stats) {
+// chunk partials -> per-channel moments (count, mean, M2) of this rank's batch
+__global__ void bn_moments_reduce(const float* __restrict__ part, int chunks, int C, float* __restrict__ mom) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && nbt) nbt[0] += 1;
   if (c >= C) return;
   double N = 0.0, M = 0.0, S = 0.0;
   for (int k = 0; k < chunks; ++k) {
@@ -80,30 +78,72 @@ __global__ void bn_stats_final(const float* __restrict__ part, int chunks, int C
     S += sb + d * d * (N * nb / nt);
     N = nt;
   }
+  mom[c] = (float)N;
+  mom[C + c] = (float)M;
+  mom[2 * C + c] = (float)S;
+}
+
+// merge `nranks` moment blocks [r][3][C] in rank order -> (mean, invstd), running stats
+__global__ void bn_finalize_kernel(const float* __restrict__ mom, int nranks, int C, float eps, float momentum,
+                                   float* running_mean, float* running_var, long long* nbt, float* stats) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) nbt[0] += 1;
+  if (c >= C) return;
+  double N = 0.0, M = 0.0, S = 0.0;
+  for (int k = 0; k < nranks; ++k) {
+    const double nb = mom[((size_t)k * 3 + 0) * C + c];
+    if (nb == 0.0) continue;
+    const double mb = mom[((size_t)k * 3 + 1) * C + c], sb = mom[((size_t)k * 3 + 2) * C + c];
+    const double nt = N + nb, d = mb - M;
+    M += d * (nb / nt);
+    S += sb + d * d * (N * nb / nt);
+    N = nt;
+  }
   const float mean = (float)M;
-  const float var = (float)(S / (double)P);
+  const float var = (float)(S / N);
   stats[c] = mean;
   stats[C + c] = 1.f / sqrtf(var + eps);
   if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
   if (running_var) {
-    const float unb = P > 1 ? (float)(S / (double)(P - 1)) : var;
+    const float unb = N > 1.0 ? (float)(S / (N - 1.0)) : var;
     running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
   }
+}
+
+extern "C" int rgan_bn_moments(const float* y, long long P, int C, long long sp, long long sc, float* moments,
+                               void* partial, void* stream) {
+  RGAN_REQUIRE(y && moments && partial && P > 0 && C > 0);
+  hipStream_t s = (hipStream_t)stream;
+  const int chunks = bn_chunks(P, C);
+  float* part = (float*)partial;
+  bn_stats_partial<<<dim3(chunks, ceil_div(C, BN_CG)), 256, 0, s>>>(y, P, C, sp, sc, chunks, part);
+  RGAN_CHECK_LAUNCH();
+  bn_moments_reduce<<<ceil_div(C, 256), 256, 0, s>>>(part, chunks, C, moments);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int rgan_bn_finalize(const float* moments, int nranks, int C, float eps, float momentum,
+                                float* running_mean, float* running_var, long long* num_batches_tracked,
+                                float* stats, void* stream) {
+  RGAN_REQUIRE(moments && stats && nranks > 0 && C > 0);
+  bn_finalize_kernel<<<ceil_div(C, 256), 256, 0, (hipStream_t)stream>>>(moments, nranks, C, eps, momentum,
+                                                                        running_mean, running_var,
+                                                                        num_batches_tracked, stats);
+  RGAN_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int rgan_bn_stats(const float* y, long long P, int C, long long sp, long long sc, float eps,
                              float momentum, float* running_mean, float* running_var,
                              long long* num_batches_tracked, float* stats, void* partial, void* stream) {
   RGAN_REQUIRE(y && stats && partial && P > 0 && C > 0);
-  hipStream_t s = (hipStream_t)stream;
   const int chunks = bn_chunks(P, C);
-  float* part = (float*)partial;
-  bn_stats_partial<<<dim3(chunks, ceil_div(C, BN_CG)), 256, 0, s>>>(y, P, C, sp, sc, chunks, part);
-  RGAN_CHECK_LAUNCH();
-  bn_stats_final<<<ceil_div(C, 256), 256, 0, s>>>(part, chunks, C, P, eps, momentum, running_mean,
-                                                   running_var, num_batches_tracked, stats);
-  RGAN_CHECK_LAUNCH();
-  return 0;
+  float* mom = (float*)partial + (size_t)chunks * 3 * C;
+  int rc = rgan_bn_moments(y, P, C, sp, sc, mom, partial, stream);
+  if (rc) return rc;
+  return rgan_bn_finalize(mom, 1, C, eps, momentum, running_mean, running_var, num_batches_tracked, stats,
+                          stream);
 }
 
 // a = act(y*alpha_c + beta_c), alpha_c = gamma*invstd, beta_c = beta - mean*alpha_c
@@ -207,10 +247,8 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ 
   }
 }
 
-// coef[c] = (k1, k2, al): dy = al*(g - k1 - (y-mean)*k2)
-__global__ void bn_bwd_final(const float* __restrict__ part, int chunks, int C, long long P,
-                             const float* __restrict__ stats, const float* __restrict__ gamma,
-                             float* dgamma, float* dbeta, float* coef) {
+// chunk partials -> this rank's per-channel (sum g, sum g*(y-mean)) = sums[2][C]
+__global__ void bn_bwd_sums_reduce(const float* __restrict__ part, int chunks, int C, float* __restrict__ sums) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   double a1 = 0.0, a2 = 0.0;
@@ -218,54 +256,81 @@ __global__ void bn_bwd_final(const float* __restrict__ part, int chunks, int C, 
     a1 += part[((size_t)k * 2 + 0) * C + c];
     a2 += part[((size_t)k * 2 + 1) * C + c];
   }
-  const float inv = stats[C + c];
-  const float sg = (float)a1, sgx = (float)a2;
-  if (dbeta) dbeta[c] = sg;
-  if (dgamma) dgamma[c] = sgx * inv;
-  coef[c] = sg / (float)P;
-  coef[C + c] = sgx * inv * inv / (float)P;
-  coef[2 * C + c] = (gamma ? gamma[c] : 1.f) * inv;
+  sums[c] = (float)a1;
+  sums[C + c] = (float)a2;
 }
 
+// dy = al*(g - sum_g/Pg - (y-mean)*invstd^2*sum_gx/Pg); dgamma = invstd*sum_gx, dbeta = sum_g
 __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ da, long long dsp,
                                                     long long dsc, const float* __restrict__ y, long long P,
                                                     int C, long long sp, long long sc,
                                                     const float* __restrict__ stats,
                                                     const float* __restrict__ gamma,
                                                     const float* __restrict__ beta, int act, float alpha,
-                                                    const float* __restrict__ coef, float* __restrict__ dy,
-                                                    long long ysp, long long ysc) {
+                                                    const float* __restrict__ sums, float inv_pg,
+                                                    float* __restrict__ dy, long long ysp, long long ysc,
+                                                    float* dgamma, float* dbeta) {
   const long long total = P * C;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const long long p = i / C;
     const int c = (int)(i - p * C);
-    const float mean = stats[c], al = coef[2 * C + c];
+    const float mean = stats[c], inv = stats[C + c];
+    const float al = (gamma ? gamma[c] : 1.f) * inv;
     const float be = (beta ? beta[c] : 0.f) - mean * al;
+    const float k1 = sums[c] * inv_pg, k2 = sums[C + c] * inv * inv * inv_pg;
     const float v = y[p * sp + c * sc];
     const float gz = da[p * dsp + c * dsc] * act_grad_from_in(v * al + be, act, alpha);
-    dy[p * ysp + c * ysc] = al * (gz - coef[c] - (v - mean) * coef[C + c]);
+    dy[p * ysp + c * ysc] = al * (gz - k1 - (v - mean) * k2);
+    if (p == 0) {
+      if (dbeta) dbeta[c] = sums[c];
+      if (dgamma) dgamma[c] = sums[C + c] * inv;
+    }
   }
+}
+
+extern "C" int rgan_bn_backward_sums(const float* da, long long dsp, long long dsc, const float* y, long long P,
+                                     int C, long long sp, long long sc, const float* stats, const float* gamma,
+                                     const float* beta, int act, float act_alpha, float* sums, void* partial,
+                                     void* stream) {
+  RGAN_REQUIRE(da && y && stats && sums && partial && P > 0 && C > 0);
+  hipStream_t s = (hipStream_t)stream;
+  const int chunks = bn_chunks(P, C);
+  float* part = (float*)partial;
+  bn_bwd_partial<<<dim3(chunks, ceil_div(C, BN_CG)), 256, 0, s>>>(da, dsp, dsc, y, P, C, sp, sc, stats,
+                                                                   gamma, beta, act, act_alpha, chunks, part);
+  RGAN_CHECK_LAUNCH();
+  bn_bwd_sums_reduce<<<ceil_div(C, 256), 256, 0, s>>>(part, chunks, C, sums);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int rgan_bn_backward_apply(const float* da, long long dsp, long long dsc, const float* y, long long P,
+                                      int C, long long sp, long long sc, const float* stats, const float* gamma,
+                                      const float* beta, int act, float act_alpha, const float* sums,
+                                      long long P_global, float* dy, long long ysp, long long ysc, float* dgamma,
+                                      float* dbeta, void* stream) {
+  RGAN_REQUIRE(da && y && stats && sums && dy && P > 0 && C > 0 && P_global >= P);
+  bn_bwd_apply<<<grid_for(P * C), 256, 0, (hipStream_t)stream>>>(da, dsp, dsc, y, P, C, sp, sc, stats, gamma,
+                                                                 beta, act, act_alpha, sums,
+                                                                 1.f / (float)P_global, dy, ysp, ysc, dgamma,
+                                                                 dbeta);
+  RGAN_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int rgan_bn_backward(const float* da, long long dsp, long long dsc, const float* y, long long P,
                                 int C, long long sp, long long sc, const float* stats, const float* gamma,
                                 const float* beta, int act, float act_alpha, float* dy, long long ysp,
                                 long long ysc, float* dgamma, float* dbeta, void* partial, void* stream) {
-  RGAN_REQUIRE(da && y && stats && dy && partial && P > 0 && C > 0);
-  hipStream_t s = (hipStream_t)stream;
+  RGAN_REQUIRE(partial);
   const int chunks = bn_chunks(P, C);
-  float* part = (float*)partial;                       // [chunks][2][C]
-  float* coef = part + (size_t)chunks * 2 * C;          // [3][C] after the [chunks][2][C] partials
-  bn_bwd_partial<<<dim3(chunks, ceil_div(C, BN_CG)), 256, 0, s>>>(da, dsp, dsc, y, P, C, sp, sc, stats,
-                                                                   gamma, beta, act, act_alpha, chunks, part);
-  RGAN_CHECK_LAUNCH();
-  bn_bwd_final<<<ceil_div(C, 256), 256, 0, s>>>(part, chunks, C, P, stats, gamma, dgamma, dbeta, coef);
-  RGAN_CHECK_LAUNCH();
-  bn_bwd_apply<<<grid_for(P * C), 256, 0, s>>>(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act,
-                                              act_alpha, coef, dy, ysp, ysc);
-  RGAN_CHECK_LAUNCH();
-  return 0;
+  float* sums = (float*)partial + (size_t)chunks * 2 * C;
+  int rc = rgan_bn_backward_sums(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, sums,
+                                 partial, stream);
+  if (rc) return rc;
+  return rgan_bn_backward_apply(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, sums, P,
+                                dy, ysp, ysc, dgamma, dbeta, stream);
 }
 
 // ------------------------------------------------------------------ activations

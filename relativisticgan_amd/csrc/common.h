@@ -28,7 +28,7 @@ __device__ __forceinline__ float act_fwd(float v, int act, float alpha) {
     case RGAN_ACT_SELU: {
       const float scale = 1.0507009873554804934193349852946f;
       const float a = 1.6732632423543772848170429916717f;
-      return v > 0.f ? scale * v : scale * (a * (expf(v) - 1.f));
+      return v > 0.f ? scale * v : scale * (a * expm1f(v));
     }
     default: return v;
   }

@@ -21,6 +21,9 @@
 // slabs reduced in fixed order (deterministic) by splitk_reduce.
 #include "common.h"
 
+#include <string>
+#include <vector>
+
 namespace rgan {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -805,6 +808,41 @@ static void launch_mode(const Plan& p, dim3 grid, hipStream_t s) {
   }
 }
 
+
+// ---------------------------------------------------------------- live launch timing
+// When enabled (rgan_profile_begin), every GEMM launch is bracketed by a pair of HIP
+// events on its own stream and tagged with the algorithmic FLOPs of the conv op it
+// serves (2*B*Cin*Cout*k*k*pixels, the torch flop-counter convention) and with the
+// kernel instantiation, so bench.py can report FLOPs / kernel time per kernel symbol.
+struct ProfRec {
+  hipEvent_t a, b;
+  double flops;
+  int kid;
+};
+static bool g_prof = false;
+static std::vector<hipEvent_t> g_pool;
+static std::vector<ProfRec> g_recs;
+static std::vector<std::string> g_kernel_names;
+static double g_cur_flops = 0.0;
+
+static int kernel_id(int mode, int cfg, bool av, bool bv) {
+  const int id = ((mode * 3 + cfg) * 2 + (av ? 1 : 0)) * 2 + (bv ? 1 : 0);
+  if (g_kernel_names.empty()) {
+    g_kernel_names.resize(36);
+    const int bm[3] = {128, 128, 256}, bn[3] = {128, 64, 32}, wmv[3] = {2, 2, 4}, wnv[3] = {2, 2, 1};
+    for (int m = 0; m < 3; ++m)
+      for (int c = 0; c < 3; ++c)
+        for (int a = 0; a < 2; ++a)
+          for (int b = 0; b < 2; ++b) {
+            char buf[160];
+            snprintf(buf, sizeof(buf), "void rgan::gemm_kernel<%d, %d, %d, %d, %d, %s, %s>(rgan::GemmArgs)", m, bm[c],
+                     bn[c], wmv[c], wnv[c], a ? "true" : "false", b ? "true" : "false");
+            g_kernel_names[((m * 3 + c) * 2 + a) * 2 + b] = buf;
+          }
+  }
+  return id;
+}
+
 static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   if (ws_bytes < plan_ws_bytes(p)) return RGAN_EINVAL;
   if (p.g.M <= 0 || p.g.N <= 0 || p.g.K <= 0) return RGAN_EINVAL;
@@ -823,12 +861,25 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   int bm, bn;
   tile_dims(p.cfg, bm, bn);
   dim3 grid(ceil_div(p.g.M, bm) * p.g.tiles_n, 1, p.phases * p.g.splits);
+  ProfRec rec{};
+  const bool prof = g_prof && g_recs.size() * 2 + 2 <= g_pool.size();
+  if (prof) {
+    rec.a = g_pool[g_recs.size() * 2];
+    rec.b = g_pool[g_recs.size() * 2 + 1];
+    rec.flops = g_cur_flops;
+    rec.kid = kernel_id(p.mode, p.cfg, p.av, p.bv);
+    hipEventRecord(rec.a, s);
+  }
   switch (p.mode) {
     case MODE_CONV: launch_mode<MODE_CONV>(p, grid, s); break;
     case MODE_CONVT2: launch_mode<MODE_CONVT2>(p, grid, s); break;
     default: launch_mode<MODE_WGRAD>(p, grid, s); break;
   }
   RGAN_CHECK_LAUNCH();
+  if (prof) {
+    hipEventRecord(rec.b, s);
+    g_recs.push_back(rec);
+  }
   if (p.g.splits > 1) {
     const size_t total = (size_t)p.g.M * p.g.N * p.phases;
     const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
@@ -857,10 +908,16 @@ extern "C" size_t rgan_conv_workspace(const RganConv* d, int which) {
   return plan_ws_bytes(p) + 256;  // never 0 for a valid descriptor (0 signals "unsupported")
 }
 
+static double conv_flops(const RganConv* d) {
+  const double pix = d->transposed ? (double)d->hin * d->win : (double)d->hout * d->wout;
+  return 2.0 * d->batch * (double)d->cin * d->cout * d->kh * d->kw * pix;
+}
+
 extern "C" int rgan_conv_fwd(const RganConv* d, const float* x, const float* w, const float* wscale,
                              const float* bias, float* y, int act, float act_alpha, void* ws,
                              size_t ws_bytes, void* stream) {
   if (!x || !w || !y) return RGAN_EINVAL;
+  g_cur_flops = conv_flops(d);
   Plan p;
   int rc = plan_fwd(d, x, w, wscale, bias, y, act, act_alpha, p);
   if (rc) return rc;
@@ -870,6 +927,7 @@ extern "C" int rgan_conv_fwd(const RganConv* d, const float* x, const float* w, 
 extern "C" int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* w, const float* wscale,
                                float* dx, void* ws, size_t ws_bytes, void* stream) {
   if (!dy || !w || !dx) return RGAN_EINVAL;
+  g_cur_flops = conv_flops(d);
   Plan p;
   int rc = plan_dgrad(d, dy, w, wscale, dx, p);
   if (rc) return rc;
@@ -879,16 +937,81 @@ extern "C" int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* 
 extern "C" int rgan_conv_wgrad(const RganConv* d, const float* x, const float* dy, float* dw,
                                float* dbias, void* ws, size_t ws_bytes, void* stream) {
   if (!x || !dy || !dw) return RGAN_EINVAL;
+  g_cur_flops = conv_flops(d);
   Plan p;
   int rc = plan_wgrad(d, x, dy, dw, p);
   if (rc) return rc;
   rc = run_plan(p, ws, ws_bytes, (hipStream_t)stream);
   if (rc) return rc;
   if (dbias) {
-    // per-output-channel sum of dy: for Conv2d dy has cout channels, for ConvT too
+    // per-output-channel sum of dy (Conv2d and ConvTranspose2d alike: dy has cout channels)
     const long long P = (long long)d->batch * d->hout * d->wout;
-    if (d->ys[1] != 1 || d->ys[3] != d->cout || d->ys[2] != (long long)d->wout * d->cout) return RGAN_EINVAL;
-    return rgan_channel_sum(dy, P, d->cout, d->cout, 1, dbias, nullptr, stream);
+    long long sp;
+    if ((long long)d->hout * d->wout == 1) {
+      sp = d->ys[0];
+    } else {
+      if (d->ys[1] != 1 || d->ys[3] != d->cout || d->ys[2] != (long long)d->wout * d->cout ||
+          d->ys[0] != (long long)d->hout * d->wout * d->cout)
+        return RGAN_EINVAL;
+      sp = d->cout;
+    }
+    return rgan_channel_sum(dy, P, d->cout, sp, d->ys[1], dbias, nullptr, stream);
   }
+  return 0;
+}
+
+extern "C" int rgan_profile_begin(int capacity) {
+  if (capacity <= 0) return RGAN_EINVAL;
+  for (auto e : g_pool) hipEventDestroy(e);
+  g_pool.clear();
+  g_recs.clear();
+  g_pool.resize((size_t)capacity * 2);
+  for (auto& e : g_pool) {
+    hipError_t rc = hipEventCreate(&e);
+    if (rc != hipSuccess) return (int)rc;
+  }
+  g_prof = true;
+  return 0;
+}
+
+// Stops recording, waits for the last event and returns totals over all recorded GEMM
+// launches; per-kernel-symbol totals are then available via rgan_profile_kernel.
+static std::vector<double> g_kms, g_kflops;
+static std::vector<long long> g_kn;
+
+extern "C" int rgan_profile_end(double* total_ms, double* total_flops, long long* launches) {
+  g_prof = false;
+  g_kms.assign(36, 0.0);
+  g_kflops.assign(36, 0.0);
+  g_kn.assign(36, 0);
+  double ms = 0.0, fl = 0.0;
+  if (!g_recs.empty()) {
+    hipError_t rc = hipEventSynchronize(g_recs.back().b);
+    if (rc != hipSuccess) return (int)rc;
+  }
+  for (const ProfRec& r : g_recs) {
+    float t = 0.f;
+    hipError_t rc = hipEventElapsedTime(&t, r.a, r.b);
+    if (rc != hipSuccess) return (int)rc;
+    ms += t;
+    fl += r.flops;
+    g_kms[r.kid] += t;
+    g_kflops[r.kid] += r.flops;
+    g_kn[r.kid] += 1;
+  }
+  if (total_ms) *total_ms = ms;
+  if (total_flops) *total_flops = fl;
+  if (launches) *launches = (long long)g_recs.size();
+  g_recs.clear();
+  return 0;
+}
+
+extern "C" int rgan_profile_kernel(int idx, char* name, int name_len, double* ms, double* flops, long long* n) {
+  if (idx < 0 || idx >= 36 || g_kms.empty()) return RGAN_EINVAL;
+  kernel_id(0, 0, false, false);
+  if (name && name_len > 0) snprintf(name, name_len, "%s", g_kernel_names[idx].c_str());
+  if (ms) *ms = g_kms[idx];
+  if (flops) *flops = g_kflops[idx];
+  if (n) *n = g_kn[idx];
   return 0;
 }

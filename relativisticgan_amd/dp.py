@@ -1,0 +1,127 @@
+"""Data parallelism: one process per GPU, torch.distributed over RCCL (xGMI).
+
+Replaces the reference's only parallelism, ``torch.nn.parallel.data_parallel`` inside
+every forward (GLI:228-229,312-313,393-394,455-456).  Instead of re-broadcasting all
+parameters per forward call and gathering outputs to GPU 0, every rank keeps a
+persistent replica and processes ``B_global / world`` samples; the exchanges are
+(SURVEY §8(e)):
+
+  * loss heads: the batch sums the relativistic means need (2 floats fwd, 4 bwd);
+  * BatchNorm (SyncBN, default on): per-layer moments [3C] all-gathered and merged in
+    rank order in the forward, [2C] sums all-reduced in the backward, so the math equals
+    the global-batch single-process result (the reference's DP did NOT sync BN:
+    ``sync_bn=False`` reproduces that per-shard behaviour);
+  * gradients: one bucketed all-reduce (SUM: the losses already divide by the global
+    batch) before each optimizer step.
+Spectral-norm u/v and Adam are replicated and stay identical on every rank.
+
+The helpers in this module are backend-agnostic (they only move small tensors through
+``torch.distributed``), so the same code runs on RCCL (``nccl``) on the GPUs and on
+``gloo`` in the CPU tests.
+"""
+import torch
+import torch.distributed as dist
+
+
+class _State:
+    group = None
+    world = 1
+    rank = 0
+    sync_bn = True
+
+
+_S = _State()
+
+
+def setup(group=None, sync_bn=True):
+    """Activate data-parallel mode for the current process (after init_process_group)."""
+    if not dist.is_available() or not dist.is_initialized():
+        _S.group, _S.world, _S.rank = None, 1, 0
+    else:
+        _S.group = group
+        _S.world = dist.get_world_size(group)
+        _S.rank = dist.get_rank(group)
+    _S.sync_bn = sync_bn
+
+
+def reset():
+    _S.group, _S.world, _S.rank, _S.sync_bn = None, 1, 0, True
+
+
+def world():
+    return _S.world
+
+
+def rank():
+    return _S.rank
+
+
+def active():
+    return _S.world > 1
+
+
+def sync_bn():
+    return _S.world > 1 and _S.sync_bn
+
+
+def all_reduce_sum(t):
+    """In-place SUM over ranks (no-op for world 1)."""
+    if _S.world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=_S.group)
+    return t
+
+
+def all_gather_cat(t):
+    """[world * numel] concatenation of every rank's ``t`` in rank order."""
+    if _S.world == 1:
+        return t
+    out = torch.empty(_S.world * t.numel(), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.contiguous().view(-1), group=_S.group)
+    return out
+
+
+def merge_moments(moments, C):
+    """Reference merge of [world][3][C] (count, mean, M2) -> (mean, biased var, count).
+
+    Same Chan-formula, rank-ordered merge as the device kernel (rgan_bn_finalize);
+    used by tests and by CPU-side checks.
+    """
+    m = moments.view(-1, 3, C).double()
+    N = torch.zeros(C, dtype=torch.float64)
+    M = torch.zeros(C, dtype=torch.float64)
+    S = torch.zeros(C, dtype=torch.float64)
+    for k in range(m.shape[0]):
+        nb, mb, sb = m[k, 0].cpu(), m[k, 1].cpu(), m[k, 2].cpu()
+        nt = N + nb
+        d = mb - M
+        w = torch.where(nt > 0, nb / nt.clamp_min(1), torch.zeros_like(nb))
+        M = M + d * w
+        S = S + sb + d * d * torch.where(nt > 0, N * nb / nt.clamp_min(1), torch.zeros_like(nb))
+        N = nt
+    return M, S / N, N
+
+
+def allreduce_grads(params, bucket_bytes=64 << 20):
+    """SUM-all-reduce the .grad of ``params`` in flat buckets (one RCCL call per bucket)."""
+    if _S.world == 1:
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    bucket, size = [], 0
+    for g in grads:
+        bucket.append(g)
+        size += g.numel() * g.element_size()
+        if size >= bucket_bytes:
+            _flush(bucket)
+            bucket, size = [], 0
+    if bucket:
+        _flush(bucket)
+
+
+def _flush(bucket):
+    flat = torch.cat([g.reshape(-1) for g in bucket])
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=_S.group)
+    off = 0
+    for g in bucket:
+        n = g.numel()
+        g.view(-1).copy_(flat[off:off + n].view_as(g.view(-1)))
+        off += n

@@ -145,6 +145,53 @@ def bn_stats(y, eps, momentum, running_mean=None, running_var=None, num_batches_
     return stats
 
 
+def bn_moments(y):
+    """This rank's per-channel (count, mean, M2) as float[3C] (SyncBN stage 1)."""
+    P, C, sp, sc = _pc(y)
+    lib = L.lib()
+    mom = torch.empty(3 * C, dtype=torch.float32, device=y.device)
+    part = L.workspace(lib.rgan_bn_partial_bytes(P, C), y.device)
+    L.check(lib.rgan_bn_moments(L.ptr(y), P, C, sp, sc, L.ptr(mom), L.ptr(part), L.stream()), "rgan_bn_moments")
+    return mom
+
+
+def bn_finalize(moments, nranks, C, eps, momentum, running_mean=None, running_var=None,
+                num_batches_tracked=None):
+    """Merge [nranks][3][C] moments in rank order -> stats float[2C] (SyncBN stage 2)."""
+    stats = torch.empty(2 * C, dtype=torch.float32, device=moments.device)
+    L.check(L.lib().rgan_bn_finalize(L.ptr(moments), int(nranks), C, float(eps), float(momentum),
+                                     L.ptr(running_mean), L.ptr(running_var), L.ptr(num_batches_tracked),
+                                     L.ptr(stats), L.stream()), "rgan_bn_finalize")
+    return stats
+
+
+def bn_backward_sums(da, y, stats, gamma, beta, act="none", alpha=0.0):
+    if not is_nhwc(da):
+        da = da.contiguous(memory_format=torch.channels_last)
+    P, C, sp, sc = _pc(y)
+    _, _, dsp, dsc = _pc(da)
+    sums = torch.empty(2 * C, dtype=torch.float32, device=y.device)
+    lib = L.lib()
+    part = L.workspace(lib.rgan_bn_partial_bytes(P, C), y.device)
+    L.check(lib.rgan_bn_backward_sums(L.ptr(da), dsp, dsc, L.ptr(y), P, C, sp, sc, L.ptr(stats), L.ptr(gamma),
+                                      L.ptr(beta), L.ACT[act], float(alpha), L.ptr(sums), L.ptr(part),
+                                      L.stream()), "rgan_bn_backward_sums")
+    return sums, da
+
+
+def bn_backward_apply(da, y, stats, gamma, beta, act, alpha, sums, P_global, need_affine=True):
+    P, C, sp, sc = _pc(y)
+    _, _, dsp, dsc = _pc(da)
+    dy = torch.empty_like(y)
+    dgamma = torch.empty(C, dtype=torch.float32, device=y.device) if need_affine and gamma is not None else None
+    dbeta = torch.empty(C, dtype=torch.float32, device=y.device) if need_affine and beta is not None else None
+    L.check(L.lib().rgan_bn_backward_apply(L.ptr(da), dsp, dsc, L.ptr(y), P, C, sp, sc, L.ptr(stats),
+                                           L.ptr(gamma), L.ptr(beta), L.ACT[act], float(alpha), L.ptr(sums),
+                                           int(P_global), L.ptr(dy), sp, sc, L.ptr(dgamma), L.ptr(dbeta),
+                                           L.stream()), "rgan_bn_backward_apply")
+    return dy, dgamma, dbeta
+
+
 def bn_apply(y, stats, gamma, beta, act="none", alpha=0.0, out=None):
     P, C, sp, sc = _pc(y)
     if out is None:
@@ -299,3 +346,25 @@ def gather_images(images, idx, out=None):
     L.check(L.lib().rgan_gather_images(L.ptr(images), L.ptr(idx), B, per, L.ptr(out), L.stream()),
             "rgan_gather_images")
     return out
+
+
+# ------------------------------------------------------------------ live launch timing
+def profile_begin(capacity=100000):
+    L.check(L.lib().rgan_profile_begin(int(capacity)), "rgan_profile_begin")
+
+
+def profile_end():
+    """{'ms', 'flops', 'launches', 'kernels': [{name, ms, flops, launches}]} of the GEMM launches."""
+    lib = L.lib()
+    ms, fl, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_longlong()
+    L.check(lib.rgan_profile_end(ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(n)), "rgan_profile_end")
+    kern = []
+    for i in range(36):
+        name = ctypes.create_string_buffer(200)
+        kms, kfl, kn = ctypes.c_double(), ctypes.c_double(), ctypes.c_longlong()
+        L.check(lib.rgan_profile_kernel(i, name, 200, ctypes.byref(kms), ctypes.byref(kfl), ctypes.byref(kn)),
+                "rgan_profile_kernel")
+        if kn.value:
+            kern.append({"name": name.value.decode(), "ms": kms.value, "flops": kfl.value, "launches": kn.value,
+                         "tflops": kfl.value / kms.value / 1e9 if kms.value > 0 else 0.0})
+    return {"ms": ms.value, "flops": fl.value, "launches": n.value, "kernels": kern}

@@ -1,0 +1,107 @@
+"""The eight --loss_D heads and the WGAN-GP penalty as autograd ops on the HIP kernels.
+
+Heads (GLI:481-484 criteria; D side GLI:592-644; G side GLI:686-709):
+  1 SGAN (BCE on D's sigmoid), 2 LSGAN, 3 WGAN(-GP), 4 HingeGAN: real and fake terms
+  are separate losses backpropagated separately (GLI:605, 624), G loss per GLI:686-693;
+  5 RSGAN, 6 RaSGAN, 7 RaLSGAN, 8 RaHingeGAN: one loss over (y_pred, y_pred_fake).
+Each head is ONE kernel launch computing the loss and both input gradients; the
+backward only scales them by the upstream gradient.  Under data parallelism the
+batch means are global: the head runs in three phases with two tiny
+all-reduces in between.
+"""
+import torch
+
+from . import dp
+from . import kernels as K
+
+
+class _Head(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, r, f, kind, side):
+        need_r = r is not None and ctx.needs_input_grad[0]
+        need_f = f is not None and ctx.needs_input_grad[1]
+        if dp.active():
+            loss, dr, df = _head_dist(kind, side, r, f, need_r, need_f)
+        else:
+            loss, dr, df = K.loss_head(kind, side, r, f, need_dr=need_r, need_df=need_f)
+        ctx.save_for_backward(dr, df)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        dr, df = ctx.saved_tensors
+        g = g.contiguous()
+        return (K.scale(dr, g) if dr is not None else None,
+                K.scale(df, g) if df is not None else None, None, None)
+
+
+def _head_dist(kind, side, r, f, need_r, need_f):
+    t = r if r is not None else f
+    n_global = t.numel() * dp.world()
+    if kind >= 6:
+        s0, _, _, _ = K.loss_head_dist(kind, side, 0, r, f, n_global)
+        g = dp.all_reduce_sum(s0[:2].clone())
+        s1, _, _, _ = K.loss_head_dist(kind, side, 1, r, f, n_global, gsum=g)
+        g6 = torch.cat([g, dp.all_reduce_sum(s1.clone())])
+        _, loss, dr, df = K.loss_head_dist(kind, side, 2, r, f, n_global, gsum=g6, need_dr=need_r, need_df=need_f)
+    else:
+        s0, _, _, _ = K.loss_head_dist(kind, side, 0, r, f, n_global)
+        g = dp.all_reduce_sum(s0[:1].clone())
+        _, loss, dr, df = K.loss_head_dist(kind, side, 2, r, f, n_global, gsum=g, need_dr=need_r, need_df=need_f)
+    return loss, dr, df
+
+
+def _flat(t):
+    return None if t is None else t.reshape(-1)
+
+
+def loss_D_real(kind, y_pred):
+    """errD_real for heads 1-4 (GLI:595-604)."""
+    assert 1 <= kind <= 4
+    return _Head.apply(_flat(y_pred), None, kind, 0)
+
+
+def loss_D_fake(kind, y_pred_fake):
+    """errD_fake for heads 1-4 (GLI:614-623)."""
+    assert 1 <= kind <= 4
+    return _Head.apply(None, _flat(y_pred_fake), kind, 1)
+
+
+def loss_D(kind, y_pred, y_pred_fake):
+    """errD for heads 5-8 (GLI:634-641)."""
+    assert 5 <= kind <= 8
+    return _Head.apply(_flat(y_pred), _flat(y_pred_fake), kind, 0)
+
+
+def loss_G(kind, y_pred_fake, y_pred=None):
+    """errG (GLI:686-709); y_pred (a no-grad D(x) of a fresh real batch) for heads 5-8."""
+    if kind <= 4:
+        return _Head.apply(None, _flat(y_pred_fake), kind, 2)
+    return _Head.apply(_flat(y_pred), _flat(y_pred_fake), kind, 2)
+
+
+# ---------------------------------------------------------------- gradient penalty
+class _GPPenalty(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, g, lam, n_global):
+        loss, norms, gc = K.gp_penalty(g, lam, n_global)
+        ctx.lam, ctx.n_global = lam, n_global
+        ctx.save_for_backward(gc, norms)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gl):
+        gc, norms = ctx.saved_tensors
+        return K.gp_penalty_backward(gc, norms, ctx.lam, ctx.n_global, gl.contiguous()), None, None
+
+
+def gradient_penalty(D, x, x_fake, u, penalty):
+    """penalty * mean((||dD(x_hat)/dx_hat||_2 - 1)^2), x_hat = x*u + x_fake*(1-u) (GLI:648-657).
+
+    The double backward runs through the create-graph path of ConvLayerFn (conv
+    dgrad/wgrad GEMMs differentiated on the MFMA kernels)."""
+    x_both = K.gp_interp(x.detach(), x_fake.detach(), u.detach()).requires_grad_(True)
+    out = D(x_both)
+    grad = torch.autograd.grad(outputs=out, inputs=x_both, grad_outputs=torch.ones_like(out),
+                               retain_graph=True, create_graph=True, only_inputs=True)[0]
+    return _GPPenalty.apply(grad, float(penalty), x.shape[0] * dp.world())

@@ -1,0 +1,403 @@
+"""DCGAN_G / DCGAN_D with the reference's surface, running on the HIP kernels.
+
+The reference builds its nets from ``param`` globals (GLI:183-460).  Here the classes
+take ``param`` explicitly (any namespace with the GLI:17-62 flag names) and keep:
+
+* the module tree and ``add_module`` names, hence every ``state_dict`` key (SURVEY
+  Appendix C), so reference checkpoints load unchanged;
+* the parameter-initialisation RNG stream: each conv/linear/spectral-norm layer is
+  initialised by the same torch CPU init calls in the same order as the reference's
+  constructors (kaiming-uniform, bias uniform, spectral u/v normal draws), and
+  ``weights_init`` (GLI:466-477) matches the same class-name patterns;
+* forward semantics: train-mode BatchNorm with running-stat updates, one spectral
+  power iteration per train-mode forward, ``D(x).view(-1)`` outputs.
+
+Forward runs the layers as fused ``ConvLayerFn`` calls (conv + bias + BN + activation)
+rather than module-by-module: the activation modules are name placeholders only.
+Activations between layers are NHWC; G's output image is NCHW-contiguous like the
+reference's, and D accepts images in any layout.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from .autograd import ConvLayerFn, LayerSpec
+from .kernels import ConvGeom, spectral_power
+
+
+# ---------------------------------------------------------------- parameter holders
+class _ConvBase(nn.Module):
+    transposed = False
+
+    def __init__(self, cin, cout, k, stride, pad, bias, spectral):
+        super().__init__()
+        self.cin, self.cout, self.k, self.stride, self.pad = cin, cout, k, stride, pad
+        self.spectral = spectral
+        ctor = torch.nn.ConvTranspose2d if self.transposed else torch.nn.Conv2d
+        tmp = ctor(cin, cout, k, stride, pad, bias=bias)  # same RNG draws as the reference
+        if spectral:
+            tmp = torch.nn.utils.spectral_norm(tmp)       # draws u then v (spectral_norm.py:168-169)
+            self.weight_orig = nn.Parameter(tmp.weight_orig.detach().clone())
+            self.register_buffer("weight_u", tmp.weight_u.detach().clone())
+            self.register_buffer("weight_v", tmp.weight_v.detach().clone())
+        else:
+            self.weight = nn.Parameter(tmp.weight.detach().clone())
+        self.bias = nn.Parameter(tmp.bias.detach().clone()) if bias else None
+        self.geom = ConvGeom(k, stride, pad, self.transposed)
+
+    @property
+    def w(self):
+        return self.weight_orig if self.spectral else self.weight
+
+    def extra_repr(self):
+        return (f"{self.cin}, {self.cout}, kernel_size=({self.k}, {self.k}), stride=({self.stride}, {self.stride}),"
+                f" padding=({self.pad}, {self.pad}), bias={self.bias is not None}, spectral={self.spectral}")
+
+
+class Conv2d(_ConvBase):
+    """Conv2d parameters (torch layout [cout][cin][k][k])."""
+
+    def __init__(self, cin, cout, k, stride=1, pad=0, bias=True, spectral=False):
+        super().__init__(cin, cout, k, stride, pad, bias, spectral)
+
+
+class ConvTranspose2d(_ConvBase):
+    """ConvTranspose2d parameters (torch layout [cin][cout][k][k])."""
+    transposed = True
+
+    def __init__(self, cin, cout, k, stride=1, pad=0, bias=True, spectral=False):
+        super().__init__(cin, cout, k, stride, pad, bias, spectral)
+
+
+class SpectralConv2d(Conv2d):
+    """Spectral-norm Conv2d: state_dict weight_orig / weight_u / weight_v; ``.weight``
+    aliases weight_orig like torch's hook-based attribute (so weights_init hits it)."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, spectral=True, **k)
+
+    @property
+    def weight(self):
+        return self.weight_orig
+
+
+class SpectralConvTranspose2d(ConvTranspose2d):
+    def __init__(self, *a, **k):
+        super().__init__(*a, spectral=True, **k)
+
+    @property
+    def weight(self):
+        return self.weight_orig
+
+
+class Linear(nn.Module):
+    """Linear parameters; run as a 1x1 (arch-1 G) or k4 (arch-1 D) convolution."""
+
+    def __init__(self, fin, fout):
+        super().__init__()
+        tmp = torch.nn.Linear(fin, fout)
+        self.weight = nn.Parameter(tmp.weight.detach().clone())
+        self.bias = nn.Parameter(tmp.bias.detach().clone())
+        self.in_features, self.out_features = fin, fout
+
+    def extra_repr(self):
+        return f"in_features={self.in_features}, out_features={self.out_features}, bias=True"
+
+
+class BatchNorm2d(nn.Module):
+    """BatchNorm2d parameters and running buffers (torch.nn.BatchNorm2d's names/defaults)."""
+
+    def __init__(self, c, eps=1e-5, momentum=0.1):
+        super().__init__()
+        self.num_features, self.eps, self.momentum = c, eps, momentum
+        self.weight = nn.Parameter(torch.ones(c))
+        self.bias = nn.Parameter(torch.zeros(c))
+        self.register_buffer("running_mean", torch.zeros(c))
+        self.register_buffer("running_var", torch.ones(c))
+        self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+
+    def extra_repr(self):
+        return f"{self.num_features}, eps={self.eps}, momentum={self.momentum}, affine=True, track_running_stats=True"
+
+
+class _Act(nn.Module):
+    """Name placeholder for an activation module (the math is fused into the kernels)."""
+
+    def __init__(self, kind, alpha=0.0):
+        super().__init__()
+        self.kind, self.alpha = kind, alpha
+
+    def extra_repr(self):
+        return f"{self.kind}" + (f", {self.alpha}" if self.kind == "lrelu" else "")
+
+
+class _Upsample(nn.Module):
+    def __init__(self):
+        super().__init__()
+
+
+def weights_init(m):
+    """GLI:467-475: N(0,0.02) for *Conv* weights, N(1,0.02)/0 for *BatchNorm* affine."""
+    name = m.__class__.__name__
+    if name.find("Conv") != -1:
+        m.weight.data.normal_(0.0, 0.02)
+    elif name.find("BatchNorm") != -1:
+        m.weight.data.normal_(1.0, 0.02)
+        m.bias.data.fill_(0)
+
+
+# ---------------------------------------------------------------- fused layer plan
+class _Layer:
+    """One fused step: conv module (+ bn module) + activation."""
+
+    __slots__ = ("conv", "bn", "spec", "w_view", "in_view", "out_view")
+
+    def __init__(self, conv, bn, act, alpha=0.0, nchw_out=False, w_view=None, in_view=None, out_view=None):
+        self.conv, self.bn = conv, bn
+        geom = conv.geom if isinstance(conv, _ConvBase) else None
+        self.spec = (LayerSpec(geom, act, alpha, bn is not None, spectral=getattr(conv, "spectral", False),
+                               nchw_out=nchw_out) if geom is not None else None)
+        self.w_view, self.in_view, self.out_view = w_view, in_view, out_view
+
+    def run(self, h, training):
+        conv, bn = self.conv, self.bn
+        w = conv.w if isinstance(conv, _ConvBase) else conv.weight
+        if self.w_view is not None:
+            w = w.view(*self.w_view)
+        if self.in_view is not None:
+            h = h.reshape(h.shape[0], *self.in_view)
+        sn = None
+        if self.spec.spectral:
+            with torch.no_grad():
+                inv_sigma = spectral_power(w.detach(), conv.weight_u, conv.weight_v, conv.geom.transposed,
+                                           do_iter=training)
+            sn = (conv.weight_u.clone(), conv.weight_v.clone(), inv_sigma)
+        bufs = (bn.running_mean, bn.running_var, bn.num_batches_tracked, training) if bn is not None else None
+        out = ConvLayerFn.apply(h, w, conv.bias, bn.weight if bn is not None else None,
+                                bn.bias if bn is not None else None, self.spec, bufs, sn)
+        if self.out_view is not None:
+            out = out.reshape(out.shape[0], *self.out_view)
+        return out
+
+
+def _lin_spec(layer, geom, act, alpha=0.0, nchw_out=False):
+    layer.spec = LayerSpec(geom, act, alpha, False, nchw_out=nchw_out)
+    return layer
+
+
+class _Net(nn.Module):
+    def _run(self, x):
+        if getattr(self.param, "NN_conv", False) and self.param.arch == 0:
+            raise NotImplementedError("--NN_conv (Upsample+Conv3x3) is not on this build's hot path yet")
+        h = x
+        for layer in self._plan:
+            h = layer.run(h, self.training)
+        return h
+
+
+# ---------------------------------------------------------------- arch 0 (DCGAN)
+class _G0(_Net):
+    """DCGAN generator (GLI:323-397)."""
+
+    def __init__(self, p):
+        super().__init__()
+        self.param = p
+        main = nn.Sequential()
+        plan = []
+        mult = p.image_size // 8
+        sn = p.spectral_G
+
+        def block(part, suffix, conv, ch):
+            main.add_module(conv[0], conv[1])
+            if p.SELU:
+                main.add_module(f"{part}-SELU{suffix}", _Act("selu"))
+                plan.append(_Layer(conv[1], None, "selu"))
+                return
+            bn = None
+            if not p.no_batch_norm_G and not sn:
+                bn = BatchNorm2d(ch)
+                main.add_module(f"{part}-BatchNorm2d{suffix}", bn)
+            act = "tanh" if p.Tanh_GD else "relu"
+            main.add_module(f"{part}-{'Tanh' if p.Tanh_GD else 'ReLU'}{suffix}", _Act(act))
+            plan.append(_Layer(conv[1], bn, act))
+
+        cls = SpectralConvTranspose2d if sn else ConvTranspose2d
+        start = cls(p.z_size, p.G_h_size * mult, 4, 1, 0, bias=False)
+        block("Start", "", ("Start-SpectralConvTranspose2d" if sn else "Start-ConvTranspose2d", start),
+              p.G_h_size * mult)
+        i = 1
+        while mult > 1:
+            cin, cout = p.G_h_size * mult, p.G_h_size * (mult // 2)
+            if p.NN_conv:
+                main.add_module("Middle-UpSample [%d]" % i, _Upsample())
+                ccls = SpectralConv2d if sn else Conv2d
+                conv = ccls(cin, cout, 3, 1, 1, bias=True)
+                name = ("Middle-SpectralConv2d [%d]" if sn else "Middle-Conv2d [%d]") % i
+            else:
+                conv = cls(cin, cout, 4, 2, 1, bias=False)
+                name = ("Middle-SpectralConvTranspose2d [%d]" if sn else "Middle-ConvTranspose2d [%d]") % i
+            block("Middle", " [%d]" % i, (name, conv), cout)
+            mult //= 2
+            i += 1
+        if p.NN_conv:
+            main.add_module("End-UpSample", _Upsample())
+            ccls = SpectralConv2d if sn else Conv2d
+            end = ccls(p.G_h_size, p.n_colors, 3, 1, 1, bias=True)
+            main.add_module("End-SpectralConv2d" if sn else "End-Conv2d", end)
+        else:
+            end = cls(p.G_h_size, p.n_colors, 4, 2, 1, bias=False)
+            main.add_module("End-SpectralConvTranspose2d" if sn else "End-ConvTranspose2d", end)
+        main.add_module("End-Tanh", _Act("tanh"))
+        plan.append(_Layer(end, None, "tanh", nchw_out=True))
+        self.main = main
+        self._plan = plan
+
+    def forward(self, z):
+        return self._run(z)
+
+
+class _D0(_Net):
+    """DCGAN discriminator (GLI:400-460)."""
+
+    def __init__(self, p):
+        super().__init__()
+        self.param = p
+        main = nn.Sequential()
+        plan = []
+        sn = p.spectral
+        cls = SpectralConv2d if sn else Conv2d
+        start = cls(p.n_colors, p.D_h_size, 4, 2, 1, bias=False)
+        main.add_module("Start-SpectralConv2d" if sn else "Start-Conv2d", start)
+        if p.SELU:
+            main.add_module("Start-SELU", _Act("selu"))
+            plan.append(_Layer(start, None, "selu"))
+        elif p.Tanh_GD:
+            main.add_module("Start-Tanh", _Act("tanh"))
+            plan.append(_Layer(start, None, "tanh"))
+        else:
+            main.add_module("Start-LeakyReLU", _Act("lrelu", 0.2))
+            plan.append(_Layer(start, None, "lrelu", 0.2))
+        size, mult, i = p.image_size // 2, 1, 0
+        while size > 4:
+            cin, cout = p.D_h_size * mult, p.D_h_size * 2 * mult
+            conv = cls(cin, cout, 4, 2, 1, bias=False)
+            main.add_module(("Middle-SpectralConv2d [%d]" if sn else "Middle-Conv2d [%d]") % i, conv)
+            if p.SELU:
+                main.add_module("Middle-SELU [%d]" % i, _Act("selu"))
+                plan.append(_Layer(conv, None, "selu"))
+            else:
+                bn = None
+                if not p.no_batch_norm_D and not sn:
+                    bn = BatchNorm2d(cout)
+                    main.add_module("Middle-BatchNorm2d [%d]" % i, bn)
+                if p.Tanh_GD:
+                    main.add_module("Start-Tanh [%d]" % i, _Act("tanh"))  # the reference's name (GLI:435)
+                    plan.append(_Layer(conv, bn, "tanh"))
+                else:
+                    main.add_module("Middle-LeakyReLU [%d]" % i, _Act("lrelu", 0.2))
+                    plan.append(_Layer(conv, bn, "lrelu", 0.2))
+            size //= 2
+            mult *= 2
+            i += 1
+        end = cls(p.D_h_size * mult, 1, 4, 1, 0, bias=False)
+        main.add_module("End-SpectralConv2d" if sn else "End-Conv2d", end)
+        act = "none"
+        if p.loss_D == 1:
+            main.add_module("End-Sigmoid", _Act("sigmoid"))
+            act = "sigmoid"
+        plan.append(_Layer(end, None, act))
+        self.main = main
+        self._plan = plan
+
+    def forward(self, x):
+        return self._run(x).view(-1)
+
+
+# ---------------------------------------------------------------- arch 1 ("standard CNN", 32x32)
+class _G1(_Net):
+    """Standard-CNN generator (GLI:186-233)."""
+
+    def __init__(self, p):
+        super().__init__()
+        self.param = p
+        self.z_size = p.z_size
+        self.dense = Linear(p.z_size, 512 * 4 * 4)
+        layers, plan = [], []
+        # dense as a 1x1 conv on [B, z, 1, 1]; its [B, 8192] output is the NCHW [B,512,4,4]
+        plan.append(_lin_spec(_Layer(self.dense, None, "none", w_view=(8192, p.z_size, 1, 1),
+                                     in_view=(p.z_size, 1, 1), out_view=(512, 4, 4)),
+                              ConvGeom(1, 1, 0, False), "none"))
+        self.dense.geom = ConvGeom(1, 1, 0, False)
+        sn = p.spectral_G
+        for cin, cout in ((512, 256), (256, 128), (128, 64)):
+            conv = (SpectralConvTranspose2d if sn else ConvTranspose2d)(cin, cout, 4, 2, 1, bias=True)
+            layers.append(conv)
+            if sn:
+                layers.append(_Act("relu"))
+                plan.append(_Layer(conv, None, "relu"))
+                continue
+            bn = None
+            if not p.no_batch_norm_G:
+                bn = BatchNorm2d(cout)
+                layers.append(bn)
+            act = "tanh" if p.Tanh_GD else "relu"
+            layers.append(_Act(act))
+            plan.append(_Layer(conv, bn, act))
+        end = (SpectralConv2d if sn else Conv2d)(64, p.n_colors, 3, 1, 1, bias=True)
+        layers += [end, _Act("tanh")]
+        plan.append(_Layer(end, None, "tanh", nchw_out=True))
+        self.model = nn.Sequential(*layers)
+        self._plan = plan
+
+    def forward(self, z):
+        return self._run(z)
+
+
+class _D1(_Net):
+    """Standard-CNN discriminator (GLI:235-319)."""
+
+    SPEC = ((None, 64, 3, 1), (64, 64, 4, 2), (64, 128, 3, 1), (128, 128, 4, 2),
+            (128, 256, 3, 1), (256, 256, 4, 2), (256, 512, 3, 1))
+
+    def __init__(self, p):
+        super().__init__()
+        self.param = p
+        self.dense = Linear(512 * 4 * 4, 1)
+        layers, plan = [], []
+        sn = p.spectral
+        for idx, (cin, cout, k, s) in enumerate(self.SPEC):
+            cin = p.n_colors if cin is None else cin
+            conv = (SpectralConv2d if sn else Conv2d)(cin, cout, k, s, 1, bias=True)
+            layers.append(conv)
+            if sn:
+                layers.append(_Act("lrelu", 0.1))
+                plan.append(_Layer(conv, None, "lrelu", 0.1))
+                continue
+            bn = None
+            if not p.no_batch_norm_D and idx < len(self.SPEC) - 1:
+                bn = BatchNorm2d(cout)
+                layers.append(bn)
+            act = "tanh" if p.Tanh_GD else "lrelu"
+            layers.append(_Act(act, 0.1))
+            plan.append(_Layer(conv, bn, act, 0.1))
+        self.model = nn.Sequential(*layers)
+        self.sig = _Act("sigmoid")
+        # dense(view(-1, 512*4*4)) == a k4 conv over the [B,512,4,4] map with W viewed [1,512,4,4]
+        act = "sigmoid" if p.loss_D == 1 else "none"
+        plan.append(_lin_spec(_Layer(self.dense, None, act, w_view=(1, 512, 4, 4)), ConvGeom(4, 1, 0, False), act))
+        self.dense.geom = ConvGeom(4, 1, 0, False)
+        self._plan = plan
+
+    def forward(self, x):
+        return self._run(x).view(-1)
+
+
+def DCGAN_G(param):
+    """Generator for ``param.arch`` (0: DCGAN, 1: standard CNN), like GLI's DCGAN_G()."""
+    return _G1(param) if param.arch == 1 else _G0(param)
+
+
+def DCGAN_D(param):
+    """Discriminator for ``param.arch``, like GLI's DCGAN_D()."""
+    return _D1(param) if param.arch == 1 else _D0(param)
