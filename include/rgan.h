@@ -46,20 +46,29 @@ typedef struct RganConv {
   long long ys[4];         /* y strides (b, c, h, w) in elements */
 } RganConv;
 
-/* Workspace bytes needed by rgan_conv_{fwd,dgrad,wgrad}; `which` = 0 fwd, 1 dgrad, 2 wgrad. */
-size_t rgan_conv_workspace(const RganConv* d, int which);
+/* Workspace bytes needed by rgan_conv_{fwd,dgrad,wgrad}; `which` = 0 fwd, 1 dgrad, 2 wgrad;
+ * `prepacked` != 0: the caller passes packed weights (no packing scratch).  0 = unsupported. */
+size_t rgan_conv_workspace(const RganConv* d, int which, int prepacked);
 
-/* y = act(conv(x, w) * wscale + bias).  Replaces Conv2d/ConvTranspose2d.forward
+/* GEMM-ready weight layout for which = 0 (fwd) or 1 (dgrad): [phases][K][N] floats.
+ * Packing is separated so callers can cache it per weight version (weights change only
+ * at the optimizer step, but each net is run 2-4 times per iteration). */
+size_t rgan_conv_pack_floats(const RganConv* d, int which);
+int rgan_conv_pack(const RganConv* d, int which, const float* w, float* packed, void* stream);
+
+/* y = act(conv(x, w) * (*wscale) + bias).  Replaces Conv2d/ConvTranspose2d.forward
  * (GLI:336,361,387,410,428,448; arch 1 GLI:202-223,260-302) fused with the
- * following activation when no BatchNorm sits between them.  wscale: nullable device
- * scalar (spectral norm's 1/sigma, torch/nn/utils/spectral_norm.py:115-116). */
-int rgan_conv_fwd(const RganConv* d, const float* x, const float* w, const float* wscale,
-                  const float* bias, float* y, int act, float act_alpha,
+ * following activation when no BatchNorm sits between them.  wpacked: nullable
+ * rgan_conv_pack(which=0) output (then w may be NULL).  wscale: nullable device scalar
+ * (spectral norm's 1/sigma, torch/nn/utils/spectral_norm.py:115-116), applied to the
+ * accumulator in the epilogue. */
+int rgan_conv_fwd(const RganConv* d, const float* x, const float* w, const float* wpacked,
+                  const float* wscale, const float* bias, float* y, int act, float act_alpha,
                   void* ws, size_t ws_bytes, void* stream);
 
 /* dx = d conv / d x applied to dy  (aten convolution_backward, grad_input). */
-int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* w, const float* wscale,
-                    float* dx, void* ws, size_t ws_bytes, void* stream);
+int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* w, const float* wpacked,
+                    const float* wscale, float* dx, void* ws, size_t ws_bytes, void* stream);
 
 /* dw = d conv / d w applied to dy (aten convolution_backward, grad_weight), written
  * in torch weight layout; dbias (nullable) = per-output-channel sum of dy. */
@@ -80,11 +89,11 @@ int rgan_bn_apply(const float* y, long long P, int C, long long sp, long long sc
                   const float* stats, const float* gamma, const float* beta,
                   int act, float act_alpha, float* a, long long asp, long long asc, void* stream);
 /* Staged form for data parallelism (SyncBN): local moments (count, mean, M2) as
- * float[3][C]; the caller gathers them from all ranks into [nranks][3][C] and merges
+ * double[3][C]; the caller gathers them from all ranks into [nranks][3][C] and merges
  * in rank order with rgan_bn_finalize (Chan's parallel variance; deterministic). */
 int rgan_bn_moments(const float* y, long long P, int C, long long sp, long long sc,
-                    float* moments, void* partial, void* stream);
-int rgan_bn_finalize(const float* moments, int nranks, int C, float eps, float momentum,
+                    double* moments, void* partial, void* stream);
+int rgan_bn_finalize(const double* moments, int nranks, int C, float eps, float momentum,
                      float* running_mean, float* running_var, long long* num_batches_tracked,
                      float* stats, void* stream);
 /* Backward through act(BN(y)): given da, produce dy, dgamma, dbeta. */
@@ -93,16 +102,18 @@ int rgan_bn_backward(const float* da, long long dsp, long long dsc,
                      const float* stats, const float* gamma, const float* beta,
                      int act, float act_alpha, float* dy, long long ysp, long long ysc,
                      float* dgamma, float* dbeta, void* partial, void* stream);
-/* Staged backward: local sums[2][C] = (sum g, sum g*(y-mean)), g = da*act'; the caller
- * all-reduces them over ranks, then apply with the global pixel count P_global. */
+/* Staged backward: local sums double[2][C] = (sum g, sum g*(y-mean)), g = da*act'; the
+ * caller all-reduces them over ranks, then apply with the global pixel count P_global.
+ * All BN sums accumulate in double (torch's CPU kernel does too): the backward sums can
+ * cancel almost completely and a float accumulator leaves a coherent error in dy. */
 int rgan_bn_backward_sums(const float* da, long long dsp, long long dsc, const float* y,
                           long long P, int C, long long sp, long long sc, const float* stats,
                           const float* gamma, const float* beta, int act, float act_alpha,
-                          float* sums, void* partial, void* stream);
+                          double* sums, void* partial, void* stream);
 int rgan_bn_backward_apply(const float* da, long long dsp, long long dsc, const float* y,
                            long long P, int C, long long sp, long long sc, const float* stats,
                            const float* gamma, const float* beta, int act, float act_alpha,
-                           const float* sums, long long P_global, float* dy, long long ysp,
+                           const double* sums, long long P_global, float* dy, long long ysp,
                            long long ysc, float* dgamma, float* dbeta, void* stream);
 
 /* ---- elementwise ---- */

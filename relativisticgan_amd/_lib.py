@@ -27,9 +27,12 @@ class RganConv(ctypes.Structure):
 
 # name -> (restype, argtypes)
 _SIGS = {
-    "rgan_conv_workspace": (c_sz, [ctypes.POINTER(RganConv), c_int]),
-    "rgan_conv_fwd": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_vp, c_sz, c_vp]),
-    "rgan_conv_dgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "rgan_conv_workspace": (c_sz, [ctypes.POINTER(RganConv), c_int, c_int]),
+    "rgan_conv_pack_floats": (c_sz, [ctypes.POINTER(RganConv), c_int]),
+    "rgan_conv_pack": (c_int, [ctypes.POINTER(RganConv), c_int, c_vp, c_vp, c_vp]),
+    "rgan_conv_fwd": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_vp, c_sz,
+                              c_vp]),
+    "rgan_conv_dgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "rgan_conv_wgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "rgan_bn_partial_bytes": (c_sz, [c_ll, c_int]),
     "rgan_bn_stats": (c_int, [c_vp, c_ll, c_int, c_ll, c_ll, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -22,6 +22,13 @@ from . import dp
 from . import kernels as K
 
 
+# Test/diagnostic hook: when a list, every fused layer whose activation has a derivative
+# discontinuous at 0 (ReLU, LeakyReLU, SELU) appends the sign mask of its output, in call
+# order, so parity tests can count sign flips against an exact (fp64) forward.
+ACT_TRACE = None
+_KINKED = ("relu", "lrelu", "selu")
+
+
 class LayerSpec:
     """Static description of one fused layer."""
 
@@ -152,7 +159,7 @@ class ConvLayerFn(torch.autograd.Function):
         wscale = sn[2] if spec.spectral else None
         stats_eval = None
         if spec.bn:
-            y = K.conv_fwd(x, w, spec.geom, bias=bias, wscale=wscale)
+            y = K.conv_fwd(x, w, spec.geom, bias=bias, wscale=wscale, cache=True)
             rm, rv, nbt, training = bufs
             C = y.shape[1]
             if training:
@@ -168,8 +175,10 @@ class ConvLayerFn(torch.autograd.Function):
             ctx.save_for_backward(x, w, bias, gamma, beta, y, stats, *(sn if spec.spectral else ()))
         else:
             a = K.conv_fwd(x, w, spec.geom, bias=bias, act=spec.act, alpha=spec.alpha, wscale=wscale,
-                           nchw_out=spec.nchw_out)
+                           nchw_out=spec.nchw_out, cache=True)
             ctx.save_for_backward(x, w, bias, gamma, beta, a, None, *(sn if spec.spectral else ()))
+        if ACT_TRACE is not None and spec.act in _KINKED:
+            ACT_TRACE.append((a.detach() > 0).cpu())
         ctx.spec = spec
         ctx.stats_eval = stats_eval
         ctx.training = bufs[3] if bufs is not None else True
@@ -205,7 +214,7 @@ class ConvLayerFn(torch.autograd.Function):
             dy = K.act_backward(da, t5, spec.act, spec.alpha)
         else:
             dy = da
-        dx = K.conv_dgrad(dy, w, spec.geom, tuple(x.shape), wscale=wscale, like=x) if nx else None
+        dx = K.conv_dgrad(dy, w, spec.geom, tuple(x.shape), wscale=wscale, like=x, cache=True) if nx else None
         dw = db = None
         if nw or nb:
             dw, db = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), with_bias=bias is not None and nb)

@@ -1,129 +1,208 @@
-// BatchNorm2d (train mode) + activation kernels, NHWC ([P][C] with strides).
+// BatchNorm2d (train mode) + activation kernels on NHWC activations ([P][C], P = B*H*W).
 //
 // Replaces torch.nn.BatchNorm2d forward/backward in training mode and the activation
-// modules that follow it (GLI:341-345,366-370,433-437; arch 1 GLI:204-218,262-297).
-// Statistics: per (pixel-chunk, channel) Welford partials merged by Chan's formula in a
-// fixed order -> deterministic and free of the E[x^2]-E[x]^2 cancellation.
-// HBM-bound: algorithmic bytes per element are 4 (stats read) + 8 (apply read+write)
-// forward and 8 (reduce: da, y) + 12 (apply: da, y read, dy write) backward.
+// that follows it (GLI:341-345,366-370,433-437; arch 1 GLI:204-218,262-297).
+//
+// Numerics: per-thread sums are accumulated in double (torch's CPU kernel uses a double
+// accumulator too): the backward sums sum(g) and sum(g*(y-mean)) can cancel almost
+// completely when the upstream gradient lies near BN's null space, and a float sum
+// there leaves a coherent per-channel offset in dy.  Forward moments use shifted sums
+// (shift = the thread's first sample) in double; partials are merged with Chan's
+// parallel formula in a fixed order (deterministic, no E[x^2]-E[x]^2 cancellation).
+//
+// Layout/perf: the vector path gives every thread a fixed quad of 4 channels (float4
+// loads, no per-element index division) and walks pixels; HBM-bound with algorithmic
+// bytes per element 4 (moments) + 8 (apply) forward, 8 (sums: da, y) + 12 (apply: da,
+// y -> dy) backward.  Chunk partials are reduced by a parallel merge kernel.
 #include "common.h"
 
 namespace rgan {
 
-constexpr int BN_CG = 64;     // channels per block (one lane per channel)
-constexpr int BN_ROWS = 4;    // waves per block, each walks its own pixel rows
+// ------------------------------------------------------------------ geometry
+struct BnGeo {
+  bool vec;        // NHWC dense, C % 4 == 0
+  int Q;           // channels per thread (4 or 1)
+  int tpr;         // threads per pixel row (power of two)
+  int rp;          // pixel rows in flight per block (256 / tpr)
+  int cgroups;     // channel groups
+  int chunks;      // pixel chunks
+  long long rows;  // pixels per chunk
+};
 
-static int bn_chunks(long long P, int C) {
-  // aim for ~1024 blocks total, at least 64 pixels per chunk
-  const int cgroups = ceil_div(C, BN_CG);
-  long long want = std::max<long long>(1, 1024 / cgroups);
-  long long per = std::max<long long>(64, (P + want - 1) / want);
-  return ceil_div(P, per);
+static int pow2_floor(int v) {
+  int p = 1;
+  while (p * 2 <= v) p *= 2;
+  return p;
+}
+
+static BnGeo bn_geo(long long P, int C, long long sp, long long sc) {
+  BnGeo g;
+  g.vec = sc == 1 && sp == C && C % 4 == 0;
+  g.Q = g.vec ? 4 : 1;
+  const int cq = C / g.Q;
+  int t = 1;
+  if (g.vec) {
+    while (t < 64 && cq % (t * 2) == 0) t *= 2;
+  } else {
+    t = std::min(64, pow2_floor(C));
+  }
+  g.tpr = t;
+  g.rp = 256 / t;
+  g.cgroups = ceil_div(cq, t);
+  const long long want_blocks = 1024;
+  long long chunks = std::max<long long>(1, want_blocks / g.cgroups);
+  long long rows = (P + chunks - 1) / chunks;
+  rows = std::max<long long>(rows, (long long)g.rp * 4);
+  g.rows = rows;
+  g.chunks = ceil_div(P, rows);
+  return g;
+}
+
+static int max_chunks(long long P, int C) {
+  return std::max(bn_geo(P, C, C, 1).chunks, bn_geo(P, C, 1, 2).chunks);
 }
 
 extern "C" size_t rgan_bn_partial_bytes(long long P, int C) {
-  return ((size_t)bn_chunks(P, C) * 3 + 3) * C * sizeof(float) + 256;
+  // [chunks][2][C] partial sums + [2][C] merged sums + [3][C] moments, doubles
+  return ((size_t)max_chunks(P, C) * 2 + 5) * C * sizeof(double) + 256;
 }
 
-// partial layout: [chunk][3][C] = (count, mean, M2)
-__global__ __launch_bounds__(256) void bn_stats_partial(const float* __restrict__ y, long long P, int C,
-                                                        long long sp, long long sc, int chunks,
-                                                        float* __restrict__ part) {
-  __shared__ float sh[3][BN_ROWS][BN_CG];
-  const int lane = threadIdx.x & 63, row = threadIdx.x >> 6;
-  const int c = blockIdx.y * BN_CG + lane;
-  const int chunk = blockIdx.x;
-  const long long per = (P + chunks - 1) / chunks;
-  const long long p0 = chunk * per, p1 = min(P, p0 + per);
-  float n = 0.f, mean = 0.f, m2 = 0.f;
-  if (c < C) {
-    for (long long p = p0 + row; p < p1; p += BN_ROWS) {
-      const float v = y[p * sp + c * sc];
-      n += 1.f;
-      const float d = v - mean;
-      mean += d / n;
-      m2 += d * (v - mean);
+template <int Q>
+__device__ __forceinline__ void load_q(const float* __restrict__ y, long long off, float (&v)[Q]) {
+  if constexpr (Q == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(y + off);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  } else {
+    v[0] = y[off];
+  }
+}
+
+__device__ __forceinline__ void chan_merge(double& N, double& M, double& S, double nb, double mb, double sb) {
+  if (nb == 0.0) return;
+  const double nt = N + nb, d = mb - M;
+  M += d * (nb / nt);
+  S += sb + d * d * (N * nb / nt);
+  N = nt;
+}
+
+// ------------------------------------------------------------------ forward moments
+// Shifted sums with ONE shift per channel (its first pixel, y[0][c]) shared by every
+// block: partials are plain (sum d, sum d^2), d = y - shift, accumulated in double, so
+// the merge is a division-free parallel sum.  partial layout: [chunk][2][C] doubles.
+template <int Q>
+__global__ __launch_bounds__(256) void bn_moments_partial(const float* __restrict__ y, long long P, int C,
+                                                          long long sp, long long sc, int tpr, long long rows,
+                                                          double* __restrict__ part) {
+  __shared__ double sh[2][256][Q];
+  const int tid = threadIdx.x, lc = tid % tpr, rl = tid / tpr, rp = blockDim.x / tpr;
+  const int c0 = (blockIdx.y * tpr + lc) * Q;
+  const long long p0 = blockIdx.x * rows, p1 = min(P, p0 + rows);
+  double s1[Q], s2[Q];
+  float sft[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) { s1[q] = 0.0; s2[q] = 0.0; sft[q] = 0.f; }
+  if (c0 < C) {
+    load_q<Q>(y, (long long)c0 * sc, sft);
+    for (long long p = p0 + rl; p < p1; p += rp) {
+      float v[Q];
+      load_q<Q>(y, p * sp + (long long)c0 * sc, v);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const double d = (double)(v[q] - sft[q]);
+        s1[q] += d;
+        s2[q] += d * d;
+      }
     }
   }
-  sh[0][row][lane] = n; sh[1][row][lane] = mean; sh[2][row][lane] = m2;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) { sh[0][tid][q] = s1[q]; sh[1][tid][q] = s2[q]; }
   __syncthreads();
-  if (row == 0 && c < C) {
-    float N = sh[0][0][lane], M = sh[1][0][lane], S = sh[2][0][lane];
-    for (int r = 1; r < BN_ROWS; ++r) {
-      const float nb = sh[0][r][lane];
-      if (nb == 0.f) continue;
-      const float mb = sh[1][r][lane], sb = sh[2][r][lane];
-      const float nt = N + nb, d = mb - M;
-      M += d * (nb / nt);
-      S += sb + d * d * (N * nb / nt);
-      N = nt;
+  if (rl == 0 && c0 < C) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      if (c0 + q < C) {
+        double a1 = 0.0, a2 = 0.0;
+        for (int r = 0; r < rp; ++r) { a1 += sh[0][r * tpr + lc][q]; a2 += sh[1][r * tpr + lc][q]; }
+        part[((size_t)blockIdx.x * 2 + 0) * C + c0 + q] = a1;
+        part[((size_t)blockIdx.x * 2 + 1) * C + c0 + q] = a2;
+      }
     }
-    part[((size_t)chunk * 3 + 0) * C + c] = N;
-    part[((size_t)chunk * 3 + 1) * C + c] = M;
-    part[((size_t)chunk * 3 + 2) * C + c] = S;
   }
 }
 
-// chunk partials -> per-channel moments (count, mean, M2) of this rank's batch
-__global__ void bn_moments_reduce(const float* __restrict__ part, int chunks, int C, float* __restrict__ mom) {
+// [k][2][C] partial sums -> sums[2][C]; block = 64 channels x 16 lanes, fixed order
+__global__ __launch_bounds__(1024) void bn_sums_merge(const double* __restrict__ part, int chunks, int C,
+                                                      double* __restrict__ sums) {
+  __shared__ double sh[2][16][64];
+  const int lane = threadIdx.x & 63, ml = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  double a1 = 0.0, a2 = 0.0;
+  if (c < C)
+    for (int k = ml; k < chunks; k += 16) {
+      a1 += part[((size_t)k * 2 + 0) * C + c];
+      a2 += part[((size_t)k * 2 + 1) * C + c];
+    }
+  sh[0][ml][lane] = a1; sh[1][ml][lane] = a2;
+  __syncthreads();
+  if (ml == 0 && c < C) {
+    double t1 = 0.0, t2 = 0.0;
+    for (int r = 0; r < 16; ++r) { t1 += sh[0][r][lane]; t2 += sh[1][r][lane]; }
+    sums[c] = t1;
+    sums[C + c] = t2;
+  }
+}
+
+// shifted sums -> moments (count, mean, M2)
+__global__ void bn_sums_to_moments(const double* __restrict__ sums, const float* __restrict__ y, long long P,
+                                   int C, long long sc, double* __restrict__ mom) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  double N = 0.0, M = 0.0, S = 0.0;
-  for (int k = 0; k < chunks; ++k) {
-    const double nb = part[((size_t)k * 3 + 0) * C + c];
-    if (nb == 0.0) continue;
-    const double mb = part[((size_t)k * 3 + 1) * C + c], sb = part[((size_t)k * 3 + 2) * C + c];
-    const double nt = N + nb, d = mb - M;
-    M += d * (nb / nt);
-    S += sb + d * d * (N * nb / nt);
-    N = nt;
-  }
-  mom[c] = (float)N;
-  mom[C + c] = (float)M;
-  mom[2 * C + c] = (float)S;
+  const double n = (double)P, s1 = sums[c], s2 = sums[C + c];
+  mom[c] = n;
+  mom[C + c] = (double)y[(long long)c * sc] + s1 / n;
+  mom[2 * C + c] = fmax(s2 - s1 * s1 / n, 0.0);
 }
 
-// merge `nranks` moment blocks [r][3][C] in rank order -> (mean, invstd), running stats
-__global__ void bn_finalize_kernel(const float* __restrict__ mom, int nranks, int C, float eps, float momentum,
+// merge `nranks` moment blocks [r][3][C] in rank order -> (mean, invstd) float, running stats
+__global__ void bn_finalize_kernel(const double* __restrict__ mom, int nranks, int C, float eps, float momentum,
                                    float* running_mean, float* running_var, long long* nbt, float* stats) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c == 0 && nbt) nbt[0] += 1;
   if (c >= C) return;
   double N = 0.0, M = 0.0, S = 0.0;
-  for (int k = 0; k < nranks; ++k) {
-    const double nb = mom[((size_t)k * 3 + 0) * C + c];
-    if (nb == 0.0) continue;
-    const double mb = mom[((size_t)k * 3 + 1) * C + c], sb = mom[((size_t)k * 3 + 2) * C + c];
-    const double nt = N + nb, d = mb - M;
-    M += d * (nb / nt);
-    S += sb + d * d * (N * nb / nt);
-    N = nt;
-  }
-  const float mean = (float)M;
-  const float var = (float)(S / N);
-  stats[c] = mean;
-  stats[C + c] = 1.f / sqrtf(var + eps);
-  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mean;
+  for (int k = 0; k < nranks; ++k)
+    chan_merge(N, M, S, mom[((size_t)k * 3 + 0) * C + c], mom[((size_t)k * 3 + 1) * C + c],
+               mom[((size_t)k * 3 + 2) * C + c]);
+  const double var = S / N;
+  stats[c] = (float)M;
+  stats[C + c] = (float)(1.0 / sqrt(var + (double)eps));
+  if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)M;
   if (running_var) {
-    const float unb = N > 1.0 ? (float)(S / (N - 1.0)) : var;
+    const float unb = N > 1.0 ? (float)(S / (N - 1.0)) : (float)var;
     running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
   }
 }
 
-extern "C" int rgan_bn_moments(const float* y, long long P, int C, long long sp, long long sc, float* moments,
+extern "C" int rgan_bn_moments(const float* y, long long P, int C, long long sp, long long sc, double* moments,
                                void* partial, void* stream) {
   RGAN_REQUIRE(y && moments && partial && P > 0 && C > 0);
   hipStream_t s = (hipStream_t)stream;
-  const int chunks = bn_chunks(P, C);
-  float* part = (float*)partial;
-  bn_stats_partial<<<dim3(chunks, ceil_div(C, BN_CG)), 256, 0, s>>>(y, P, C, sp, sc, chunks, part);
+  BnGeo g = bn_geo(P, C, sp, sc);
+  if (g.vec && ((uintptr_t)y & 15)) g = bn_geo(P, C, 1, 2);
+  double* part = (double*)partial;
+  double* sums = part + (size_t)g.chunks * 2 * C;
+  dim3 grid(g.chunks, g.cgroups);
+  if (g.vec) bn_moments_partial<4><<<grid, 256, 0, s>>>(y, P, C, sp, sc, g.tpr, g.rows, part);
+  else bn_moments_partial<1><<<grid, 256, 0, s>>>(y, P, C, sp, sc, g.tpr, g.rows, part);
   RGAN_CHECK_LAUNCH();
-  bn_moments_reduce<<<ceil_div(C, 256), 256, 0, s>>>(part, chunks, C, moments);
+  bn_sums_merge<<<ceil_div(C, 64), 1024, 0, s>>>(part, g.chunks, C, sums);
+  RGAN_CHECK_LAUNCH();
+  bn_sums_to_moments<<<ceil_div(C, 256), 256, 0, s>>>(sums, y, P, C, sc, moments);
   RGAN_CHECK_LAUNCH();
   return 0;
 }
 
-extern "C" int rgan_bn_finalize(const float* moments, int nranks, int C, float eps, float momentum,
+extern "C" int rgan_bn_finalize(const double* moments, int nranks, int C, float eps, float momentum,
                                 float* running_mean, float* running_var, long long* num_batches_tracked,
                                 float* stats, void* stream) {
   RGAN_REQUIRE(moments && stats && nranks > 0 && C > 0);
@@ -138,58 +217,50 @@ extern "C" int rgan_bn_stats(const float* y, long long P, int C, long long sp, l
                              float momentum, float* running_mean, float* running_var,
                              long long* num_batches_tracked, float* stats, void* partial, void* stream) {
   RGAN_REQUIRE(y && stats && partial && P > 0 && C > 0);
-  const int chunks = bn_chunks(P, C);
-  float* mom = (float*)partial + (size_t)chunks * 3 * C;
+  double* mom = (double*)partial + ((size_t)max_chunks(P, C) * 2 + 2) * C;
   int rc = rgan_bn_moments(y, P, C, sp, sc, mom, partial, stream);
   if (rc) return rc;
   return rgan_bn_finalize(mom, 1, C, eps, momentum, running_mean, running_var, num_batches_tracked, stats,
                           stream);
 }
 
-// a = act(y*alpha_c + beta_c), alpha_c = gamma*invstd, beta_c = beta - mean*alpha_c
+// ------------------------------------------------------------------ apply
+// per-thread fixed channel quad (blockIdx.x = channel group); pixels strided over blockIdx.y
+template <int Q>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ y, long long P, int C,
-                                                       long long sp, long long sc,
-                                                       const float* __restrict__ stats,
+                                                       long long sp, long long sc, const float* __restrict__ stats,
                                                        const float* __restrict__ gamma,
-                                                       const float* __restrict__ beta, int act,
-                                                       float alpha, float* __restrict__ a, long long asp,
-                                                       long long asc) {
-  const long long total = P * C;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long p = i / C;
-    const int c = (int)(i - p * C);
-    const float al = (gamma ? gamma[c] : 1.f) * stats[C + c];
-    const float be = (beta ? beta[c] : 0.f) - stats[c] * al;
-    a[p * asp + c * asc] = act_fwd(y[p * sp + c * sc] * al + be, act, alpha);
-  }
-}
-
-// vectorised NHWC form (sc == asc == 1, sp == asp == C, C % 4 == 0)
-__global__ __launch_bounds__(256) void bn_apply_vec(const float4* __restrict__ y, long long n4, int C,
-                                                    const float* __restrict__ stats,
-                                                    const float* __restrict__ gamma,
-                                                    const float* __restrict__ beta, int act, float alpha,
-                                                    float4* __restrict__ a) {
-  const int C4 = C >> 2;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C4) * 4;
-    float4 v = y[i];
-    float r[4] = {v.x, v.y, v.z, v.w};
+                                                       const float* __restrict__ beta, int act, float alpha,
+                                                       float* __restrict__ a, long long asp, long long asc,
+                                                       int tpr) {
+  const int tid = threadIdx.x, lc = tid % tpr, rl = tid / tpr, rp = blockDim.x / tpr;
+  const int c0 = (blockIdx.x * tpr + lc) * Q;
+  if (c0 >= C) return;
+  float al[Q], be[Q];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float al = (gamma ? gamma[c + j] : 1.f) * stats[C + c + j];
-      const float be = (beta ? beta[c + j] : 0.f) - stats[c + j] * al;
-      r[j] = act_fwd(r[j] * al + be, act, alpha);
+  for (int q = 0; q < Q; ++q) {
+    const int c = min(c0 + q, C - 1);
+    al[q] = (gamma ? gamma[c] : 1.f) * stats[C + c];
+    be[q] = (beta ? beta[c] : 0.f) - stats[c] * al[q];
+  }
+  const long long step = (long long)gridDim.y * rp;
+  for (long long p = (long long)blockIdx.y * rp + rl; p < P; p += step) {
+    float v[Q];
+    load_q<Q>(y, p * sp + (long long)c0 * sc, v);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) v[q] = act_fwd(v[q] * al[q] + be[q], act, alpha);
+    if constexpr (Q == 4) {
+      *reinterpret_cast<float4*>(a + p * asp + c0) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      a[p * asp + (long long)c0 * asc] = v[0];
     }
-    a[i] = make_float4(r[0], r[1], r[2], r[3]);
   }
 }
 
-static int grid_for(long long n, int per_thread = 1) {
-  long long b = (n / per_thread + 255) / 256;
-  return (int)std::max<long long>(1, std::min<long long>(b, 8192));
+static dim3 apply_grid(const BnGeo& g, long long P) {
+  const long long rb = std::max<long long>(
+      1, std::min<long long>((P + g.rp - 1) / g.rp, std::max(1, 4096 / g.cgroups)));
+  return dim3(g.cgroups, (unsigned)rb);
 }
 
 extern "C" int rgan_bn_apply(const float* y, long long P, int C, long long sp, long long sc,
@@ -197,124 +268,161 @@ extern "C" int rgan_bn_apply(const float* y, long long P, int C, long long sp, l
                              float act_alpha, float* a, long long asp, long long asc, void* stream) {
   RGAN_REQUIRE(y && stats && a && P > 0 && C > 0);
   hipStream_t s = (hipStream_t)stream;
-  const bool vec = sc == 1 && asc == 1 && sp == C && asp == C && C % 4 == 0 &&
-                   ((uintptr_t)y & 15) == 0 && ((uintptr_t)a & 15) == 0;
-  if (vec) {
-    const long long n4 = P * C / 4;
-    bn_apply_vec<<<grid_for(n4), 256, 0, s>>>((const float4*)y, n4, C, stats, gamma, beta, act, act_alpha,
-                                             (float4*)a);
-  } else {
-    bn_apply_kernel<<<grid_for(P * C), 256, 0, s>>>(y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, a,
-                                                   asp, asc);
-  }
+  BnGeo g = bn_geo(P, C, sp, sc);
+  const bool vec = g.vec && asc == 1 && asp == C && ((uintptr_t)y & 15) == 0 && ((uintptr_t)a & 15) == 0;
+  if (!vec && g.vec) g = bn_geo(P, C, 1, 2);
+  if (vec)
+    bn_apply_kernel<4><<<apply_grid(g, P), 256, 0, s>>>(y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, a,
+                                                       asp, asc, g.tpr);
+  else
+    bn_apply_kernel<1><<<apply_grid(g, P), 256, 0, s>>>(y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, a,
+                                                       asp, asc, g.tpr);
   RGAN_CHECK_LAUNCH();
   return 0;
 }
 
-// backward reduce: per (chunk, channel) sum g and sum g*(y-mean), g = da * act'(z)
-__global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ da, long long dsp,
-                                                      long long dsc, const float* __restrict__ y,
-                                                      long long P, int C, long long sp, long long sc,
-                                                      const float* __restrict__ stats,
+// ------------------------------------------------------------------ backward
+// partial [chunk][2][C] doubles: sum g, sum g*(y-mean);  g = da * act'(y*al + be)
+template <int Q>
+__global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ da, long long dsp, long long dsc,
+                                                      const float* __restrict__ y, long long P, int C, long long sp,
+                                                      long long sc, const float* __restrict__ stats,
                                                       const float* __restrict__ gamma,
-                                                      const float* __restrict__ beta, int act, float alpha,
-                                                      int chunks, float* __restrict__ part) {
-  __shared__ float sh[2][BN_ROWS][BN_CG];
-  const int lane = threadIdx.x & 63, row = threadIdx.x >> 6;
-  const int c = blockIdx.y * BN_CG + lane;
-  const int chunk = blockIdx.x;
-  const long long per = (P + chunks - 1) / chunks;
-  const long long p0 = chunk * per, p1 = min(P, p0 + per);
-  float s1 = 0.f, s2 = 0.f;
-  if (c < C) {
-    const float mean = stats[c], inv = stats[C + c];
-    const float al = (gamma ? gamma[c] : 1.f) * inv;
-    const float be = (beta ? beta[c] : 0.f) - mean * al;
-    for (long long p = p0 + row; p < p1; p += BN_ROWS) {
-      const float v = y[p * sp + c * sc];
-      const float gz = da[p * dsp + c * dsc] * act_grad_from_in(v * al + be, act, alpha);
-      s1 += gz;
-      s2 += gz * (v - mean);
+                                                      const float* __restrict__ beta, int act, float alpha, int tpr,
+                                                      long long rows, double* __restrict__ part) {
+  __shared__ double sh[2][256][Q];
+  const int tid = threadIdx.x, lc = tid % tpr, rl = tid / tpr, rp = blockDim.x / tpr;
+  const int c0 = (blockIdx.y * tpr + lc) * Q;
+  const long long p0 = blockIdx.x * rows, p1 = min(P, p0 + rows);
+  double s1[Q], s2[Q];
+  float mean[Q], al[Q], be[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    s1[q] = 0.0; s2[q] = 0.0;
+    const int c = min(c0 + q, C - 1);
+    mean[q] = stats[c];
+    al[q] = (gamma ? gamma[c] : 1.f) * stats[C + c];
+    be[q] = (beta ? beta[c] : 0.f) - mean[q] * al[q];
+  }
+  if (c0 < C) {
+    for (long long p = p0 + rl; p < p1; p += rp) {
+      float v[Q], g[Q];
+      load_q<Q>(y, p * sp + (long long)c0 * sc, v);
+      load_q<Q>(da, p * dsp + (long long)c0 * dsc, g);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const double gz = (double)(g[q] * act_grad_from_in(v[q] * al[q] + be[q], act, alpha));
+        s1[q] += gz;
+        s2[q] += gz * (double)(v[q] - mean[q]);
+      }
     }
   }
-  sh[0][row][lane] = s1; sh[1][row][lane] = s2;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) { sh[0][tid][q] = s1[q]; sh[1][tid][q] = s2[q]; }
   __syncthreads();
-  if (row == 0 && c < C) {
-    float a1 = 0.f, a2 = 0.f;
-    for (int r = 0; r < BN_ROWS; ++r) { a1 += sh[0][r][lane]; a2 += sh[1][r][lane]; }
-    part[((size_t)chunk * 2 + 0) * C + c] = a1;
-    part[((size_t)chunk * 2 + 1) * C + c] = a2;
+  if (rl == 0 && c0 < C) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      if (c0 + q < C) {
+        double a1 = 0.0, a2 = 0.0;
+        for (int r = 0; r < rp; ++r) { a1 += sh[0][r * tpr + lc][q]; a2 += sh[1][r * tpr + lc][q]; }
+        part[((size_t)blockIdx.x * 2 + 0) * C + c0 + q] = a1;
+        part[((size_t)blockIdx.x * 2 + 1) * C + c0 + q] = a2;
+      }
+    }
   }
-}
-
-// chunk partials -> this rank's per-channel (sum g, sum g*(y-mean)) = sums[2][C]
-__global__ void bn_bwd_sums_reduce(const float* __restrict__ part, int chunks, int C, float* __restrict__ sums) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double a1 = 0.0, a2 = 0.0;
-  for (int k = 0; k < chunks; ++k) {
-    a1 += part[((size_t)k * 2 + 0) * C + c];
-    a2 += part[((size_t)k * 2 + 1) * C + c];
-  }
-  sums[c] = (float)a1;
-  sums[C + c] = (float)a2;
 }
 
 // dy = al*(g - sum_g/Pg - (y-mean)*invstd^2*sum_gx/Pg); dgamma = invstd*sum_gx, dbeta = sum_g
-__global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ da, long long dsp,
-                                                    long long dsc, const float* __restrict__ y, long long P,
-                                                    int C, long long sp, long long sc,
-                                                    const float* __restrict__ stats,
+template <int Q>
+__global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ da, long long dsp, long long dsc,
+                                                    const float* __restrict__ y, long long P, int C, long long sp,
+                                                    long long sc, const float* __restrict__ stats,
                                                     const float* __restrict__ gamma,
                                                     const float* __restrict__ beta, int act, float alpha,
-                                                    const float* __restrict__ sums, float inv_pg,
+                                                    const double* __restrict__ sums, double inv_pg,
                                                     float* __restrict__ dy, long long ysp, long long ysc,
-                                                    float* dgamma, float* dbeta) {
-  const long long total = P * C;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long p = i / C;
-    const int c = (int)(i - p * C);
-    const float mean = stats[c], inv = stats[C + c];
-    const float al = (gamma ? gamma[c] : 1.f) * inv;
-    const float be = (beta ? beta[c] : 0.f) - mean * al;
-    const float k1 = sums[c] * inv_pg, k2 = sums[C + c] * inv * inv * inv_pg;
-    const float v = y[p * sp + c * sc];
-    const float gz = da[p * dsp + c * dsc] * act_grad_from_in(v * al + be, act, alpha);
-    dy[p * ysp + c * ysc] = al * (gz - k1 - (v - mean) * k2);
-    if (p == 0) {
-      if (dbeta) dbeta[c] = sums[c];
-      if (dgamma) dgamma[c] = sums[C + c] * inv;
+                                                    float* dgamma, float* dbeta, int tpr) {
+  const int tid = threadIdx.x, lc = tid % tpr, rl = tid / tpr, rp = blockDim.x / tpr;
+  const int c0 = (blockIdx.x * tpr + lc) * Q;
+  if (c0 >= C) return;
+  float mean[Q], al[Q], be[Q], k1[Q], k2[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int c = min(c0 + q, C - 1);
+    const float inv = stats[C + c];
+    mean[q] = stats[c];
+    al[q] = (gamma ? gamma[c] : 1.f) * inv;
+    be[q] = (beta ? beta[c] : 0.f) - mean[q] * al[q];
+    k1[q] = (float)(sums[c] * inv_pg);
+    k2[q] = (float)(sums[C + c] * (double)inv * (double)inv * inv_pg);
+    if (blockIdx.y == 0 && rl == 0 && c0 + q < C) {
+      if (dbeta) dbeta[c] = (float)sums[c];
+      if (dgamma) dgamma[c] = (float)(sums[C + c] * (double)inv);
     }
   }
+  const long long step = (long long)gridDim.y * rp;
+  for (long long p = (long long)blockIdx.y * rp + rl; p < P; p += step) {
+    float v[Q], g[Q];
+    load_q<Q>(y, p * sp + (long long)c0 * sc, v);
+    load_q<Q>(da, p * dsp + (long long)c0 * dsc, g);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const float gz = g[q] * act_grad_from_in(v[q] * al[q] + be[q], act, alpha);
+      v[q] = al[q] * (gz - k1[q] - (v[q] - mean[q]) * k2[q]);
+    }
+    if constexpr (Q == 4) {
+      *reinterpret_cast<float4*>(dy + p * ysp + c0) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      dy[p * ysp + (long long)c0 * ysc] = v[0];
+    }
+  }
+}
+
+static bool dense_nhwc(long long sp, long long sc, int C, const void* p) {
+  return sc == 1 && sp == C && ((uintptr_t)p & 15) == 0;
 }
 
 extern "C" int rgan_bn_backward_sums(const float* da, long long dsp, long long dsc, const float* y, long long P,
                                      int C, long long sp, long long sc, const float* stats, const float* gamma,
-                                     const float* beta, int act, float act_alpha, float* sums, void* partial,
+                                     const float* beta, int act, float act_alpha, double* sums, void* partial,
                                      void* stream) {
   RGAN_REQUIRE(da && y && stats && sums && partial && P > 0 && C > 0);
   hipStream_t s = (hipStream_t)stream;
-  const int chunks = bn_chunks(P, C);
-  float* part = (float*)partial;
-  bn_bwd_partial<<<dim3(chunks, ceil_div(C, BN_CG)), 256, 0, s>>>(da, dsp, dsc, y, P, C, sp, sc, stats,
-                                                                   gamma, beta, act, act_alpha, chunks, part);
+  BnGeo g = bn_geo(P, C, sp, sc);
+  const bool vec = g.vec && dense_nhwc(sp, sc, C, y) && dense_nhwc(dsp, dsc, C, da);
+  if (!vec && g.vec) g = bn_geo(P, C, 1, 2);
+  double* part = (double*)partial;
+  dim3 grid(g.chunks, g.cgroups);
+  if (vec)
+    bn_bwd_partial<4><<<grid, 256, 0, s>>>(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act, act_alpha,
+                                           g.tpr, g.rows, part);
+  else
+    bn_bwd_partial<1><<<grid, 256, 0, s>>>(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act, act_alpha,
+                                           g.tpr, g.rows, part);
   RGAN_CHECK_LAUNCH();
-  bn_bwd_sums_reduce<<<ceil_div(C, 256), 256, 0, s>>>(part, chunks, C, sums);
+  bn_sums_merge<<<ceil_div(C, 64), 1024, 0, s>>>(part, g.chunks, C, sums);
   RGAN_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int rgan_bn_backward_apply(const float* da, long long dsp, long long dsc, const float* y, long long P,
                                       int C, long long sp, long long sc, const float* stats, const float* gamma,
-                                      const float* beta, int act, float act_alpha, const float* sums,
+                                      const float* beta, int act, float act_alpha, const double* sums,
                                       long long P_global, float* dy, long long ysp, long long ysc, float* dgamma,
                                       float* dbeta, void* stream) {
   RGAN_REQUIRE(da && y && stats && sums && dy && P > 0 && C > 0 && P_global >= P);
-  bn_bwd_apply<<<grid_for(P * C), 256, 0, (hipStream_t)stream>>>(da, dsp, dsc, y, P, C, sp, sc, stats, gamma,
-                                                                 beta, act, act_alpha, sums,
-                                                                 1.f / (float)P_global, dy, ysp, ysc, dgamma,
-                                                                 dbeta);
+  hipStream_t s = (hipStream_t)stream;
+  BnGeo g = bn_geo(P, C, sp, sc);
+  const bool vec = g.vec && dense_nhwc(sp, sc, C, y) && dense_nhwc(dsp, dsc, C, da) && dense_nhwc(ysp, ysc, C, dy);
+  if (!vec && g.vec) g = bn_geo(P, C, 1, 2);
+  const double inv_pg = 1.0 / (double)P_global;
+  if (vec)
+    bn_bwd_apply<4><<<apply_grid(g, P), 256, 0, s>>>(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act,
+                                                    act_alpha, sums, inv_pg, dy, ysp, ysc, dgamma, dbeta, g.tpr);
+  else
+    bn_bwd_apply<1><<<apply_grid(g, P), 256, 0, s>>>(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act,
+                                                    act_alpha, sums, inv_pg, dy, ysp, ysc, dgamma, dbeta, g.tpr);
   RGAN_CHECK_LAUNCH();
   return 0;
 }
@@ -323,9 +431,8 @@ extern "C" int rgan_bn_backward(const float* da, long long dsp, long long dsc, c
                                 int C, long long sp, long long sc, const float* stats, const float* gamma,
                                 const float* beta, int act, float act_alpha, float* dy, long long ysp,
                                 long long ysc, float* dgamma, float* dbeta, void* partial, void* stream) {
-  RGAN_REQUIRE(partial);
-  const int chunks = bn_chunks(P, C);
-  float* sums = (float*)partial + (size_t)chunks * 2 * C;
+  RGAN_REQUIRE(partial && P > 0 && C > 0);
+  double* sums = (double*)partial + (size_t)max_chunks(P, C) * 2 * C;
   int rc = rgan_bn_backward_sums(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, sums,
                                  partial, stream);
   if (rc) return rc;
@@ -335,9 +442,18 @@ extern "C" int rgan_bn_backward(const float* da, long long dsp, long long dsc, c
 
 // ------------------------------------------------------------------ activations
 __global__ void act_bwd_kernel(const float* __restrict__ da, const float* __restrict__ a, long long n, int act,
-                               float alpha, float* __restrict__ dx) {
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n;
-       i += (long long)gridDim.x * blockDim.x)
+                               float alpha, float* __restrict__ dx, int vec) {
+  const long long n4 = vec ? n >> 2 : 0;
+  const float4* da4 = reinterpret_cast<const float4*>(da);
+  const float4* a4 = reinterpret_cast<const float4*>(a);
+  float4* dx4 = reinterpret_cast<float4*>(dx);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 g = da4[i], v = a4[i];
+    dx4[i] = make_float4(g.x * act_grad_from_out(v.x, act, alpha), g.y * act_grad_from_out(v.y, act, alpha),
+                         g.z * act_grad_from_out(v.z, act, alpha), g.w * act_grad_from_out(v.w, act, alpha));
+  }
+  for (long long i = (n4 << 2) + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
     dx[i] = da[i] * act_grad_from_out(a[i], act, alpha);
 }
 
@@ -345,30 +461,32 @@ extern "C" int rgan_act_backward(const float* da, const float* a, long long n, i
                                  float* dx, void* stream) {
   RGAN_REQUIRE(da && a && dx && n >= 0);
   if (n == 0) return 0;
-  act_bwd_kernel<<<grid_for(n), 256, 0, (hipStream_t)stream>>>(da, a, n, act, act_alpha, dx);
+  const int vec = ((((uintptr_t)da | (uintptr_t)a | (uintptr_t)dx) & 15) == 0) ? 1 : 0;
+  const int blocks = (int)std::max<long long>(1, std::min<long long>((n / 4 + 255) / 256, 4096));
+  act_bwd_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(da, a, n, act, act_alpha, dx, vec);
   RGAN_CHECK_LAUNCH();
   return 0;
 }
 
-// per-channel sum over pixels (bias gradients); one block per 64 channels, fixed order
+// per-channel sum over pixels (bias gradients); one block per 64 channels, fixed order, double
 __global__ __launch_bounds__(256) void channel_sum_kernel(const float* __restrict__ t, long long P, int C,
                                                           long long sp, long long sc, float* __restrict__ out) {
-  __shared__ float sh[BN_ROWS][BN_CG];
+  __shared__ double sh[4][64];
   const int lane = threadIdx.x & 63, row = threadIdx.x >> 6;
-  const int c = blockIdx.x * BN_CG + lane;
-  float s = 0.f;
+  const int c = blockIdx.x * 64 + lane;
+  double s = 0.0;
   if (c < C)
-    for (long long p = row; p < P; p += BN_ROWS) s += t[p * sp + c * sc];
+    for (long long p = row; p < P; p += 4) s += t[p * sp + c * sc];
   sh[row][lane] = s;
   __syncthreads();
-  if (row == 0 && c < C) out[c] = sh[0][lane] + sh[1][lane] + sh[2][lane] + sh[3][lane];
+  if (row == 0 && c < C) out[c] = (float)(sh[0][lane] + sh[1][lane] + sh[2][lane] + sh[3][lane]);
 }
 
 extern "C" int rgan_channel_sum(const float* t, long long P, int C, long long sp, long long sc, float* out,
                                 void* partial, void* stream) {
   (void)partial;
   RGAN_REQUIRE(t && out && P > 0 && C > 0);
-  channel_sum_kernel<<<ceil_div(C, BN_CG), 256, 0, (hipStream_t)stream>>>(t, P, C, sp, sc, out);
+  channel_sum_kernel<<<ceil_div(C, 64), 256, 0, (hipStream_t)stream>>>(t, P, C, sp, sc, out);
   RGAN_CHECK_LAUNCH();
   return 0;
 }

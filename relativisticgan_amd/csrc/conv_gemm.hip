@@ -74,6 +74,7 @@ struct GemmArgs {
   float* C;
   OutMap out;
   const float* bias;
+  const float* wscale;    // nullable device scalar multiplying the accumulator (spectral 1/sigma)
   int act;
   float alpha;
   float* slab;
@@ -445,6 +446,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
       }
     return;
   }
+  const float wsc = g.wscale ? g.wscale[0] : 1.f;
   long long* moff = reinterpret_cast<long long*>(smem);
   long long* noff = moff + BM;
   for (int i = tid; i < BM; i += 256) {
@@ -467,7 +469,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
       for (int r = 0; r < 16; ++r) {
         const int rl = wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
         if (m0 + rl < g.M && col < g.N) {
-          float v = acc[i][j][r] + bv;
+          float v = acc[i][j][r] * wsc + bv;
           g.C[moff[rl] + noff[cl]] = act_fwd(v, g.act, g.alpha);
         }
       }
@@ -486,6 +488,7 @@ __global__ void splitk_reduce(GemmArgs g, int phases) {
     const float* s = g.slab + (size_t)phase * g.splits * MN + e;
     float v = 0.f;
     for (int sp = 0; sp < g.splits; ++sp) v += s[(size_t)sp * MN];
+    if (g.wscale) v *= g.wscale[0];
     if (g.bias) v += g.bias[n];
     g.C[row_offset(g.out, m, MODE == MODE_CONVT2 ? phase : 0) + col_offset(g.out, n)] =
         act_fwd(v, g.act, g.alpha);
@@ -496,7 +499,6 @@ __global__ void splitk_reduce(GemmArgs g, int phases) {
 struct PackArgs {
   const float* W;
   float* out;
-  const float* scale;
   int K, N, phases;
   FastDiv fpci, fpkw;      // k -> (kh, kw, ci)
   FastDiv fnco, fnkw;      // n -> (nh, nw, co)
@@ -504,37 +506,35 @@ struct PackArgs {
   int KH, KW, flip, convt2;
 };
 
-__global__ void pack_weights(PackArgs a) {
-  const size_t KN = (size_t)a.K * a.N, total = KN * a.phases;
-  const float sc = a.scale ? a.scale[0] : 1.f;
-  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (size_t)gridDim.x * blockDim.x) {
-    const int phase = (int)(idx / KN);
-    const size_t e = idx - (size_t)phase * KN;
-    const int k = (int)(e / a.N), n = (int)(e - (size_t)k * a.N);
+// out[phase][k][n]: one block row per k (k-decomposition uniform per block), threads over n
+__global__ __launch_bounds__(256) void pack_weights(PackArgs a) {
+  const int phase = blockIdx.z;
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= a.N) return;
+  uint32_t tn = a.fnco.div(n);
+  const int co = n - tn * a.fnco.d;
+  uint32_t nh = a.fnkw.div(tn);
+  const int nw = tn - nh * a.fnkw.d;
+  for (int k = blockIdx.y; k < a.K; k += gridDim.y) {
     uint32_t t = a.fpci.div(k);
     const int ci = k - t * a.fpci.d;
-    int kh, kw, co;
+    int kh, kw, c_out;
     if (a.convt2) {
-      const int th = t >> 1, tw = t & 1;
-      kh = 2 * th + 1 - (phase >> 1);
-      kw = 2 * tw + 1 - (phase & 1);
-      co = n;
+      kh = 2 * (int)(t >> 1) + 1 - (phase >> 1);
+      kw = 2 * (int)(t & 1) + 1 - (phase & 1);
+      c_out = n;
     } else {
       uint32_t kkh = a.fpkw.div(t);
-      int kkw = t - kkh * a.fpkw.d;
-      uint32_t tn = a.fnco.div(n);
-      co = n - tn * a.fnco.d;
-      uint32_t nh = a.fnkw.div(tn);
-      int nw = tn - nh * a.fnkw.d;
-      kh = kkh + nh;
-      kw = kkw + nw;
+      kh = (int)kkh + (int)nh;
+      kw = (int)(t - kkh * a.fpkw.d) + nw;
+      c_out = co;
       if (a.flip) {
         kh = a.KH - 1 - kh;
         kw = a.KW - 1 - kw;
       }
     }
-    a.out[idx] = a.W[ci * a.s_in + co * a.s_out + kh * a.s_kh + kw * a.s_kw] * sc;
+    a.out[((size_t)phase * a.K + k) * a.N + n] =
+        a.W[ci * a.s_in + c_out * a.s_out + kh * a.s_kh + kw * a.s_kw];
   }
 }
 
@@ -549,6 +549,7 @@ struct Plan {
   bool av = false, bv = false;
   // packing
   bool pack = false;
+  const float* prepacked = nullptr;  // caller-owned packed weights (skip packing)
   PackArgs pk{};
   size_t pack_floats = 0, slab_floats = 0;
 };
@@ -617,8 +618,9 @@ static void set_pack(Plan& p, const float* W, const float* scale, int K, int N, 
                      int nco, int nkw, long long s_in, long long s_out, long long s_kh, long long s_kw,
                      int KH, int KW, int flip, int convt2) {
   p.pack = true;
+  p.g.wscale = scale;
   PackArgs& a = p.pk;
-  a.W = W; a.scale = scale; a.K = K; a.N = N; a.phases = p.phases;
+  a.W = W; a.K = K; a.N = N; a.phases = p.phases;
   a.fpci = FastDiv(pci); a.fpkw = FastDiv(pkw);
   a.fnco = FastDiv(nco); a.fnkw = FastDiv(nkw);
   a.s_in = s_in; a.s_out = s_out; a.s_kh = s_kh; a.s_kw = s_kw;
@@ -788,7 +790,13 @@ static int plan_wgrad(const RganConv* d, const float* x, const float* dy, float*
 }
 
 static size_t plan_ws_bytes(const Plan& p) {
-  return align_up(p.pack_floats * 4, 256) + align_up(p.slab_floats * 4, 256);
+  const size_t pack = p.prepacked ? 0 : align_up(p.pack_floats * 4, 256);
+  return pack + align_up(p.slab_floats * 4, 256);
+}
+
+static void launch_pack(const PackArgs& a, hipStream_t s) {
+  const int ky = std::min(a.K, 8192);
+  pack_weights<<<dim3(ceil_div(a.N, 256), ky, a.phases), 256, 0, s>>>(a);
 }
 
 template <int MODE, int BM, int BN, int WM, int WN>
@@ -847,14 +855,14 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   if (ws_bytes < plan_ws_bytes(p)) return RGAN_EINVAL;
   if (p.g.M <= 0 || p.g.N <= 0 || p.g.K <= 0) return RGAN_EINVAL;
   char* w = (char*)ws;
-  if (p.pack) {
+  if (p.pack && p.prepacked) {
+    p.g.Bw = p.prepacked;
+  } else if (p.pack) {
     if (!ws) return RGAN_EINVAL;
     p.pk.out = (float*)w;
     p.g.Bw = p.pk.out;
     w += align_up(p.pack_floats * 4, 256);
-    const size_t total = p.pack_floats;
-    const int blocks = (int)std::min<size_t>((total + 255) / 256, 4096);
-    pack_weights<<<blocks, 256, 0, s>>>(p.pk);
+    launch_pack(p.pk, s);
     RGAN_CHECK_LAUNCH();
   }
   p.g.slab = p.slab_floats ? (float*)w : nullptr;
@@ -897,7 +905,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
 
 using namespace rgan;
 
-extern "C" size_t rgan_conv_workspace(const RganConv* d, int which) {
+extern "C" size_t rgan_conv_workspace(const RganConv* d, int which, int prepacked) {
   Plan p;
   static const float dummy[4] = {0, 0, 0, 0};
   int rc;
@@ -905,7 +913,30 @@ extern "C" size_t rgan_conv_workspace(const RganConv* d, int which) {
   else if (which == 1) rc = plan_dgrad(d, dummy, dummy, nullptr, (float*)dummy, p);
   else rc = plan_wgrad(d, dummy, dummy, (float*)dummy, p);
   if (rc) return 0;
+  if (prepacked && which != 2) p.prepacked = dummy;
   return plan_ws_bytes(p) + 256;  // never 0 for a valid descriptor (0 signals "unsupported")
+}
+
+extern "C" size_t rgan_conv_pack_floats(const RganConv* d, int which) {
+  Plan p;
+  static const float dummy[4] = {0, 0, 0, 0};
+  int rc = which == 0 ? plan_fwd(d, dummy, dummy, nullptr, nullptr, (float*)dummy, 0, 0.f, p)
+                      : plan_dgrad(d, dummy, dummy, nullptr, (float*)dummy, p);
+  if (rc || which > 1) return 0;
+  return p.pack_floats;
+}
+
+extern "C" int rgan_conv_pack(const RganConv* d, int which, const float* w, float* packed, void* stream) {
+  if (!w || !packed || which < 0 || which > 1) return RGAN_EINVAL;
+  Plan p;
+  static const float dummy[4] = {0, 0, 0, 0};
+  int rc = which == 0 ? plan_fwd(d, dummy, w, nullptr, nullptr, (float*)dummy, 0, 0.f, p)
+                      : plan_dgrad(d, dummy, w, nullptr, (float*)dummy, p);
+  if (rc) return rc;
+  p.pk.out = packed;
+  launch_pack(p.pk, (hipStream_t)stream);
+  RGAN_CHECK_LAUNCH();
+  return 0;
 }
 
 static double conv_flops(const RganConv* d) {
@@ -913,24 +944,26 @@ static double conv_flops(const RganConv* d) {
   return 2.0 * d->batch * (double)d->cin * d->cout * d->kh * d->kw * pix;
 }
 
-extern "C" int rgan_conv_fwd(const RganConv* d, const float* x, const float* w, const float* wscale,
-                             const float* bias, float* y, int act, float act_alpha, void* ws,
+extern "C" int rgan_conv_fwd(const RganConv* d, const float* x, const float* w, const float* wpacked,
+                             const float* wscale, const float* bias, float* y, int act, float act_alpha, void* ws,
                              size_t ws_bytes, void* stream) {
-  if (!x || !w || !y) return RGAN_EINVAL;
+  if (!x || (!w && !wpacked) || !y) return RGAN_EINVAL;
   g_cur_flops = conv_flops(d);
   Plan p;
   int rc = plan_fwd(d, x, w, wscale, bias, y, act, act_alpha, p);
   if (rc) return rc;
+  p.prepacked = wpacked;
   return run_plan(p, ws, ws_bytes, (hipStream_t)stream);
 }
 
-extern "C" int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* w, const float* wscale,
-                               float* dx, void* ws, size_t ws_bytes, void* stream) {
-  if (!dy || !w || !dx) return RGAN_EINVAL;
+extern "C" int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* w, const float* wpacked,
+                               const float* wscale, float* dx, void* ws, size_t ws_bytes, void* stream) {
+  if (!dy || (!w && !wpacked) || !dx) return RGAN_EINVAL;
   g_cur_flops = conv_flops(d);
   Plan p;
   int rc = plan_dgrad(d, dy, w, wscale, dx, p);
   if (rc) return rc;
+  p.prepacked = wpacked;
   return run_plan(p, ws, ws_bytes, (hipStream_t)stream);
 }
 

@@ -6,6 +6,7 @@ allocator and launches on the current stream.  Internal activations are NHWC
 wherever the reference hands them over (images into D, out of G).
 """
 import ctypes
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -61,8 +62,54 @@ def _f32(*ts):
             raise L.RganError(f"expected float32 tensors, got {t.dtype}")
 
 
-def conv_fwd(x, w, geom, bias=None, act="none", alpha=0.0, wscale=None, out=None, nchw_out=False):
-    """y = act(conv(x, w*wscale) + bias); x [B,Cin,H,W] any strides; w torch layout."""
+class _PackCache:
+    """GEMM-ready weight layouts, cached per (weight tensor, layout, version).
+
+    Weights change only at optimizer steps (fused Adam bumps the autograd version
+    counter), while every net runs 2-4 times per iteration, so most conv launches reuse
+    a packed copy.  Entries are keyed by the weight's base tensor object (held weakly:
+    a storage address can be reused by a later tensor with the same version count) and
+    one buffer per (weight, layout) is refilled in place when the version moves."""
+
+    def __init__(self):
+        self.entries = {}
+
+    def get(self, w, which, geom, d):
+        base = w._base if w._base is not None else w
+        key = (id(base), which, geom, d.cin, d.cout, d.hin, d.win, d.hout, d.wout)
+        ver = w._version
+        ent = self.entries.get(key)
+        if ent is not None and ent[0]() is base and ent[1] == ver and ent[3] == w.data_ptr():
+            return ent[2]
+        lib = L.lib()
+        n = lib.rgan_conv_pack_floats(ctypes.byref(d), which)
+        if n == 0:
+            raise L.RganError(f"unsupported conv {geom} (pack)")
+        reuse = ent is not None and ent[0]() is base and ent[2].numel() == n
+        buf = ent[2] if reuse else torch.empty(n, dtype=torch.float32, device=w.device)
+        L.check(lib.rgan_conv_pack(ctypes.byref(d), which, L.ptr(w), L.ptr(buf), L.stream()), "rgan_conv_pack")
+        self.entries[key] = (weakref.ref(base, self._drop(key)), ver, buf, w.data_ptr())
+        return buf
+
+    def _drop(self, key):
+        def cb(_ref):
+            ent = self.entries.get(key)
+            if ent is not None and ent[0] is _ref:
+                del self.entries[key]
+        return cb
+
+    def clear(self):
+        self.entries.clear()
+
+
+PACKS = _PackCache()
+
+
+def conv_fwd(x, w, geom, bias=None, act="none", alpha=0.0, wscale=None, out=None, nchw_out=False, cache=False):
+    """y = act(conv(x, w)*wscale + bias); x [B,Cin,H,W] any strides; w torch layout.
+
+    ``cache=True`` (module parameters only) reuses a packed weight while its version is
+    unchanged."""
     L.require_cuda(x, w, bias, wscale)
     _f32(x, w, bias)
     B, cin, H, W = x.shape
@@ -73,16 +120,18 @@ def conv_fwd(x, w, geom, bias=None, act="none", alpha=0.0, wscale=None, out=None
                else empty_nhwc(B, cout, Ho, Wo, x.device))
     d = _desc(x.shape, x.stride(), out.shape, out.stride(), geom)
     lib = L.lib()
-    nbytes = lib.rgan_conv_workspace(ctypes.byref(d), 0)
+    packed = PACKS.get(w, 0, geom, d) if cache else None
+    nbytes = lib.rgan_conv_workspace(ctypes.byref(d), 0, int(packed is not None))
     if nbytes == 0:
         raise L.RganError(f"unsupported conv {geom} for input {tuple(x.shape)}")
     ws = L.workspace(nbytes, x.device)
-    L.check(lib.rgan_conv_fwd(ctypes.byref(d), L.ptr(x), L.ptr(w), L.ptr(wscale), L.ptr(bias), L.ptr(out),
-                              L.ACT[act], float(alpha), L.ptr(ws), ws.numel(), L.stream()), "rgan_conv_fwd")
+    L.check(lib.rgan_conv_fwd(ctypes.byref(d), L.ptr(x), L.ptr(w), L.ptr(packed), L.ptr(wscale), L.ptr(bias),
+                              L.ptr(out), L.ACT[act], float(alpha), L.ptr(ws), ws.numel(), L.stream()),
+            "rgan_conv_fwd")
     return out
 
 
-def conv_dgrad(dy, w, geom, x_shape, wscale=None, out=None, like=None):
+def conv_dgrad(dy, w, geom, x_shape, wscale=None, out=None, like=None, cache=False):
     """dx of the conv (input grad), NHWC unless `like` (a tensor whose strides to copy) is given."""
     L.require_cuda(dy, w, wscale)
     _f32(dy, w)
@@ -94,12 +143,13 @@ def conv_dgrad(dy, w, geom, x_shape, wscale=None, out=None, like=None):
             out = empty_nhwc(B, cin, H, W, dy.device)
     d = _desc(out.shape, out.stride(), dy.shape, dy.stride(), geom)
     lib = L.lib()
-    nbytes = lib.rgan_conv_workspace(ctypes.byref(d), 1)
+    packed = PACKS.get(w, 1, geom, d) if cache else None
+    nbytes = lib.rgan_conv_workspace(ctypes.byref(d), 1, int(packed is not None))
     if nbytes == 0:
         raise L.RganError(f"unsupported conv dgrad {geom} for {tuple(x_shape)}")
     ws = L.workspace(nbytes, dy.device)
-    L.check(lib.rgan_conv_dgrad(ctypes.byref(d), L.ptr(dy), L.ptr(w), L.ptr(wscale), L.ptr(out), L.ptr(ws),
-                                ws.numel(), L.stream()), "rgan_conv_dgrad")
+    L.check(lib.rgan_conv_dgrad(ctypes.byref(d), L.ptr(dy), L.ptr(w), L.ptr(packed), L.ptr(wscale), L.ptr(out),
+                                L.ptr(ws), ws.numel(), L.stream()), "rgan_conv_dgrad")
     return out
 
 
@@ -115,7 +165,7 @@ def conv_wgrad(x, dy, geom, w_shape, with_bias=False):
             dy = dy.contiguous(memory_format=torch.channels_last)
     d = _desc(x.shape, x.stride(), dy.shape, dy.stride(), geom)
     lib = L.lib()
-    nbytes = lib.rgan_conv_workspace(ctypes.byref(d), 2)
+    nbytes = lib.rgan_conv_workspace(ctypes.byref(d), 2, 0)
     if nbytes == 0:
         raise L.RganError(f"unsupported conv wgrad {geom} for {tuple(x.shape)}")
     ws = L.workspace(nbytes, x.device)
@@ -146,10 +196,10 @@ def bn_stats(y, eps, momentum, running_mean=None, running_var=None, num_batches_
 
 
 def bn_moments(y):
-    """This rank's per-channel (count, mean, M2) as float[3C] (SyncBN stage 1)."""
+    """This rank's per-channel (count, mean, M2) as double[3C] (SyncBN stage 1)."""
     P, C, sp, sc = _pc(y)
     lib = L.lib()
-    mom = torch.empty(3 * C, dtype=torch.float32, device=y.device)
+    mom = torch.empty(3 * C, dtype=torch.float64, device=y.device)
     part = L.workspace(lib.rgan_bn_partial_bytes(P, C), y.device)
     L.check(lib.rgan_bn_moments(L.ptr(y), P, C, sp, sc, L.ptr(mom), L.ptr(part), L.stream()), "rgan_bn_moments")
     return mom
@@ -170,7 +220,7 @@ def bn_backward_sums(da, y, stats, gamma, beta, act="none", alpha=0.0):
         da = da.contiguous(memory_format=torch.channels_last)
     P, C, sp, sc = _pc(y)
     _, _, dsp, dsc = _pc(da)
-    sums = torch.empty(2 * C, dtype=torch.float32, device=y.device)
+    sums = torch.empty(2 * C, dtype=torch.float64, device=y.device)
     lib = L.lib()
     part = L.workspace(lib.rgan_bn_partial_bytes(P, C), y.device)
     L.check(lib.rgan_bn_backward_sums(L.ptr(da), dsp, dsc, L.ptr(y), P, C, sp, sc, L.ptr(stats), L.ptr(gamma),

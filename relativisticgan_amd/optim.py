@@ -10,6 +10,7 @@ device buffer (doubles, as torch keeps them in Python floats), refreshed only wh
 group's values change; the step counter is a device scalar incremented by the kernel.
 """
 import torch
+from torch.autograd.graph import increment_version
 
 from . import kernels as K
 
@@ -70,8 +71,9 @@ class Adam(torch.optim.Optimizer):
                 continue
             hyper, _, step = self._group_dev(gi, group, ps[0].device, first)
             K.adam(ps, gs, ms, vs, hyper, step)
-            for p in ps:  # host mirror of state['step'] (state_dict layout of torch Adam)
-                self.state[p]["step"] += 1
+            for p in ps:
+                self.state[p]["step"] += 1  # host mirror of state['step'] (torch Adam's state_dict layout)
+                increment_version(p)        # the kernel wrote p: invalidate cached packed layouts
         return loss
 
     def load_state_dict(self, state_dict):

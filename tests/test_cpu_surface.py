@@ -45,13 +45,13 @@ def test_library_rejects_bad_descriptors():
     d.batch, d.cin, d.hin, d.win, d.cout, d.hout, d.wout = 2, 3, 8, 8, 4, 5, 5  # inconsistent hout
     d.kh = d.kw = 4
     d.stride, d.pad = 2, 1
-    assert lib.rgan_conv_workspace(ctypes.byref(d), 0) == 0
+    assert lib.rgan_conv_workspace(ctypes.byref(d), 0, 0) == 0
     d.hout = d.wout = 4
     for i, s in enumerate((192, 64, 8, 1)):
         d.xs[i] = s
     for i, s in enumerate((64, 1, 16, 4)):
         d.ys[i] = s
-    assert lib.rgan_conv_workspace(ctypes.byref(d), 0) > 0
+    assert lib.rgan_conv_workspace(ctypes.byref(d), 0, 0) > 0
     assert lib.rgan_loss_head(9, 0, None, None, 8, None, None, None, None) == 1001
 
 

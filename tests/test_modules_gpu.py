@@ -63,42 +63,60 @@ def test_nets_vs_fp64_torch(case):
     Go32, Do32 = copy.deepcopy(Go), copy.deepcopy(Do)
     B = case["batch_size"]
     z = torch.randn(B, case["z_size"], 1, 1)
-    # G forward/backward
-    z64 = z.double().requires_grad_(False)
-    out64 = Go64(z64)
+    # G forward (activation signs traced on both sides: ReLU'/LeakyReLU'/SELU' jump at 0)
+    from relativisticgan_amd import autograd
+    masks64 = []
+    hooks = [m.register_forward_hook(lambda mod, i, o: masks64.append((o.detach() > 0).clone()))
+             for net in (Go64, Do64) for m in net.modules()
+             if isinstance(m, (torch.nn.ReLU, torch.nn.LeakyReLU, torch.nn.SELU))]
+    autograd.ACT_TRACE = []
+    out64 = Go64(z.double())
+    out32 = Go32(z)
     fake = G(z.to(DEV))
-    assert _rel(fake, out64) < 2e-5
-    # D on G's output with input grad (the G-step path) and param grads (D-step path)
-    x = fake.detach().requires_grad_(True)
-    x64 = out64.detach().clone().requires_grad_(True)
-    y = D(x)
-    y64 = Do64(x64)
-    assert _rel(y, y64) < 2e-5
+    flips = [0]
+
+    def env(label, ours, ref32, ref64, tol=2e-5):
+        e, e32 = _rel(ours, ref64), _rel(ref32, ref64)
+        bound = max(tol, 4 * e32, 5e-2 if flips[0] else 0.0)
+        assert e < bound, f"{label}: {e:.2e} vs fp64 (torch fp32: {e32:.2e}, flips {flips[0]})"
+
+    env("G out", fake, out32, out64)
+    # D on the same image with input grad (the G-step path) and param grads (D-step path)
+    img = out64.detach()
+    x = img.float().to(DEV).requires_grad_(True)
+    x32 = img.float().clone().requires_grad_(True)
+    x64 = img.clone().requires_grad_(True)
+    y, y32, y64 = D(x), Do32(x32), Do64(x64)
+    ours_masks, autograd.ACT_TRACE = autograd.ACT_TRACE, None
+    for h in hooks:
+        h.remove()
+    assert len(ours_masks) == len(masks64)
+    flips[0] = sum(int((a != b).sum()) for a, b in zip(ours_masks, masks64))
+    print(f"activation-sign flips vs fp64: {flips[0]}")
+    env("D out", y, y32, y64)
     gy = torch.randn(B)
     y.backward(gy.to(DEV))
+    y32.backward(gy)
     y64.backward(gy.double())
-    assert _rel(x.grad, x64.grad) < 2e-5, "D input grad"
+    env("D input grad", x.grad, x32.grad, x64.grad)
     skip = _biases_before_bn(Do64)
-    for (n, q), (n64, q64) in zip(D.named_parameters(), Do64.named_parameters()):
+    for (n, q), (_, q32), (n64, q64) in zip(D.named_parameters(), Do32.named_parameters(), Do64.named_parameters()):
         assert n == n64
-        if n in skip:
-            assert q.grad.abs().max().item() < 1e-4 * max(1e-12, x64.grad.abs().max().item()) + 1e-6, n
+        if n in skip:  # exact gradient is 0: both fp32 results are roundoff
+            assert q.grad.abs().max().item() <= 10 * q32.grad.abs().max().item() + 1e-7, n
             continue
-        assert _rel(q.grad, q64.grad) < 2e-5, f"D grad {n}"
-    # G backward from the D-input gradient; envelope vs torch fp32 on the same path
-    fake.backward(x.grad)
-    out64.backward(x64.grad)
-    out32 = Go32(z)
-    x32 = out32.detach().clone().requires_grad_(True)
-    Do32(x32).backward(gy)
-    out32.backward(x32.grad)
+        env(f"D grad {n}", q.grad, q32.grad, q64.grad)
+    # G backward from one shared upstream gradient (the fp64 one, rounded to fp32)
+    gfake = x64.grad.detach()
+    fake.backward(gfake.float().to(DEV))
+    out32.backward(gfake.float())
+    out64.backward(gfake)
     skipg = _biases_before_bn(Go64)
-    for (n, q), (_, q64), (_, q32) in zip(G.named_parameters(), Go64.named_parameters(), Go32.named_parameters()):
+    for (n, q), (_, q32), (_, q64) in zip(G.named_parameters(), Go32.named_parameters(), Go64.named_parameters()):
         if n in skipg:
             continue
-        e, e32 = _rel(q.grad, q64.grad), _rel(q32.grad, q64.grad)
-        assert e < max(2e-5, 4 * e32), f"G grad {n}: {e:.2e} (torch fp32: {e32:.2e})"
-    # BN running statistics after two train-mode forwards each
-    for (n, b), (n64, b64) in zip(D.named_buffers(), Do64.named_buffers()):
+        env(f"G grad {n}", q.grad, q32.grad, q64.grad)
+    # BN running statistics after the train-mode forwards
+    for (n, b), (_, b32), (_, b64) in zip(D.named_buffers(), Do32.named_buffers(), Do64.named_buffers()):
         if "running" in n:
-            assert _rel(b, b64) < 1e-5, n
+            env(n, b, b32, b64, 1e-5)
