@@ -145,7 +145,8 @@ class _AllReduceSum(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        return dp.all_reduce_sum(g.clone())
+        # itself differentiable: the WGAN-GP second backward runs through this node
+        return _AllReduceSum.apply(g)
 
 
 # ---------------------------------------------------------------- fused layer
@@ -204,9 +205,16 @@ class ConvLayerFn(torch.autograd.Function):
                 raise NotImplementedError("backward through eval-mode BatchNorm is not on the training path")
             if dp.sync_bn():
                 sums, da_c = K.bn_backward_sums(da, y, stats, gamma, beta, spec.act, spec.alpha)
+                # dgamma/dbeta stay shard-local (from the pre-all-reduce sums): the bucketed
+                # gradient all-reduce sums them like every other parameter gradient
+                C = y.shape[1]
+                if ng and gamma is not None:
+                    dgamma = (sums[C:] * stats[C:2 * C].double()).float()
+                if nbeta and beta is not None:
+                    dbeta = sums[:C].float()
                 dp.all_reduce_sum(sums)
-                dy, dgamma, dbeta = K.bn_backward_apply(da_c, y, stats, gamma, beta, spec.act, spec.alpha, sums,
-                                                        P * dp.world(), need_affine=ng or nbeta)
+                dy, _, _ = K.bn_backward_apply(da_c, y, stats, gamma, beta, spec.act, spec.alpha, sums,
+                                               P * dp.world(), need_affine=False)
             else:
                 dy, dgamma, dbeta = K.bn_backward(da, y, stats, gamma, beta, spec.act, spec.alpha,
                                                   need_affine=ng or nbeta)

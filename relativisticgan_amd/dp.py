@@ -75,9 +75,14 @@ def all_gather_cat(t):
     """[world * numel] concatenation of every rank's ``t`` in rank order."""
     if _S.world == 1:
         return t
-    out = torch.empty(_S.world * t.numel(), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(out, t.contiguous().view(-1), group=_S.group)
-    return out
+    flat = t.contiguous().view(-1)
+    if dist.get_backend(_S.group) == "nccl":  # RCCL: one fused collective
+        out = torch.empty(_S.world * flat.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, flat, group=_S.group)
+        return out
+    parts = [torch.empty_like(flat) for _ in range(_S.world)]
+    dist.all_gather(parts, flat, group=_S.group)
+    return torch.cat(parts)
 
 
 def merge_moments(moments, C):

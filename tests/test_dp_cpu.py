@@ -1,0 +1,138 @@
+"""Data-parallel algebra on CPU: world_size-2 gloo processes (no GPU).
+
+Checks the collective helpers of relativisticgan_amd.dp and the exchange protocol the
+build uses against single-process global-batch math:
+  * SyncBN forward: per-rank (count, mean, M2) all-gathered and merged in rank order
+    == the global batch statistics;
+  * SyncBN backward: all-reduced (sum g, sum g*(y-mean)) == global sums;
+  * relativistic loss heads: the 3-phase protocol (local sums of r/f -> all-reduce ->
+    local sums of a, b, a', b' -> all-reduce -> grads) reproduces the global-batch loss
+    and gradients of the reference expressions (GLI:634-641, 698-709);
+  * bucketed gradient all-reduce == per-tensor sum.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle.reference_cpu import head_G, head_relativistic_D
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from relativisticgan_amd import dp
+    dp.setup()
+    return dp
+
+
+def _local_moments(y):
+    C = y.shape[1]
+    t = y.transpose(0, 1).reshape(C, -1).double()
+    n = torch.full((C,), float(t.shape[1]), dtype=torch.float64)
+    mean = t.mean(1)
+    m2 = ((t - mean[:, None]) ** 2).sum(1)
+    return torch.cat([n, mean, m2])
+
+
+def _ra_terms(kind, side, r, f, mr, mf):
+    """Per-element a(r - m_f), b(f - m_r) and derivatives."""
+    g = side == 2
+    dr_, df_ = r - mf, f - mr
+    sp = torch.nn.functional.softplus
+    if kind == 6:
+        a = sp(dr_) if g else sp(-dr_)
+        da = torch.sigmoid(dr_) if g else torch.sigmoid(dr_) - 1
+        b = sp(-df_) if g else sp(df_)
+        db = torch.sigmoid(df_) - 1 if g else torch.sigmoid(df_)
+    elif kind == 7:
+        sa, sb = (dr_ + 1, df_ - 1) if g else (dr_ - 1, df_ + 1)
+        a, da, b, db = sa * sa, 2 * sa, sb * sb, 2 * sb
+    else:
+        ha, hb = (1 + dr_, 1 - df_) if g else (1 - dr_, 1 + df_)
+        a, b = ha.clamp_min(0), hb.clamp_min(0)
+        da = (ha > 0).double() * (1 if g else -1)
+        db = (hb > 0).double() * (-1 if g else 1)
+    return a, b, da, db
+
+
+def _worker(rank, world, port, q):
+    try:
+        dp = _init(rank, world, port)
+        torch.manual_seed(0)
+        B, C = 16, 6
+        y = torch.randn(B, C, 5, 5, dtype=torch.float64) * 3 + 1
+        r_all = torch.randn(B, dtype=torch.float64)
+        f_all = torch.randn(B, dtype=torch.float64)
+        lo, hi = rank * B // world, (rank + 1) * B // world
+        # SyncBN forward
+        mom = dp.all_gather_cat(_local_moments(y[lo:hi]))
+        mean, var, n = dp.merge_moments(mom, C)
+        assert torch.allclose(mean, y.mean((0, 2, 3)), atol=1e-12)
+        assert torch.allclose(var, y.var((0, 2, 3), unbiased=False), atol=1e-12)
+        assert torch.all(n == B * 25)
+        # SyncBN backward sums
+        g = torch.randn_like(y)
+        loc = torch.cat([g[lo:hi].sum((0, 2, 3)), (g[lo:hi] * (y[lo:hi] - mean.view(1, -1, 1, 1))).sum((0, 2, 3))])
+        dp.all_reduce_sum(loc)
+        glob = torch.cat([g.sum((0, 2, 3)), (g * (y - mean.view(1, -1, 1, 1))).sum((0, 2, 3))])
+        assert torch.allclose(loc, glob, atol=1e-10)
+        # relativistic heads, 3-phase protocol vs the reference expressions on the global batch
+        ones, zeros = torch.ones(B, dtype=torch.float64), torch.zeros(B, dtype=torch.float64)
+        for kind in (6, 7, 8):
+            for side in (0, 2):
+                r, f = r_all[lo:hi], f_all[lo:hi]
+                s = dp.all_reduce_sum(torch.stack([r.sum(), f.sum()]))
+                mr, mf = s[0] / B, s[1] / B
+                a, b, da, db = _ra_terms(kind, side, r, f, mr, mf)
+                s2 = dp.all_reduce_sum(torch.stack([a.sum(), b.sum(), da.sum(), db.sum()]))
+                loss = (s2[0] / B + s2[1] / B) / 2
+                grad_r = 0.5 / B * (da - s2[3] / B)
+                grad_f = 0.5 / B * (db - s2[2] / B)
+                rr = r_all.clone().requires_grad_(True)
+                ff = f_all.clone().requires_grad_(True)
+                ref = (head_relativistic_D(kind, rr, ff, ones, zeros) if side == 0
+                       else head_G(kind, ff, rr, ones, zeros))
+                ref.backward()
+                assert abs(loss.item() - ref.item()) < 1e-12, (kind, side)
+                assert torch.allclose(grad_r, rr.grad[lo:hi], atol=1e-12), (kind, side)
+                assert torch.allclose(grad_f, ff.grad[lo:hi], atol=1e-12), (kind, side)
+        # bucketed gradient all-reduce
+        ps = [torch.nn.Parameter(torch.zeros(s)) for s in ((3, 4), (7,), (2, 2, 2))]
+        for k, prm in enumerate(ps):
+            prm.grad = torch.full(prm.shape, float(rank + 1 + k))
+        dp.allreduce_grads(ps, bucket_bytes=40)
+        for k, prm in enumerate(ps):
+            assert torch.all(prm.grad == sum(rk + 1 + k for rk in range(world)))
+        q.put((rank, "ok"))
+    except Exception as e:  # report to the parent
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_dp_collectives_and_protocol_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(120)
+    res = [q.get() for _ in range(world)]
+    assert all(msg == "ok" for _, msg in res), res
