@@ -189,7 +189,7 @@ int rgan_gather_images(const float* images, const long long* idx, int batch, lon
  * rgan_profile_begin(capacity): bracket each subsequent conv GEMM launch with HIP events
  * on its stream (up to `capacity` launches).  rgan_profile_end: wait, stop, return
  * summed GEMM time, summed algorithmic FLOPs (2*B*Cin*Cout*k*k*pixels per conv op) and
- * the launch count.  rgan_profile_kernel(i in [0,36)): the same per kernel symbol. */
+ * the launch count.  rgan_profile_kernel(i = 0, 1, ... until it returns RGAN_EINVAL): the same per kernel symbol. */
 int rgan_profile_begin(int capacity);
 int rgan_profile_end(double* total_ms, double* total_flops, long long* launches);
 int rgan_profile_kernel(int idx, char* name, int name_len, double* ms, double* flops, long long* n);

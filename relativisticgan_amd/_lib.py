@@ -10,7 +10,7 @@ import os
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librgan.so")
+LIB_PATH = os.environ.get("RGAN_LIB") or os.path.join(HERE, "librgan.so")  # RGAN_LIB: experiment builds (tools/build_variant.py)
 
 ACT = {"none": 0, "relu": 1, "lrelu": 2, "tanh": 3, "sigmoid": 4, "selu": 5}
 

@@ -27,6 +27,12 @@
 namespace rgan {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Raw-buffer byte offset past every record of a descriptor (< 2^31 bytes): loads return 0.
+constexpr int OOB = (int)0x80000000;
+// fast-path tensors must fit a buffer descriptor with this margin
+constexpr long long FAST_MAX_BYTES = (1LL << 31) - (1LL << 24);
 
 enum { MODE_CONV = 0, MODE_CONVT2 = 1, MODE_WGRAD = 2 };
 constexpr int BK = 32;
@@ -78,6 +84,8 @@ struct GemmArgs {
   int act;
   float alpha;
   float* slab;
+  // FAST paths (raw buffer loads, scalar per-tile offsets): descriptor sizes in bytes
+  int a_bytes, im_bytes, bw_bytes;
 };
 
 __device__ __forceinline__ long long row_offset(const OutMap& o, int m, int phase) {
@@ -97,7 +105,16 @@ __device__ __forceinline__ long long col_offset(const OutMap& o, int n) {
   return (long long)nh * o.th + (long long)nw * o.tw + (long long)c * o.tc;
 }
 
-template <int MODE, int BM, int BN, int WM, int WN, bool AV, bool BV>
+// FAST (AV && BV only; host checks the conditions in set_fast): every BK tile of a
+// CONV/CONVT2 GEMM lies inside one filter tap (Cin % BK == 0), so per-row input offsets
+// change only when the tap does and the per-tile advance (channel chunk, weight row
+// block) is a wave-uniform scalar passed as the buffer load's soffset: the main loop
+// issues almost no VALU (fp32 MFMA shares the VALU datapath on gfx950 --
+// SQ_VALU_MFMA_COEXEC_CYCLES = 0 -- so every address instruction costs MFMA cycles).
+// WGRAD: the gradient rows are pixel-contiguous (offset = p * pixel stride: scalar
+// advance) and the im2col operand reads one tap per block tile (Cin % BN == 0) through
+// a per-tile table of pixel offsets built by one wave into LDS two tiles ahead.
+template <int MODE, int BM, int BN, int WM, int WN, bool AV, bool BV, bool FAST>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert(TM >= 1 && TN >= 1 && WM * WN == 4, "tile config");
@@ -168,6 +185,118 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
   constexpr int B_ELEMS = BK * BN / 256;
   float ra[A_ELEMS];
   float rb[B_ELEMS];
+
+  // ---------------- FAST-path state ----------------
+  static_assert(!FAST || (AV && BV), "FAST needs vector operands");
+  constexpr int FA_TPR = (MODE == MODE_WGRAD) ? BM / 4 : BK / 4;   // threads per A row
+  constexpr int FA_N = (MODE == MODE_WGRAD) ? BK / (256 / FA_TPR) : AR;  // A loads per thread
+  constexpr int FB_TPR = BN / 4, FB_RPP = 256 / FB_TPR, FB_N = BK / FB_RPP;
+  __shared__ int ptab[2][BK];   // WGRAD FAST: im2col pixel offsets of the next tiles
+  __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g.a.p, (short)0, g.a_bytes, 0x00020000);
+  __amdgpu_buffer_rsrc_t brsrc =
+      MODE == MODE_WGRAD ? __builtin_amdgcn_make_buffer_rsrc((void*)g.im.p, (short)0, g.im_bytes, 0x00020000)
+                         : __builtin_amdgcn_make_buffer_rsrc((void*)Bw, (short)0, g.bw_bytes, 0x00020000);
+  int aoff[FAST ? FA_N : 1], boff[FAST ? FB_N : 1];
+  int f_tap = 0, f_c0 = 0, f_cin = 1, w_tab = 0;
+  if constexpr (FAST) {
+    if constexpr (MODE != MODE_WGRAD) {
+      const int n = n0 + 4 * (tid % FB_TPR), r = tid / FB_TPR;
+#pragma unroll
+      for (int i = 0; i < FB_N; ++i) boff[i] = n < g.N ? ((r + FB_RPP * i) * g.N + n) * 4 : OOB;
+      f_cin = g.fC.d;
+      f_tap = kbeg / f_cin;
+      f_c0 = kbeg - f_tap * f_cin;
+    } else {
+      const int m = m0 + 4 * (tid % FA_TPR), r = tid / FA_TPR;
+      constexpr int RPP = 256 / FA_TPR;
+#pragma unroll
+      for (int i = 0; i < FA_N; ++i) aoff[i] = m < g.M ? ((r + RPP * i) * (int)g.a.sw + m) * 4 : OOB;
+      // the block's n tile lies in one tap: n0 -> (kh, kw, ci0), wave-uniform
+      const uint32_t t = g.fC.div(n0);
+      const int ci0 = n0 - t * g.fC.d;
+      const uint32_t kh = g.fKW.div(t);
+      const int kw = t - kh * g.fKW.d;
+      w_tab = ((int)kh - g.pad) * (int)g.im.sh + ((int)kw - g.pad) * (int)g.im.sw + ci0;  // tap part
+      f_tap = (int)kh;   // kept for the bounds checks below
+      f_c0 = kw;
+    }
+  }
+  // CONV/CONVT2 FAST: per-row offsets for the current tap
+  auto set_tap = [&](int tap) {
+    if constexpr (FAST && MODE != MODE_WGRAD) {
+      int dh, dw;
+      if constexpr (MODE == MODE_CONV) {
+        dh = tap / g.KW;
+        dw = tap - dh * g.KW;
+      } else {
+        dh = ph - (tap >> 1);
+        dw = pw - (tap & 1);
+      }
+      const int q = tid & 7;
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const int ih = aih[i] + dh, iw = aiw[i] + dw;
+        aoff[i] = ((unsigned)ih < (unsigned)g.a.H && (unsigned)iw < (unsigned)g.a.W)
+                      ? ((int)abase[i] + ih * (int)g.a.sh + iw * (int)g.a.sw) * 4 + q * 16
+                      : OOB;
+      }
+    }
+  };
+  // WGRAD FAST: one wave writes the im2col pixel offsets of tile k0 into ptab[slot]
+  auto build_table = [&](int k0, int slot) {
+    if constexpr (FAST && MODE == MODE_WGRAD) {
+      const int l = tid & 63;
+      if (l < BK) {
+        const int p = k0 + l;
+        const uint32_t b = g.fghw.div(p);
+        const uint32_t rem = p - b * g.fghw.d;
+        const uint32_t oi = g.fgw.div(rem);
+        const uint32_t oj = rem - oi * g.fgw.d;
+        const int ih = (int)oi * g.stride - g.pad + f_tap, iw = (int)oj * g.stride - g.pad + f_c0;
+        ptab[slot][l] = (p < kend && (unsigned)ih < (unsigned)g.im.H && (unsigned)iw < (unsigned)g.im.W)
+                            ? ((int)b * (int)g.im.sb + (int)oi * g.stride * (int)g.im.sh +
+                               (int)oj * g.stride * (int)g.im.sw + w_tab) * 4
+                            : OOB;
+      }
+    }
+  };
+  auto load_fast = [&](int k0, int slot) {
+    if constexpr (FAST && MODE != MODE_WGRAD) {
+      if (f_c0 == f_cin) {
+        f_c0 = 0;
+        set_tap(++f_tap);
+      }
+#pragma unroll
+      for (int i = 0; i < AR; ++i) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(arsrc, aoff[i], f_c0 * 4, 0);
+        ra[4 * i + 0] = __uint_as_float(v.x); ra[4 * i + 1] = __uint_as_float(v.y);
+        ra[4 * i + 2] = __uint_as_float(v.z); ra[4 * i + 3] = __uint_as_float(v.w);
+      }
+      f_c0 += BK;
+      const int so = k0 * g.N * 4;
+#pragma unroll
+      for (int i = 0; i < FB_N; ++i) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(brsrc, boff[i], so, 0);
+        rb[4 * i + 0] = __uint_as_float(v.x); rb[4 * i + 1] = __uint_as_float(v.y);
+        rb[4 * i + 2] = __uint_as_float(v.z); rb[4 * i + 3] = __uint_as_float(v.w);
+      }
+    } else if constexpr (FAST) {
+      const int so = k0 * (int)g.a.sw * 4;
+#pragma unroll
+      for (int i = 0; i < FA_N; ++i) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(arsrc, aoff[i], so, 0);
+        ra[4 * i + 0] = __uint_as_float(v.x); ra[4 * i + 1] = __uint_as_float(v.y);
+        ra[4 * i + 2] = __uint_as_float(v.z); ra[4 * i + 3] = __uint_as_float(v.w);
+      }
+      const int qb = (tid % FB_TPR) * 16, r = tid / FB_TPR;
+#pragma unroll
+      for (int i = 0; i < FB_N; ++i) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(brsrc, ptab[slot][r + FB_RPP * i] + qb, 0, 0);
+        rb[4 * i + 0] = __uint_as_float(v.x); rb[4 * i + 1] = __uint_as_float(v.y);
+        rb[4 * i + 2] = __uint_as_float(v.z); rb[4 * i + 3] = __uint_as_float(v.w);
+      }
+    }
+  };
 
   auto load_tiles = [&](int k0) {
     // ---------------- A ----------------
@@ -400,32 +529,93 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  if constexpr (FAST && MODE == MODE_WGRAD) {
+    if (wid == 0) build_table(kbeg, 0);
+    if (wid == 1 && nk > 1) build_table(kbeg + BK, 1);
+    __syncthreads();
+  }
+  if constexpr (FAST && MODE != MODE_WGRAD) set_tap(f_tap);
   if (nk > 0) {
-    load_tiles(kbeg);
+    if constexpr (FAST) load_fast(kbeg, 0);
+    else load_tiles(kbeg);
     store_tiles(0);
   }
   __syncthreads();
   const int l32 = lane & 31, lk = lane >> 5;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_tiles(kbeg + (kt + 1) * BK);
+    if (kt + 1 < nk) {
+      if constexpr (FAST) load_fast(kbeg + (kt + 1) * BK, (kt + 1) & 1);
+      else load_tiles(kbeg + (kt + 1) * BK);
+    }
+    if constexpr (FAST && MODE == MODE_WGRAD) {
+      if (kt + 2 < nk && wid == (kt & 3)) build_table(kbeg + (kt + 2) * BK, kt & 1);
+    }
     const float* As = smem + cur * STAGE;
     const float* Bs = As + A_SZ;
+#if RGAN_GEMM_FRAGALL
+    // all of the tile's MFMA operands to registers first: the LDS reads are in flight
+    // together and the MFMA chain waits on them progressively
+    float af[BK / 2][TM], bf[BK / 2][TN];
 #pragma unroll
     for (int kk = 0; kk < BK / 2; ++kk) {
       const int k = 2 * kk + lk;
-      float af[TM], bf[TN];
 #pragma unroll
       for (int t = 0; t < TM; ++t)
-        af[t] = AK ? As[k * A_LD + wm + 32 * t + l32] : As[(wm + 32 * t + l32) * A_LD + k];
+        af[kk][t] = AK ? As[k * A_LD + wm + 32 * t + l32] : As[(wm + 32 * t + l32) * A_LD + k];
 #pragma unroll
-      for (int t = 0; t < TN; ++t) bf[t] = Bs[k * B_LD + wn + 32 * t + l32];
+      for (int t = 0; t < TN; ++t) bf[kk][t] = Bs[k * B_LD + wn + 32 * t + l32];
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[kk][i], bf[kk][j], acc[i][j], 0, 0, 0);
+#elif RGAN_GEMM_PREF
+    // operands of step kk+PREF are read while step kk's MFMAs run
+    constexpr int PF = RGAN_GEMM_PREF;
+    float af[PF + 1][TM], bf[PF + 1][TN];
+    auto rd = [&](int kk, int s) {
+      const int k = 2 * kk + lk;
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+        af[s][t] = AK ? As[k * A_LD + wm + 32 * t + l32] : As[(wm + 32 * t + l32) * A_LD + k];
+#pragma unroll
+      for (int t = 0; t < TN; ++t) bf[s][t] = Bs[k * B_LD + wn + 32 * t + l32];
+    };
+#pragma unroll
+    for (int kk = 0; kk < PF; ++kk) rd(kk, kk);
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      if (kk + PF < BK / 2) rd(kk + PF, (kk + PF) % (PF + 1));
+      const int s = kk % (PF + 1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s][i], bf[s][j], acc[i][j], 0, 0, 0);
+    }
+#else
+    // per-lane base pointers: every operand read below is base + compile-time offset,
+    // which folds into the DS instruction's immediate (no per-read address VALU)
+    const float* Al = AK ? As + lk * A_LD + wm + l32 : As + (wm + l32) * A_LD + lk;
+    const float* Bl = Bs + lk * B_LD + wn + l32;
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      float af[TM], bf[TN];
+#pragma unroll
+      for (int t = 0; t < TM; ++t) af[t] = AK ? Al[2 * kk * A_LD + 32 * t] : Al[32 * t * A_LD + 2 * kk];
+#pragma unroll
+      for (int t = 0; t < TN; ++t) bf[t] = Bl[2 * kk * B_LD + 32 * t];
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
+#endif
     if (kt + 1 < nk) store_tiles(cur ^ 1);
     __syncthreads();
   }
@@ -546,7 +736,7 @@ struct Plan {
   GemmArgs g{};
   int phases = 1;
   int cfg = CFG_L;
-  bool av = false, bv = false;
+  bool av = false, bv = false, fast = false;
   // packing
   bool pack = false;
   const float* prepacked = nullptr;  // caller-owned packed weights (skip packing)
@@ -612,6 +802,40 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 static bool vec_img_ok(const Img& im) {
   return im.sc == 1 && im.C % 4 == 0 && im.sh % 4 == 0 && im.sw % 4 == 0 && im.sb % 4 == 0 &&
          aligned16(im.p);
+}
+
+// bytes spanned by an image of `batch` samples (largest element offset + 1)
+static long long img_span_bytes(const Img& im, int batch) {
+  return 4LL * ((long long)(batch - 1) * im.sb + (long long)(im.H - 1) * im.sh + (long long)(im.W - 1) * im.sw +
+                (long long)(im.C - 1) * im.sc + 1);
+}
+
+// FAST-path eligibility (see gemm_kernel): call after choose_tiling
+static void set_fast(Plan& p, int batch) {
+  GemmArgs& g = p.g;
+  p.fast = false;
+  if (!p.av || !p.bv || g.K % BK != 0) return;
+  int bm, bn;
+  tile_dims(p.cfg, bm, bn);
+  const long long a_bytes = img_span_bytes(g.a, batch);
+  if (a_bytes > FAST_MAX_BYTES) return;
+  if (p.mode != MODE_WGRAD) {
+    const long long bw = 4LL * g.K * g.N * p.phases;
+    if ((int)g.fC.d % BK != 0 || bw > FAST_MAX_BYTES) return;
+    g.a_bytes = (int)a_bytes;
+    g.bw_bytes = (int)(4LL * g.K * g.N);
+  } else {
+    const long long im_bytes = img_span_bytes(g.im, batch);
+    if (im_bytes > FAST_MAX_BYTES) return;
+    if (g.a.sh != (long long)g.a.W * g.a.sw || g.a.sb != (long long)g.a.H * g.a.sh) return;
+    if (g.im.C % bn != 0) return;
+    g.a_bytes = (int)a_bytes;
+    g.im_bytes = (int)im_bytes;
+  }
+  p.fast = true;
+#if RGAN_EXP_NOLOAD  // timing-only experiment: zero-record descriptors drop every operand load
+  g.a_bytes = g.im_bytes = g.bw_bytes = 0;
+#endif
 }
 
 static void set_pack(Plan& p, const float* W, const float* scale, int K, int N, int pci, int pkw,
@@ -706,6 +930,7 @@ static int plan_fwd(const RganConv* d, const float* x, const float* w, const flo
   p.av = vec_img_ok(g.a);
   p.bv = g.N % 4 == 0;
   choose_tiling(p);
+  set_fast(p, d->batch);
   return 0;
 }
 
@@ -754,6 +979,7 @@ static int plan_dgrad(const RganConv* d, const float* dy, const float* w, const 
   p.av = vec_img_ok(g.a);
   p.bv = g.N % 4 == 0;
   choose_tiling(p);
+  set_fast(p, d->batch);
   return 0;
 }
 
@@ -786,6 +1012,7 @@ static int plan_wgrad(const RganConv* d, const float* x, const float* dy, float*
          aligned16(g.a.p);
   p.bv = vec_img_ok(g.im);
   choose_tiling(p);
+  set_fast(p, d->batch);
   return 0;
 }
 
@@ -801,10 +1028,11 @@ static void launch_pack(const PackArgs& a, hipStream_t s) {
 
 template <int MODE, int BM, int BN, int WM, int WN>
 static void launch_cfg(const Plan& p, dim3 grid, hipStream_t s) {
-  if (p.av && p.bv) gemm_kernel<MODE, BM, BN, WM, WN, true, true><<<grid, 256, 0, s>>>(p.g);
-  else if (p.av) gemm_kernel<MODE, BM, BN, WM, WN, true, false><<<grid, 256, 0, s>>>(p.g);
-  else if (p.bv) gemm_kernel<MODE, BM, BN, WM, WN, false, true><<<grid, 256, 0, s>>>(p.g);
-  else gemm_kernel<MODE, BM, BN, WM, WN, false, false><<<grid, 256, 0, s>>>(p.g);
+  if (p.fast) gemm_kernel<MODE, BM, BN, WM, WN, true, true, true><<<grid, 256, 0, s>>>(p.g);
+  else if (p.av && p.bv) gemm_kernel<MODE, BM, BN, WM, WN, true, true, false><<<grid, 256, 0, s>>>(p.g);
+  else if (p.av) gemm_kernel<MODE, BM, BN, WM, WN, true, false, false><<<grid, 256, 0, s>>>(p.g);
+  else if (p.bv) gemm_kernel<MODE, BM, BN, WM, WN, false, true, false><<<grid, 256, 0, s>>>(p.g);
+  else gemm_kernel<MODE, BM, BN, WM, WN, false, false, false><<<grid, 256, 0, s>>>(p.g);
 }
 
 template <int MODE>
@@ -833,20 +1061,29 @@ static std::vector<ProfRec> g_recs;
 static std::vector<std::string> g_kernel_names;
 static double g_cur_flops = 0.0;
 
-static int kernel_id(int mode, int cfg, bool av, bool bv) {
-  const int id = ((mode * 3 + cfg) * 2 + (av ? 1 : 0)) * 2 + (bv ? 1 : 0);
+constexpr int N_KERNEL_IDS = 45;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg)
+
+static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
+  const int id = fast ? 36 + mode * 3 + cfg : ((mode * 3 + cfg) * 2 + (av ? 1 : 0)) * 2 + (bv ? 1 : 0);
   if (g_kernel_names.empty()) {
-    g_kernel_names.resize(36);
+    g_kernel_names.resize(N_KERNEL_IDS);
     const int bm[3] = {128, 128, 256}, bn[3] = {128, 64, 32}, wmv[3] = {2, 2, 4}, wnv[3] = {2, 2, 1};
     for (int m = 0; m < 3; ++m)
       for (int c = 0; c < 3; ++c)
         for (int a = 0; a < 2; ++a)
           for (int b = 0; b < 2; ++b) {
             char buf[160];
-            snprintf(buf, sizeof(buf), "void rgan::gemm_kernel<%d, %d, %d, %d, %d, %s, %s>(rgan::GemmArgs)", m, bm[c],
-                     bn[c], wmv[c], wnv[c], a ? "true" : "false", b ? "true" : "false");
+            snprintf(buf, sizeof(buf), "void rgan::gemm_kernel<%d, %d, %d, %d, %d, %s, %s, false>(rgan::GemmArgs)", m,
+                     bm[c], bn[c], wmv[c], wnv[c], a ? "true" : "false", b ? "true" : "false");
             g_kernel_names[((m * 3 + c) * 2 + a) * 2 + b] = buf;
           }
+    for (int m = 0; m < 3; ++m)
+      for (int c = 0; c < 3; ++c) {
+        char buf[160];
+        snprintf(buf, sizeof(buf), "void rgan::gemm_kernel<%d, %d, %d, %d, %d, true, true, true>(rgan::GemmArgs)", m,
+                 bm[c], bn[c], wmv[c], wnv[c]);
+        g_kernel_names[36 + m * 3 + c] = buf;
+      }
   }
   return id;
 }
@@ -875,7 +1112,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     rec.a = g_pool[g_recs.size() * 2];
     rec.b = g_pool[g_recs.size() * 2 + 1];
     rec.flops = g_cur_flops;
-    rec.kid = kernel_id(p.mode, p.cfg, p.av, p.bv);
+    rec.kid = kernel_id(p.mode, p.cfg, p.av, p.bv, p.fast);
     hipEventRecord(rec.a, s);
   }
   switch (p.mode) {
@@ -1014,9 +1251,9 @@ static std::vector<long long> g_kn;
 
 extern "C" int rgan_profile_end(double* total_ms, double* total_flops, long long* launches) {
   g_prof = false;
-  g_kms.assign(36, 0.0);
-  g_kflops.assign(36, 0.0);
-  g_kn.assign(36, 0);
+  g_kms.assign(N_KERNEL_IDS, 0.0);
+  g_kflops.assign(N_KERNEL_IDS, 0.0);
+  g_kn.assign(N_KERNEL_IDS, 0);
   double ms = 0.0, fl = 0.0;
   if (!g_recs.empty()) {
     hipError_t rc = hipEventSynchronize(g_recs.back().b);
@@ -1040,7 +1277,7 @@ extern "C" int rgan_profile_end(double* total_ms, double* total_flops, long long
 }
 
 extern "C" int rgan_profile_kernel(int idx, char* name, int name_len, double* ms, double* flops, long long* n) {
-  if (idx < 0 || idx >= 36 || g_kms.empty()) return RGAN_EINVAL;
+  if (idx < 0 || idx >= N_KERNEL_IDS || g_kms.empty()) return RGAN_EINVAL;
   kernel_id(0, 0, false, false);
   if (name && name_len > 0) snprintf(name, name_len, "%s", g_kernel_names[idx].c_str());
   if (ms) *ms = g_kms[idx];

@@ -409,11 +409,11 @@ def profile_end():
     ms, fl, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_longlong()
     L.check(lib.rgan_profile_end(ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(n)), "rgan_profile_end")
     kern = []
-    for i in range(36):
+    for i in range(256):
         name = ctypes.create_string_buffer(200)
         kms, kfl, kn = ctypes.c_double(), ctypes.c_double(), ctypes.c_longlong()
-        L.check(lib.rgan_profile_kernel(i, name, 200, ctypes.byref(kms), ctypes.byref(kfl), ctypes.byref(kn)),
-                "rgan_profile_kernel")
+        if lib.rgan_profile_kernel(i, name, 200, ctypes.byref(kms), ctypes.byref(kfl), ctypes.byref(kn)) != 0:
+            break  # past the last kernel id
         if kn.value:
             kern.append({"name": name.value.decode(), "ms": kms.value, "flops": kfl.value, "launches": kn.value,
                          "tflops": kfl.value / kms.value / 1e9 if kms.value > 0 else 0.0})

@@ -1,0 +1,30 @@
+"""Build an experimental librgan variant with extra -D flags (GEMM tuning A/B runs).
+
+usage: python tools/build_variant.py NAME -DFOO=1 ...   -> relativisticgan_amd/build/variants/librgan_NAME.so
+Run with RGAN_LIB=<that path> to load it instead of the in-tree library.
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "relativisticgan_amd"))
+import build as B  # noqa: E402
+
+
+def main():
+    name, defs = sys.argv[1], sys.argv[2:]
+    out_dir = os.path.join(B.BUILD, "variants")
+    os.makedirs(out_dir, exist_ok=True)
+    B.build()
+    obj = os.path.join(out_dir, f"conv_gemm_{name}.o")
+    subprocess.run([B.HIPCC, *B.FLAGS, *defs, "-c", os.path.join(B.CSRC, "conv_gemm.hip"), "-o", obj], check=True,
+                   stderr=subprocess.DEVNULL)
+    objs = [obj] + [os.path.join(B.BUILD, s.replace(".hip", ".o")) for s in B.SOURCES if s != "conv_gemm.hip"]
+    so = os.path.join(out_dir, f"librgan_{name}.so")
+    subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o", so, *objs], check=True)
+    print(so)
+
+
+if __name__ == "__main__":
+    main()
