@@ -50,9 +50,13 @@ typedef struct RganConv {
  * `prepacked` != 0: the caller passes packed weights (no packing scratch).  0 = unsupported. */
 size_t rgan_conv_workspace(const RganConv* d, int which, int prepacked);
 
-/* GEMM-ready weight layout for which = 0 (fwd) or 1 (dgrad): [phases][K][N] floats.
- * Packing is separated so callers can cache it per weight version (weights change only
- * at the optimizer step, but each net is run 2-4 times per iteration). */
+/* Kernel-ready weight layout for which = 0 (fwd) or 1 (dgrad): [phases][K][N] floats for
+ * the implicit GEMMs, [Cin][4][4][Cout] for the narrow (<= 4 output channel) transposed
+ * conv.  Packing is separated so callers can cache it per weight version (weights change
+ * only at the optimizer step, but each net is run 2-4 times per iteration).
+ * rgan_conv_pack_floats returns 0 when the op reads the torch layout directly (narrow
+ * 4x4 convs with <= 4 input channels) -- or when the descriptor is unsupported, which
+ * rgan_conv_workspace reports separately (0). */
 size_t rgan_conv_pack_floats(const RganConv* d, int which);
 int rgan_conv_pack(const RganConv* d, int which, const float* w, float* packed, void* stream);
 

@@ -34,7 +34,7 @@ constexpr int OOB = (int)0x80000000;
 // fast-path tensors must fit a buffer descriptor with this margin
 constexpr long long FAST_MAX_BYTES = (1LL << 31) - (1LL << 24);
 
-enum { MODE_CONV = 0, MODE_CONVT2 = 1, MODE_WGRAD = 2 };
+enum { MODE_CONV = 0, MODE_CONVT2 = 1, MODE_WGRAD = 2, MODE_NARROW_T = 3, MODE_NARROW_IN = 4 };
 constexpr int BK = 32;
 
 // n / d for 0 <= n < 2^31 via multiply-high (host-computed magic numbers)
@@ -728,6 +728,212 @@ __global__ __launch_bounds__(256) void pack_weights(PackArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------- narrow convolutions
+// fp32 MFMA runs at the fp32 VALU rate on gfx950, so a GEMM with N <= 4 (a 32-wide MFMA
+// tile at <= 12% occupancy) or K <= 64 (one or two BK tiles around a full prologue and
+// epilogue) loses to a direct VALU convolution that wastes no lanes:
+//   convt2_narrow   k4 s2 p1 ConvTranspose2d (and the Conv2d dgrad of the same shape)
+//                   with <= 4 output channels: G's image layer (GLI:448) and D's image
+//                   gradient (the backward of GLI:361 into G).  One thread per input-grid
+//                   pixel computes the 4 output phases x NC channels from its 3x3
+//                   neighbourhood; weights are wave-uniform (scalar loads).
+//   conv_narrow_in  Conv2d with <= 4 input channels and a 4x4 kernel: D's image layer
+//                   (GLI:361).  One thread per output pixel x 32 output channels (grid.y
+//                   over channel groups; the weights of a group are wave-uniform).
+struct NarrowArgs {
+  const float* x;
+  long long xsb, xsc, xsh, xsw;
+  int B, H, W, C;         // input grid
+  const float* w;         // NARROW_T: packed [C][4][4][NC];  NARROW_IN: torch [Cout][C][KH][KW]
+  float* y;
+  long long ysb, ysc, ysh, ysw;
+  int Ho, Wo, Cout;
+  int stride, pad;
+  const float* bias;
+  const float* wscale;
+  int act;
+  float alpha;
+};
+
+constexpr int NT_T = 16, NT_HT = NT_T + 2, NT_CH = 32, NT_LDP = NT_CH + 4;
+
+// Block = a 16x16 tile of input-grid pixels of one sample; the (16+2)^2 halo tile is
+// staged through LDS 32 channels at a time with coalesced float4 loads (each pixel's
+// channel chunk is one 128-byte line), then every thread reads its 3x3 neighbourhood
+// from LDS (row stride 36 floats: conflict-free ds_read_b128 across 16 lanes).  The
+// chunk's weights are staged in LDS too and read as wave-uniform broadcasts: loading
+// them as 192 scalar values per step drove hipcc (ROCm 7.2) into SGPR spills that it
+// miscompiled (the spilled weight pointer was overwritten by another kernel argument).
+template <int NC>
+__global__ __launch_bounds__(256) void convt2_narrow(NarrowArgs a) {
+  __shared__ __attribute__((aligned(16))) float xs[NT_HT * NT_HT * NT_LDP];
+  __shared__ __attribute__((aligned(16))) float wl[NT_CH * 16 * NC];
+  const int tid = threadIdx.x;
+  const int tiles_w = (a.W + NT_T - 1) / NT_T, tiles_h = (a.H + NT_T - 1) / NT_T;
+  const int per_img = tiles_w * tiles_h;
+  const int b = blockIdx.x / per_img, trem = blockIdx.x - b * per_img;
+  const int ty = trem / tiles_w, tx = trem - ty * tiles_w;
+  const int ti = tid / NT_T, tj = tid % NT_T;
+  const int i = ty * NT_T + ti, j = tx * NT_T + tj;
+  const float* xb = a.x + (long long)b * a.xsb;
+  float acc[4][NC];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[q][c] = 0.f;
+  const float* __restrict__ wp = a.w;
+  for (int c0 = 0; c0 < a.C; c0 += NT_CH) {
+    __syncthreads();
+    for (int e = tid; e < NT_HT * NT_HT * (NT_CH / 4); e += 256) {
+      const int pix = e / (NT_CH / 4), q = e % (NT_CH / 4);
+      const int hi = pix / NT_HT, hj = pix - hi * NT_HT;
+      const int ih = ty * NT_T - 1 + hi, iw = tx * NT_T - 1 + hj, c = c0 + 4 * q;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W && c < a.C)
+        v = *reinterpret_cast<const float4*>(xb + (long long)ih * a.xsh + (long long)iw * a.xsw + c);
+      *reinterpret_cast<float4*>(xs + pix * NT_LDP + 4 * q) = v;
+    }
+    const int nw = min(NT_CH, a.C - c0) * 16 * NC;
+    for (int e = tid; e < nw; e += 256) wl[e] = wp[(size_t)c0 * 16 * NC + e];
+    __syncthreads();
+    const int nq = min(NT_CH, a.C - c0) / 4;
+    for (int c4 = 0; c4 < nq; ++c4) {
+      float4 xv[3][3];
+#pragma unroll
+      for (int u = 0; u < 3; ++u)
+#pragma unroll
+        for (int v = 0; v < 3; ++v)
+          xv[u][v] = *reinterpret_cast<const float4*>(xs + ((ti + u) * NT_HT + tj + v) * NT_LDP + 4 * c4);
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        const float* wr = wl + (4 * c4 + cc) * 16 * NC;
+#pragma unroll
+        for (int ph = 0; ph < 2; ++ph)
+#pragma unroll
+          for (int pw = 0; pw < 2; ++pw)
+#pragma unroll
+            for (int th = 0; th < 2; ++th)
+#pragma unroll
+              for (int tw = 0; tw < 2; ++tw) {
+                // output (2i+ph, 2j+pw) <- input (i+ph-th, j+pw-tw) through tap (2th+1-ph, 2tw+1-pw)
+                const float4 xq = xv[ph - th + 1][pw - tw + 1];
+                const float xsv = cc == 0 ? xq.x : cc == 1 ? xq.y : cc == 2 ? xq.z : xq.w;
+                const int tap = (2 * th + 1 - ph) * 4 + (2 * tw + 1 - pw);
+#pragma unroll
+                for (int c = 0; c < NC; ++c)
+                  acc[ph * 2 + pw][c] = fmaf(xsv, wr[tap * NC + c], acc[ph * 2 + pw][c]);
+              }
+      }
+    }
+  }
+  if (i >= a.H || j >= a.W) return;
+  const float wsc = a.wscale ? a.wscale[0] : 1.f;
+  float* yb = a.y + (long long)b * a.ysb;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const long long o = (long long)(2 * i + (q >> 1)) * a.ysh + (long long)(2 * j + (q & 1)) * a.ysw;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const float v = acc[q][c] * wsc + (a.bias ? a.bias[c] : 0.f);
+      yb[o + (long long)c * a.ysc] = act_fwd(v, a.act, a.alpha);
+    }
+  }
+}
+
+constexpr int NARROW_CG = 32;  // output channels per thread in conv_narrow_in
+
+template <int CI>
+__global__ __launch_bounds__(256) void conv_narrow_in(NarrowArgs a) {
+  constexpr int KP = CI * 16;  // patch (ci, kh, kw) of a 4x4 kernel
+  const int HWo = a.Ho * a.Wo;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= a.B * HWo) return;
+  const int b = idx / HWo, rem = idx - b * HWo, oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
+  float patch[KP];
+  const float* xb = a.x + (long long)b * a.xsb;
+#pragma unroll
+  for (int ci = 0; ci < CI; ++ci)
+#pragma unroll
+    for (int kh = 0; kh < 4; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 4; ++kw) {
+        const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
+        patch[(ci * 4 + kh) * 4 + kw] =
+            ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                ? xb[(long long)ci * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
+                : 0.f;
+      }
+  const int co0 = blockIdx.y * NARROW_CG;
+  const float* __restrict__ wg = a.w + (size_t)co0 * KP;
+  const float wsc = a.wscale ? a.wscale[0] : 1.f;
+  float* yp = a.y + (long long)b * a.ysb + (long long)oh * a.ysh + (long long)ow * a.ysw;
+  const int ncg = min(NARROW_CG, a.Cout - co0);
+  float out[NARROW_CG];
+#pragma unroll
+  for (int c = 0; c < NARROW_CG; ++c) {
+    float s = 0.f;
+    if (c < ncg) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) s = fmaf(patch[k], wg[c * KP + k], s);
+    }
+    out[c] = act_fwd(s * wsc + (a.bias && c < ncg ? a.bias[co0 + c] : 0.f), a.act, a.alpha);
+  }
+  if (a.ysc == 1 && ncg == NARROW_CG && ((uintptr_t)(yp + co0) & 15) == 0) {
+#pragma unroll
+    for (int c = 0; c < NARROW_CG; c += 4)
+      *reinterpret_cast<float4*>(yp + co0 + c) = make_float4(out[c], out[c + 1], out[c + 2], out[c + 3]);
+  } else {
+#pragma unroll
+    for (int c = 0; c < NARROW_CG; ++c)
+      if (c < ncg) yp[(long long)(co0 + c) * a.ysc] = out[c];
+  }
+}
+
+// packed narrow-ConvT weights: out[ci][kh][kw][co] = W[ci * s_in + co * s_out + kh * 4 + kw]
+__global__ void pack_narrow(const float* __restrict__ W, float* __restrict__ out, int C, int NC, long long s_in,
+                            long long s_out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= C * 16 * NC) return;
+  const int co = e % NC, t = (e / NC) % 16, ci = e / (16 * NC);
+  out[e] = W[ci * s_in + co * s_out + t];
+}
+
+// Tiled pack for the layouts whose columns are one weight index (n = out_idx) and whose
+// rows are (tap, in_idx) with in_idx fastest -- every pack on the FAST paths: a block
+// moves a 16 in x 16 out x (<= 16 taps) brick through LDS, reading W in its own
+// contiguous order (taps, then the smaller-stride index) and writing 16-column rows.
+__global__ __launch_bounds__(256) void pack_tiled(PackArgs a) {
+  __shared__ float t[16][16][17];  // [in][out][tap]
+  const int KK = a.KH * a.KW;
+  const int Nin = (int)a.fpci.d, Nout = a.N;
+  const int i0 = blockIdx.x * 16, o0 = blockIdx.y * 16;
+  const bool in_fast = a.s_in < a.s_out;
+  for (int e = threadIdx.x; e < 16 * 16 * 16; e += 256) {
+    const int tap = e & 15, u = (e >> 4) & 15, v = e >> 8;
+    const int i = in_fast ? u : v, o = in_fast ? v : u;
+    float val = 0.f;
+    if (tap < KK && i0 + i < Nin && o0 + o < Nout)
+      val = a.W[(long long)(i0 + i) * a.s_in + (long long)(o0 + o) * a.s_out + tap];
+    t[i][o][tap] = val;
+  }
+  __syncthreads();
+  const int K = a.K;
+  for (int e = threadIdx.x; e < 16 * 16 * 16; e += 256) {
+    const int o = e & 15, i = (e >> 4) & 15, tap = e >> 8;
+    if (tap >= KK || i0 + i >= Nin || o0 + o >= Nout) continue;
+    const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
+    int phase = 0, kt;
+    if (a.convt2) {  // tap (kh, kw) of phase (ph, pw) = (2th+1-ph, 2tw+1-pw)
+      phase = (1 - (kh & 1)) * 2 + (1 - (kw & 1));
+      kt = (kh >> 1) * 2 + (kw >> 1);
+    } else {
+      kt = a.flip ? (a.KH - 1 - kh) * a.KW + (a.KW - 1 - kw) : tap;
+    }
+    a.out[((size_t)phase * K + (size_t)kt * Nin + i0 + i) * Nout + o0 + o] = t[i][o][tap];
+  }
+}
+
 // ---------------------------------------------------------------- host planning
 enum { CFG_L = 0, CFG_M = 1, CFG_N = 2 };
 
@@ -742,6 +948,9 @@ struct Plan {
   const float* prepacked = nullptr;  // caller-owned packed weights (skip packing)
   PackArgs pk{};
   size_t pack_floats = 0, slab_floats = 0;
+  // narrow kernels (MODE_NARROW_T / MODE_NARROW_IN)
+  NarrowArgs na{};
+  long long pn_s_in = 0, pn_s_out = 0;  // narrow pack strides
 };
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
@@ -874,12 +1083,56 @@ static bool is_k4s2p1(const RganConv* d) {
   return d->kh == 4 && d->kw == 4 && d->stride == 2 && d->pad == 1;
 }
 
+static bool vec_nhwc(const float* p, const long long* s, int C) {
+  return s[1] == 1 && C % 4 == 0 && s[0] % 4 == 0 && s[2] % 4 == 0 && s[3] % 4 == 0 && aligned16(p);
+}
+
+// k4 s2 p1 ConvTranspose2d over input grid x (channels C, NHWC) with nc <= 4 outputs;
+// weight element (in ci, out co, kh, kw) at w[ci * s_in + co * s_out + kh * 4 + kw]
+static bool plan_narrow_t(Plan& p, int batch, const float* x, const long long* xs, int H, int W, int C,
+                          const float* w, long long s_in, long long s_out, int nc, float* y, const long long* ys,
+                          const float* wscale, const float* bias, int act, float alpha) {
+  if (nc > 4 || !vec_nhwc(x, xs, C)) return false;
+  p.mode = MODE_NARROW_T;
+  NarrowArgs& a = p.na;
+  a.x = x; a.xsb = xs[0]; a.xsc = xs[1]; a.xsh = xs[2]; a.xsw = xs[3];
+  a.B = batch; a.H = H; a.W = W; a.C = C;
+  a.w = w; a.y = y; a.ysb = ys[0]; a.ysc = ys[1]; a.ysh = ys[2]; a.ysw = ys[3];
+  a.Ho = 2 * H; a.Wo = 2 * W; a.Cout = nc; a.stride = 2; a.pad = 1;
+  a.bias = bias; a.wscale = wscale; a.act = act; a.alpha = alpha;
+  p.pack = true;
+  p.pack_floats = (size_t)C * 16 * nc;
+  p.pn_s_in = s_in; p.pn_s_out = s_out;
+  p.pk.W = w;
+  return true;
+}
+
+// Conv2d with a 4x4 kernel and <= 4 input channels (any input strides)
+static bool plan_narrow_in(Plan& p, const RganConv* d, const float* x, const float* w, const float* wscale,
+                           const float* bias, float* y, int act, float alpha) {
+  if (d->transposed || d->cin > 4 || d->kh != 4 || d->kw != 4) return false;
+  p.mode = MODE_NARROW_IN;
+  NarrowArgs& a = p.na;
+  a.x = x; a.xsb = d->xs[0]; a.xsc = d->xs[1]; a.xsh = d->xs[2]; a.xsw = d->xs[3];
+  a.B = d->batch; a.H = d->hin; a.W = d->win; a.C = d->cin;
+  a.w = w; a.y = y; a.ysb = d->ys[0]; a.ysc = d->ys[1]; a.ysh = d->ys[2]; a.ysw = d->ys[3];
+  a.Ho = d->hout; a.Wo = d->wout; a.Cout = d->cout; a.stride = d->stride; a.pad = d->pad;
+  a.bias = bias; a.wscale = wscale; a.act = act; a.alpha = alpha;
+  p.pack = false;
+  return true;
+}
+
 // forward GEMM over the conv's input x producing y (conv or transposed conv)
 static int plan_fwd(const RganConv* d, const float* x, const float* w, const float* wscale,
                     const float* bias, float* y, int act, float alpha, Plan& p) {
   if (!desc_ok(d)) return RGAN_EINVAL;
   GemmArgs& g = p.g;
   const int KK = d->kh * d->kw;
+  if (d->transposed && is_k4s2p1(d) && d->hout == 2 * d->hin && d->wout == 2 * d->win &&
+      plan_narrow_t(p, d->batch, x, d->xs, d->hin, d->win, d->cin, w, (long long)d->cout * 16, 16, d->cout, y, d->ys,
+                    wscale, bias, act, alpha))
+    return 0;
+  if (plan_narrow_in(p, d, x, w, wscale, bias, y, act, alpha)) return 0;
   g.a = make_img(x, d->hin, d->win, d->cin, d->xs);
   g.C = y; g.bias = bias; g.act = act; g.alpha = alpha;
   if (!d->transposed) {
@@ -940,6 +1193,11 @@ static int plan_dgrad(const RganConv* d, const float* dy, const float* w, const 
   if (!desc_ok(d)) return RGAN_EINVAL;
   GemmArgs& g = p.g;
   const int KK = d->kh * d->kw;
+  // Conv2d k4 s2 p1 dgrad == ConvT of dy with W[co][ci] read as [in=co][out=ci]
+  if (!d->transposed && is_k4s2p1(d) && d->hin == 2 * d->hout && d->win == 2 * d->wout &&
+      plan_narrow_t(p, d->batch, dy, d->ys, d->hout, d->wout, d->cout, w, (long long)d->cin * 16, 16, d->cin, dx,
+                    d->xs, wscale, nullptr, RGAN_ACT_NONE, 0.f))
+    return 0;
   g.a = make_img(dy, d->hout, d->wout, d->cout, d->ys);
   g.C = dx; g.bias = nullptr; g.act = RGAN_ACT_NONE; g.alpha = 0.f;
   g.out = make_out(d->hin, d->win, 1, d->xs[0], d->xs[2], d->xs[3], 1, 1, d->cin, 0, 0, d->xs[1]);
@@ -1022,6 +1280,12 @@ static size_t plan_ws_bytes(const Plan& p) {
 }
 
 static void launch_pack(const PackArgs& a, hipStream_t s) {
+  // tiled when n is one weight index and the taps are contiguous in W
+  if (a.fnco.d == (uint32_t)a.N && a.fnkw.d == 1 && a.s_kw == 1 && a.s_kh == a.KW && a.KH * a.KW <= 16 &&
+      (!a.convt2 || (a.KH == 4 && a.KW == 4))) {
+    pack_tiled<<<dim3(ceil_div((int)a.fpci.d, 16), ceil_div(a.N, 16)), 256, 0, s>>>(a);
+    return;
+  }
   const int ky = std::min(a.K, 8192);
   pack_weights<<<dim3(ceil_div(a.N, 256), ky, a.phases), 256, 0, s>>>(a);
 }
@@ -1061,10 +1325,13 @@ static std::vector<ProfRec> g_recs;
 static std::vector<std::string> g_kernel_names;
 static double g_cur_flops = 0.0;
 
-constexpr int N_KERNEL_IDS = 45;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg)
+constexpr int N_KERNEL_IDS = 47;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow
 
 static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
-  const int id = fast ? 36 + mode * 3 + cfg : ((mode * 3 + cfg) * 2 + (av ? 1 : 0)) * 2 + (bv ? 1 : 0);
+  const int id = mode == MODE_NARROW_T ? 45
+                 : mode == MODE_NARROW_IN ? 46
+                 : fast ? 36 + mode * 3 + cfg
+                        : ((mode * 3 + cfg) * 2 + (av ? 1 : 0)) * 2 + (bv ? 1 : 0);
   if (g_kernel_names.empty()) {
     g_kernel_names.resize(N_KERNEL_IDS);
     const int bm[3] = {128, 128, 256}, bn[3] = {128, 64, 32}, wmv[3] = {2, 2, 4}, wnv[3] = {2, 2, 1};
@@ -1084,12 +1351,72 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
                  bm[c], bn[c], wmv[c], wnv[c]);
         g_kernel_names[36 + m * 3 + c] = buf;
       }
+    g_kernel_names[45] = "void rgan::convt2_narrow<NC>(rgan::NarrowArgs)";
+    g_kernel_names[46] = "void rgan::conv_narrow_in<CI>(rgan::NarrowArgs)";
   }
   return id;
 }
 
+static void launch_pack_plan(Plan& p, float* out, hipStream_t s) {
+  if (p.mode == MODE_NARROW_T) {
+    const int n = p.na.C * 16 * p.na.Cout;
+    pack_narrow<<<ceil_div(n, 256), 256, 0, s>>>(p.pk.W, out, p.na.C, p.na.Cout, p.pn_s_in, p.pn_s_out);
+  } else {
+    p.pk.out = out;
+    launch_pack(p.pk, s);
+  }
+}
+
+static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
+  NarrowArgs a = p.na;
+  if (p.mode == MODE_NARROW_T) {
+    a.w = packed;
+    const int blocks = a.B * ceil_div(a.H, NT_T) * ceil_div(a.W, NT_T);
+    switch (a.Cout) {
+      case 1: convt2_narrow<1><<<blocks, 256, 0, s>>>(a); break;
+      case 2: convt2_narrow<2><<<blocks, 256, 0, s>>>(a); break;
+      case 3: convt2_narrow<3><<<blocks, 256, 0, s>>>(a); break;
+      default: convt2_narrow<4><<<blocks, 256, 0, s>>>(a); break;
+    }
+  } else {
+    dim3 grid(ceil_div(a.B * a.Ho * a.Wo, 256), ceil_div(a.Cout, NARROW_CG));
+    switch (a.C) {
+      case 1: conv_narrow_in<1><<<grid, 256, 0, s>>>(a); break;
+      case 2: conv_narrow_in<2><<<grid, 256, 0, s>>>(a); break;
+      case 3: conv_narrow_in<3><<<grid, 256, 0, s>>>(a); break;
+      default: conv_narrow_in<4><<<grid, 256, 0, s>>>(a); break;
+    }
+  }
+  return 0;
+}
+
 static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   if (ws_bytes < plan_ws_bytes(p)) return RGAN_EINVAL;
+  if (p.mode == MODE_NARROW_T || p.mode == MODE_NARROW_IN) {
+    const float* packed = p.prepacked;
+    if (p.pack && !packed) {
+      if (!ws) return RGAN_EINVAL;
+      launch_pack_plan(p, (float*)ws, s);
+      RGAN_CHECK_LAUNCH();
+      packed = (const float*)ws;
+    }
+    ProfRec rec{};
+    const bool prof = g_prof && g_recs.size() * 2 + 2 <= g_pool.size();
+    if (prof) {
+      rec.a = g_pool[g_recs.size() * 2];
+      rec.b = g_pool[g_recs.size() * 2 + 1];
+      rec.flops = g_cur_flops;
+      rec.kid = kernel_id(p.mode, 0, false, false);
+      hipEventRecord(rec.a, s);
+    }
+    run_narrow(p, packed, s);
+    RGAN_CHECK_LAUNCH();
+    if (prof) {
+      hipEventRecord(rec.b, s);
+      g_recs.push_back(rec);
+    }
+    return 0;
+  }
   if (p.g.M <= 0 || p.g.N <= 0 || p.g.K <= 0) return RGAN_EINVAL;
   char* w = (char*)ws;
   if (p.pack && p.prepacked) {
@@ -1159,7 +1486,7 @@ extern "C" size_t rgan_conv_pack_floats(const RganConv* d, int which) {
   static const float dummy[4] = {0, 0, 0, 0};
   int rc = which == 0 ? plan_fwd(d, dummy, dummy, nullptr, nullptr, (float*)dummy, 0, 0.f, p)
                       : plan_dgrad(d, dummy, dummy, nullptr, (float*)dummy, p);
-  if (rc || which > 1) return 0;
+  if (rc || which > 1 || !p.pack) return 0;  // 0: no packed layout (or unsupported)
   return p.pack_floats;
 }
 
@@ -1170,8 +1497,8 @@ extern "C" int rgan_conv_pack(const RganConv* d, int which, const float* w, floa
   int rc = which == 0 ? plan_fwd(d, dummy, w, nullptr, nullptr, (float*)dummy, 0, 0.f, p)
                       : plan_dgrad(d, dummy, w, nullptr, (float*)dummy, p);
   if (rc) return rc;
-  p.pk.out = packed;
-  launch_pack(p.pk, (hipStream_t)stream);
+  if (!p.pack) return RGAN_EINVAL;
+  launch_pack_plan(p, packed, (hipStream_t)stream);
   RGAN_CHECK_LAUNCH();
   return 0;
 }

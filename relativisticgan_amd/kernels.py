@@ -84,7 +84,7 @@ class _PackCache:
         lib = L.lib()
         n = lib.rgan_conv_pack_floats(ctypes.byref(d), which)
         if n == 0:
-            raise L.RganError(f"unsupported conv {geom} (pack)")
+            return None  # the op reads the torch layout directly (or is unsupported: workspace says)
         reuse = ent is not None and ent[0]() is base and ent[2].numel() == n
         buf = ent[2] if reuse else torch.empty(n, dtype=torch.float32, device=w.device)
         L.check(lib.rgan_conv_pack(ctypes.byref(d), which, L.ptr(w), L.ptr(buf), L.stream()), "rgan_conv_pack")

@@ -95,6 +95,32 @@ def test_conv_bias_act(K):
     assert _rel(db, dy.double().sum((0, 2, 3))) < 1e-6
 
 
+@pytest.mark.parametrize("nc", [1, 2, 3, 4])
+def test_conv_narrow_paths(K, nc):
+    """Narrow kernels: ConvT k4s2p1 with nc outputs (and the Conv2d dgrad of that shape),
+    Conv2d with nc inputs; bias / activation / wscale epilogue and the cached pack."""
+    torch.manual_seed(nc)
+    gt, gc = K.ConvGeom(4, 2, 1, True), K.ConvGeom(4, 2, 1, False)
+    x = _nhwc(torch.randn(3, 16, 6, 6, device=DEV))
+    w = torch.nn.Parameter(torch.randn(16, nc, 4, 4, device=DEV) * 0.1)
+    b = torch.randn(nc, device=DEV)
+    s = torch.tensor([0.5], device=DEV)
+    for cache in (False, True, True):
+        y = K.conv_fwd(x, w, gt, bias=b, act="tanh", wscale=s, nchw_out=True, cache=cache)
+        assert _rel(y, torch.tanh(_ref_conv(x, w * 0.5, gt, b))) < 3e-6
+    img = torch.randn(3, nc, 12, 12, device=DEV)
+    wc = torch.nn.Parameter(torch.randn(40, nc, 4, 4, device=DEV) * 0.1)
+    bc = torch.randn(40, device=DEV)
+    for cache in (False, True):
+        y = K.conv_fwd(img, wc, gc, bias=bc, act="lrelu", alpha=0.2, wscale=s, cache=cache)
+        assert _rel(y, F.leaky_relu(_ref_conv(img, wc * 0.5, gc, bc), 0.2)) < 3e-6
+        dy = _nhwc(torch.randn(3, 40, 6, 6, device=DEV))
+        dx = K.conv_dgrad(dy, wc, gc, img.shape, wscale=s, like=img, cache=cache)
+        x64 = img.double().cpu().requires_grad_(True)
+        F.conv2d(x64, (wc * 0.5).double().cpu(), stride=2, padding=1).backward(dy.double().cpu())
+        assert _rel(dx, x64.grad) < 3e-6
+
+
 def test_conv_wscale(K):
     g = K.ConvGeom(4, 2, 1, False)
     x = _nhwc(torch.randn(2, 8, 8, 8, device=DEV))
