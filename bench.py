@@ -67,6 +67,22 @@ def conv_flops_per_iteration(t):
     return 9 * sum(fd) + 4 * sum(fg) - 2 * fd[0] - fg[0]
 
 
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "round1_c2_pmc_traffic.json")
+
+
+def pmc_traffic(workload, symbol):
+    """HBM-side bytes per launch of `symbol` from the committed rocprofv3 PMC passes
+    (tools/pmc_traffic.sh on this bench command: FETCH_SIZE x2 + WRITE_SIZE), or None."""
+    if workload != "C2" or not os.path.exists(PMC_TRAFFIC):
+        return None, None
+    with open(PMC_TRAFFIC) as f:
+        d = json.load(f)
+    ent = d.get(symbol)
+    if ent is None:
+        return None, None
+    return ent["bytes_per_launch"], os.path.relpath(PMC_TRAFFIC, ROOT)
+
+
 def cpu_baseline(loss_D, size, batch, h, spectral, seconds_hint):
     """Oracle (CPU restatement, pinned to the reference) on this host: bounded sample."""
     from oracle.reference_cpu import Trainer as OracleTrainer, make_param, synthetic_images
@@ -143,15 +159,21 @@ def main():
     imgs = bpg * world * args.steps
     value = imgs / elapsed
     ms_step = 1000.0 * elapsed / args.steps
-    # dominant kernel = the implicit-GEMM conv family; report its top symbol too
+    # dominant kernel = the conv kernel symbol with the most time (HIP events around each
+    # launch on its stream); the whole conv family is reported beside it
     gemm_ms, gemm_flops = prof["ms"], prof["flops"]
-    top = max(prof["kernels"], key=lambda k: k["ms"]) if prof["kernels"] else None
-    achieved = gemm_flops / (gemm_ms / 1000.0) if gemm_ms > 0 else 0.0
+    top = max(prof["kernels"], key=lambda k: k["ms"])
+    achieved = top["flops"] / (top["ms"] / 1000.0)
+    traffic, traffic_src = pmc_traffic(args.workload, top["name"])
     roofline = {"bound": "mfma", "achieved": achieved / 1e12, "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
-                "frac": achieved / FP32_MFMA_PEAK, "traffic": None,
-                "kernel": "rgan::gemm_kernel<...> (all conv fwd/dgrad/wgrad launches)",
-                "launches": prof["launches"], "avg_launch_us": 1000.0 * gemm_ms / max(prof["launches"], 1),
-                "top_symbol": top}
+                "frac": achieved / FP32_MFMA_PEAK, "traffic": traffic, "traffic_unit": "bytes/launch",
+                "traffic_source": traffic_src, "kernel": top["name"], "launches": top["launches"],
+                "avg_launch_us": 1000.0 * top["ms"] / top["launches"],
+                "flops_per_launch": top["flops"] / top["launches"],
+                "conv_family": {"achieved": gemm_flops / (gemm_ms / 1000.0) / 1e12, "launches": prof["launches"],
+                                "ms_per_step": gemm_ms / args.steps,
+                                "frac": gemm_flops / (gemm_ms / 1000.0) / FP32_MFMA_PEAK,
+                                "kernels": prof["kernels"]}}
     out = {
         "metric": METRIC, "value": value, "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
