@@ -79,6 +79,17 @@ int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* w, const fl
 int rgan_conv_wgrad(const RganConv* d, const float* x, const float* dy, float* dw, float* dbias,
                     void* ws, size_t ws_bytes, void* stream);
 
+/* ---- --NN_conv blocks: Upsample(scale_factor=2, nearest) + Conv2d(k3, s1, p1) ----
+ * (GLI:351-356 middle, GLI:377-382 end).  conv3x3(up2(x), W) equals a k4 s2 p1
+ * ConvTranspose2d of x with the folded weight Wt = A W A^T per 3x3 slice
+ * (A = [[0,0,1],[0,1,1],[1,1,0],[1,0,0]]), so the layer runs as rgan_conv_* with
+ * transposed = 1, k = 4, stride 2, pad 1 on Wt.
+ * rgan_nn_fold_weight: W [cout][cin][3][3] -> Wt [cin][cout][4][4] (16-byte aligned).
+ * rgan_nn_unfold_grad: the adjoint, dWt [cin][cout][4][4] -> dW [cout][cin][3][3]
+ * (the Conv2d weight gradient, aten convolution_backward grad_weight). */
+int rgan_nn_fold_weight(const float* w, int cout, int cin, float* wt, void* stream);
+int rgan_nn_unfold_grad(const float* dwt, int cout, int cin, float* dw, void* stream);
+
 /* ---- BatchNorm2d, train mode (GLI:341,366,433; arch 1 GLI:204-218,262-297) ----
  * Tensors are [batch*h*w][C] with element strides (sp = pixel stride, sc = channel
  * stride); P = batch*h*w.  stats = float[2*C] workspace slot receiving (mean, invstd).

@@ -34,6 +34,8 @@ _SIGS = {
                               c_vp]),
     "rgan_conv_dgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "rgan_conv_wgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "rgan_nn_fold_weight": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    "rgan_nn_unfold_grad": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
     "rgan_bn_partial_bytes": (c_sz, [c_ll, c_int]),
     "rgan_bn_stats": (c_int, [c_vp, c_ll, c_int, c_ll, c_ll, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rgan_bn_moments": (c_int, [c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp]),

@@ -25,6 +25,7 @@ import torch.distributed as dist
 
 class _State:
     group = None
+    grad_group = None  # second communicator for the bucketed gradient all-reduce
     world = 1
     rank = 0
     sync_bn = True
@@ -36,16 +37,21 @@ _S = _State()
 def setup(group=None, sync_bn=True):
     """Activate data-parallel mode for the current process (after init_process_group)."""
     if not dist.is_available() or not dist.is_initialized():
-        _S.group, _S.world, _S.rank = None, 1, 0
+        _S.group, _S.grad_group, _S.world, _S.rank = None, None, 1, 0
     else:
         _S.group = group
         _S.world = dist.get_world_size(group)
         _S.rank = dist.get_rank(group)
+        # The overlapped gradient buckets get their own communicator (own RCCL stream):
+        # on the shared one, every latency-critical SyncBN all-reduce of the remaining
+        # backward would queue behind a 32 MB bucket in flight.
+        ranks = dist.get_process_group_ranks(group) if group is not None else list(range(_S.world))
+        _S.grad_group = dist.new_group(ranks=ranks) if _S.world > 1 else group
     _S.sync_bn = sync_bn
 
 
 def reset():
-    _S.group, _S.world, _S.rank, _S.sync_bn = None, 1, 0, True
+    _S.group, _S.grad_group, _S.world, _S.rank, _S.sync_bn = None, None, 1, 0, True
 
 
 def world():
@@ -104,6 +110,95 @@ def merge_moments(moments, C):
         S = S + sb + d * d * torch.where(nt > 0, N * nb / nt.clamp_min(1), torch.zeros_like(nb))
         N = nt
     return M, S / N, N
+
+
+class GradReducer:
+    """Gradient all-reduce overlapped with the backward pass.
+
+    Parameters are split once into static buckets (~``bucket_bytes``, in reverse
+    registration order, i.e. roughly the order the backward produces their gradients).
+    While ``arm()``-ed, a post-accumulate-grad hook marks each parameter ready; when a
+    bucket is complete it is flattened and its SUM all-reduce is launched asynchronously
+    (RCCL runs it on its own stream, overlapping the rest of the backward).  Buckets are
+    launched strictly in bucket order, so every rank issues the same collective sequence
+    whatever order its hooks fire in.  ``finish()`` launches whatever is left (parameters
+    whose gradient came only from an earlier backward of the same step), waits, and
+    points each ``.grad`` at its slice of the reduced flat buffer (no copy back).
+
+    Arm only around the LAST backward of an optimizer step: the loop's heads 1-4 run two
+    backwards (GLI:596-624) and WGAN-GP a third (GLI:658); gradients accumulated by the
+    earlier ones are already in ``.grad`` when the last one's hooks fire."""
+
+    def __init__(self, params, bucket_bytes=32 << 20):
+        self.params = [q for q in params if q.requires_grad]
+        self.buckets, cur, size = [], [], 0
+        for q in reversed(self.params):
+            cur.append(q)
+            size += q.numel() * q.element_size()
+            if size >= bucket_bytes:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.where = {}
+        for bi, b in enumerate(self.buckets):
+            for q in b:
+                self.where[id(q)] = bi
+        self.armed = False
+        self.handles = [q.register_post_accumulate_grad_hook(self._hook) for q in self.params]
+        self._reset()
+
+    def _reset(self):
+        self.pending = [len(b) for b in self.buckets]
+        self.ready = set()
+        self.next = 0
+        self.inflight = []
+
+    def arm(self):
+        if _S.world > 1:
+            self._reset()
+            self.armed = True
+
+    def _hook(self, q):
+        if not self.armed or id(q) in self.ready:
+            return
+        self.ready.add(id(q))
+        self.pending[self.where[id(q)]] -= 1
+        while self.next < len(self.buckets) and self.pending[self.next] == 0:
+            self._launch(self.next)
+            self.next += 1
+
+    def _launch(self, bi):
+        qs = [q for q in self.buckets[bi] if q.grad is not None]
+        if not qs:
+            return
+        flat = torch.cat([q.grad.reshape(-1) for q in qs])
+        work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=_S.grad_group, async_op=True)
+        self.inflight.append((work, flat, qs))
+
+    def finish(self):
+        """Complete every bucket's all-reduce; afterwards .grad holds the global SUM."""
+        if _S.world == 1:
+            return
+        if not self.armed:  # no overlapped backward this step: reduce everything now
+            self._reset()
+        while self.next < len(self.buckets):
+            self._launch(self.next)
+            self.next += 1
+        for work, flat, qs in self.inflight:
+            work.wait()
+            off = 0
+            for q in qs:
+                n = q.numel()
+                q.grad = flat[off:off + n].view_as(q)
+                off += n
+        self.inflight = []
+        self.armed = False
+
+    def remove(self):
+        for h in self.handles:
+            h.remove()
+        self.handles = []
 
 
 def allreduce_grads(params, bucket_bytes=64 << 20):

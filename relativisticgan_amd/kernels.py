@@ -21,16 +21,30 @@ class ConvGeom:
     stride: int
     pad: int
     transposed: bool
+    upsample: int = 1  # 2: nearest Upsample(x2) in front of the conv (--NN_conv, GLI:351-356)
 
     def out_hw(self, h, w):
+        h, w = h * self.upsample, w * self.upsample
         if self.transposed:
             return ((h - 1) * self.stride - 2 * self.pad + self.k, (w - 1) * self.stride - 2 * self.pad + self.k)
         return ((h + 2 * self.pad - self.k) // self.stride + 1, (w + 2 * self.pad - self.k) // self.stride + 1)
 
     def in_hw(self, ho, wo):
         if self.transposed:
-            return ((ho + 2 * self.pad - self.k) // self.stride + 1, (wo + 2 * self.pad - self.k) // self.stride + 1)
-        return ((ho - 1) * self.stride - 2 * self.pad + self.k, (wo - 1) * self.stride - 2 * self.pad + self.k)
+            h, w = (ho + 2 * self.pad - self.k) // self.stride + 1, (wo + 2 * self.pad - self.k) // self.stride + 1
+        else:
+            h, w = (ho - 1) * self.stride - 2 * self.pad + self.k, (wo - 1) * self.stride - 2 * self.pad + self.k
+        return h // self.upsample, w // self.upsample
+
+
+# Upsample(x2)+Conv2d(k3,s1,p1) runs as this transposed conv on the folded weight
+# (csrc/upsample.hip; include/rgan.h rgan_nn_fold_weight).
+NN_T = ConvGeom(4, 2, 1, True)
+
+
+def _nn_check(geom):
+    if geom.upsample != 2 or geom.transposed or (geom.k, geom.stride, geom.pad) != (3, 1, 1):
+        raise L.RganError(f"unsupported upsampling conv {geom}: only Upsample(x2)+Conv2d(k3,s1,p1) (--NN_conv)")
 
 
 def empty_nhwc(B, C, H, W, device):
@@ -105,6 +119,60 @@ class _PackCache:
 PACKS = _PackCache()
 
 
+class _FoldCache:
+    """Folded --NN_conv weights (Wt = A W A^T), one per (weight, version): like the packs,
+    refolded only after an optimizer step.  A new Wt tensor is made per version so the
+    pack cache (keyed by the Wt object) never sees a stale layout."""
+
+    def __init__(self):
+        self.entries = {}
+
+    def get(self, w):
+        base = w._base if w._base is not None else w
+        key = id(base)
+        ent = self.entries.get(key)
+        if ent is not None and ent[0]() is base and ent[1] == w._version and ent[2] == w.data_ptr():
+            return ent[3]
+        wt = nn_fold(w)
+        self.entries[key] = (weakref.ref(base, self._drop(key)), w._version, w.data_ptr(), wt)
+        return wt
+
+    def _drop(self, key):
+        def cb(_ref):
+            ent = self.entries.get(key)
+            if ent is not None and ent[0] is _ref:
+                del self.entries[key]
+        return cb
+
+    def clear(self):
+        self.entries.clear()
+
+
+FOLDS = _FoldCache()
+
+
+def nn_fold(w):
+    """Conv2d weight [cout][cin][3][3] -> ConvTranspose2d weight [cin][cout][4][4]."""
+    L.require_cuda(w)
+    _f32(w)
+    cout, cin = w.shape[0], w.shape[1]
+    if tuple(w.shape[2:]) != (3, 3):
+        raise L.RganError(f"nn_fold expects a 3x3 kernel, got {tuple(w.shape)}")
+    wt = torch.empty((cin, cout, 4, 4), dtype=torch.float32, device=w.device)
+    L.check(L.lib().rgan_nn_fold_weight(L.ptr(w.contiguous()), cout, cin, L.ptr(wt), L.stream()),
+            "rgan_nn_fold_weight")
+    return wt
+
+
+def nn_unfold_grad(dwt, w_shape):
+    """Adjoint of nn_fold: dWt [cin][cout][4][4] -> dW [cout][cin][3][3]."""
+    cout, cin = w_shape[0], w_shape[1]
+    dw = torch.empty(w_shape, dtype=torch.float32, device=dwt.device)
+    L.check(L.lib().rgan_nn_unfold_grad(L.ptr(dwt.contiguous()), cout, cin, L.ptr(dw), L.stream()),
+            "rgan_nn_unfold_grad")
+    return dw
+
+
 def conv_fwd(x, w, geom, bias=None, act="none", alpha=0.0, wscale=None, out=None, nchw_out=False, cache=False):
     """y = act(conv(x, w)*wscale + bias); x [B,Cin,H,W] any strides; w torch layout.
 
@@ -112,6 +180,11 @@ def conv_fwd(x, w, geom, bias=None, act="none", alpha=0.0, wscale=None, out=None
     unchanged."""
     L.require_cuda(x, w, bias, wscale)
     _f32(x, w, bias)
+    if geom.upsample != 1:
+        _nn_check(geom)
+        wt = FOLDS.get(w) if cache else nn_fold(w)
+        return conv_fwd(x, wt, NN_T, bias=bias, act=act, alpha=alpha, wscale=wscale, out=out, nchw_out=nchw_out,
+                        cache=cache)
     B, cin, H, W = x.shape
     cout = w.shape[1] if geom.transposed else w.shape[0]
     Ho, Wo = geom.out_hw(H, W)
@@ -135,6 +208,10 @@ def conv_dgrad(dy, w, geom, x_shape, wscale=None, out=None, like=None, cache=Fal
     """dx of the conv (input grad), NHWC unless `like` (a tensor whose strides to copy) is given."""
     L.require_cuda(dy, w, wscale)
     _f32(dy, w)
+    if geom.upsample != 1:
+        _nn_check(geom)
+        wt = FOLDS.get(w) if cache else nn_fold(w)
+        return conv_dgrad(dy, wt, NN_T, x_shape, wscale=wscale, out=out, like=like, cache=cache)
     B, cin, H, W = x_shape
     if out is None:
         if like is not None and not is_nhwc(like):
@@ -157,6 +234,11 @@ def conv_wgrad(x, dy, geom, w_shape, with_bias=False):
     """(dw in torch layout, dbias or None)."""
     L.require_cuda(x, dy)
     _f32(x, dy)
+    if geom.upsample != 1:
+        _nn_check(geom)
+        cout, cin = w_shape[0], w_shape[1]
+        dwt, db = conv_wgrad(x, dy, NN_T, (cin, cout, 4, 4), with_bias=with_bias)
+        return nn_unfold_grad(dwt, tuple(w_shape)), db
     dw = torch.empty(w_shape, dtype=torch.float32, device=x.device)
     db = None
     if with_bias:

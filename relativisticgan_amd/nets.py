@@ -30,7 +30,7 @@ from .kernels import ConvGeom, spectral_power
 class _ConvBase(nn.Module):
     transposed = False
 
-    def __init__(self, cin, cout, k, stride, pad, bias, spectral):
+    def __init__(self, cin, cout, k, stride, pad, bias, spectral, upsample=1):
         super().__init__()
         self.cin, self.cout, self.k, self.stride, self.pad = cin, cout, k, stride, pad
         self.spectral = spectral
@@ -38,13 +38,16 @@ class _ConvBase(nn.Module):
         tmp = ctor(cin, cout, k, stride, pad, bias=bias)  # same RNG draws as the reference
         if spectral:
             tmp = torch.nn.utils.spectral_norm(tmp)       # draws u then v (spectral_norm.py:168-169)
+            # torch's spectral_norm deletes `weight` and registers `weight_orig` AFTER `bias`:
+            # parameter order = optimizer state order (Adam.state_dict is positional)
+            self.bias = nn.Parameter(tmp.bias.detach().clone()) if bias else None
             self.weight_orig = nn.Parameter(tmp.weight_orig.detach().clone())
             self.register_buffer("weight_u", tmp.weight_u.detach().clone())
             self.register_buffer("weight_v", tmp.weight_v.detach().clone())
         else:
             self.weight = nn.Parameter(tmp.weight.detach().clone())
-        self.bias = nn.Parameter(tmp.bias.detach().clone()) if bias else None
-        self.geom = ConvGeom(k, stride, pad, self.transposed)
+            self.bias = nn.Parameter(tmp.bias.detach().clone()) if bias else None
+        self.geom = ConvGeom(k, stride, pad, self.transposed, upsample)
 
     @property
     def w(self):
@@ -58,8 +61,8 @@ class _ConvBase(nn.Module):
 class Conv2d(_ConvBase):
     """Conv2d parameters (torch layout [cout][cin][k][k])."""
 
-    def __init__(self, cin, cout, k, stride=1, pad=0, bias=True, spectral=False):
-        super().__init__(cin, cout, k, stride, pad, bias, spectral)
+    def __init__(self, cin, cout, k, stride=1, pad=0, bias=True, spectral=False, upsample=1):
+        super().__init__(cin, cout, k, stride, pad, bias, spectral, upsample)
 
 
 class ConvTranspose2d(_ConvBase):
@@ -188,8 +191,6 @@ def _lin_spec(layer, geom, act, alpha=0.0, nchw_out=False):
 
 class _Net(nn.Module):
     def _run(self, x):
-        if getattr(self.param, "NN_conv", False) and self.param.arch == 0:
-            raise NotImplementedError("--NN_conv (Upsample+Conv3x3) is not on this build's hot path yet")
         h = x
         for layer in self._plan:
             h = layer.run(h, self.training)
@@ -232,7 +233,7 @@ class _G0(_Net):
             if p.NN_conv:
                 main.add_module("Middle-UpSample [%d]" % i, _Upsample())
                 ccls = SpectralConv2d if sn else Conv2d
-                conv = ccls(cin, cout, 3, 1, 1, bias=True)
+                conv = ccls(cin, cout, 3, 1, 1, bias=True, upsample=2)  # Upsample folded into the conv
                 name = ("Middle-SpectralConv2d [%d]" if sn else "Middle-Conv2d [%d]") % i
             else:
                 conv = cls(cin, cout, 4, 2, 1, bias=False)
@@ -243,7 +244,7 @@ class _G0(_Net):
         if p.NN_conv:
             main.add_module("End-UpSample", _Upsample())
             ccls = SpectralConv2d if sn else Conv2d
-            end = ccls(p.G_h_size, p.n_colors, 3, 1, 1, bias=True)
+            end = ccls(p.G_h_size, p.n_colors, 3, 1, 1, bias=True, upsample=2)
             main.add_module("End-SpectralConv2d" if sn else "End-Conv2d", end)
         else:
             end = cls(p.G_h_size, p.n_colors, 4, 2, 1, bias=False)

@@ -54,6 +54,8 @@ class Adam(torch.optim.Optimizer):
                 if p.grad is None:
                     continue
                 st = self.state[p]
+                if len(st) and st["exp_avg"].shape != p.shape:
+                    raise ValueError(f"Adam state shape {tuple(st['exp_avg'].shape)} != parameter {tuple(p.shape)}")
                 if len(st) == 0:
                     st["step"] = torch.tensor(0.0)
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
@@ -79,3 +81,14 @@ class Adam(torch.optim.Optimizer):
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
         self._dev = {}
+        # torch matches optimizer state to parameters by POSITION and does not check shapes;
+        # the kernel trusts p.numel() for exp_avg/exp_avg_sq, so a mismatch must stop here
+        for group in self.param_groups:
+            for p in group["params"]:
+                st = self.state.get(p)
+                if not st:
+                    continue
+                for k in ("exp_avg", "exp_avg_sq"):
+                    if k in st and tuple(st[k].shape) != tuple(p.shape):
+                        raise ValueError(f"optimizer state '{k}' of shape {tuple(st[k].shape)} does not match its "
+                                         f"parameter {tuple(p.shape)} (parameter order differs from the checkpoint)")

@@ -62,6 +62,9 @@ class Trainer:
         self.optG = Adam(self.G.parameters(), lr=p.lr_G, betas=(p.beta1, p.beta2), weight_decay=p.weight_decay)
         self.decayD = torch.optim.lr_scheduler.ExponentialLR(self.optD, gamma=1 - p.decay)
         self.decayG = torch.optim.lr_scheduler.ExponentialLR(self.optG, gamma=1 - p.decay)
+        # gradient SUM all-reduce overlapped with the last backward of each step (world > 1)
+        self.redD = dp.GradReducer(self.D.parameters()) if self.world > 1 else None
+        self.redG = dp.GradReducer(self.G.parameters()) if self.world > 1 else None
         self.host_rng = getattr(p, "rgan_rng", "host") == "host"
         self.errD = self.errG = None
         self.last = {}
@@ -87,14 +90,21 @@ class Trainer:
             return feed[key]
         if self.host_rng:
             return self._shard(torch.empty(shape).normal_(0, 1)).to(self.device, non_blocking=True)
-        return torch.randn((self.B,) + tuple(shape[1:]), device=self.device)
+        # every rank draws the global batch from the same device generator and keeps its
+        # shard: ranks see different z, and the union is the 1-process draw
+        return self._shard(torch.randn(shape, device=self.device))
 
     def _uniform(self, feed, key, shape):
         if feed is not None and key in feed:
             return feed[key]
         if self.host_rng:
             return self._shard(torch.empty(shape).uniform_(0, 1)).to(self.device, non_blocking=True)
-        return torch.rand((self.B,) + tuple(shape[1:]), device=self.device)
+        return self._shard(torch.rand(shape, device=self.device))
+
+    @staticmethod
+    def _arm(red):
+        if red is not None:
+            red.arm()
 
     def _set_D_grad(self, flag):
         for q in self.D.parameters():
@@ -104,6 +114,7 @@ class Trainer:
     def iteration(self, i, feed=None, hooks=None):
         p, D, G = self.p, self.D, self.G
         kind = p.loss_D
+        gp_on = kind == 3 or p.grad_penalty
         zshape = (p.batch_size, p.z_size, 1, 1)
         if i % p.print_every == 0:
             with torch.no_grad():
@@ -121,6 +132,8 @@ class Trainer:
                     x_fake = G(z)
                 y_pred_fake = D(x_fake)
                 err_fake = loss_D_fake(kind, y_pred_fake)
+                if not gp_on:
+                    self._arm(self.redD)
                 err_fake.backward()
                 errD = err_real.detach() + err_fake.detach()
             else:
@@ -129,15 +142,19 @@ class Trainer:
                     x_fake = G(z)
                 y_pred_fake = D(x_fake)
                 errD = loss_D(kind, y_pred, y_pred_fake)
+                if not gp_on:
+                    self._arm(self.redD)
                 errD.backward()
             rec = {"x": x, "z": z, "y_pred": y_pred.detach(), "y_pred_fake": y_pred_fake.detach(),
                    "errD": errD.detach()}
-            if kind == 3 or p.grad_penalty:
+            if gp_on:
                 u = self._uniform(feed, "u", (p.batch_size, 1, 1, 1))
                 gp = gradient_penalty(D, x, x_fake, u, p.penalty)
+                self._arm(self.redD)
                 gp.backward()
                 rec.update(u=u, gp=gp.detach())
-            dp.allreduce_grads(list(D.parameters()))
+            if self.redD is not None:
+                self.redD.finish()
             if hooks:
                 hooks("D", rec)
             self.optD.step()
@@ -159,9 +176,11 @@ class Trainer:
                     y_pred = D(x)
                 recG.update(x=x, y_pred=y_pred)
             errG = loss_G(kind, y_pred_fake, y_pred)
+            self._arm(self.redG)
             errG.backward()
             recG.update(y_pred_fake=y_pred_fake.detach(), errG=errG.detach())
-            dp.allreduce_grads(list(G.parameters()))
+            if self.redG is not None:
+                self.redG.finish()
             if hooks:
                 hooks("G", recG)
             self.optG.step()

@@ -40,6 +40,8 @@ CONFIGS = {
     "ralsgan_tanh": _cfg(loss_D=7, Tanh_GD="True"),
     "ralsgan_selu": _cfg(loss_D=7, SELU="True"),
     "ralsgan_wd": _cfg(loss_D=7, weight_decay=0.01, decay=0.1),
+    "ralsgan_nnconv": _cfg(loss_D=7, NN_conv="True"),
+    "rasgan_nnconv_spectralG": _cfg(loss_D=6, NN_conv="True", spectral_G="True"),
     "wgangp_arch1": {"args": {"image_size": 32, "batch_size": 8, "z_size": 16, "loss_D": 3,
                               "arch": 1, "n_iter": 2}, "seed": 1, "n_images": 64},
     "rahinge_arch1": {"args": {"image_size": 32, "batch_size": 8, "z_size": 16, "loss_D": 8,

@@ -97,6 +97,41 @@ def test_nets_state_dict_and_init_match_reference(name):
                 assert sha == bytes(g[full + "@sha1"]).decode(), k
 
 
+ORDER_CASES = list(CONFIGS) + ["arch1_spectral"]
+
+
+@pytest.mark.parametrize("name", ORDER_CASES)
+def test_parameter_and_state_dict_order_match_reference(name):
+    """Parameter order == the reference's (torch optimizers load state by POSITION:
+    spectral_norm registers weight_orig after bias), and state_dict key order too."""
+    from oracle.reference_cpu import build_D, build_G
+    from oracle.reference_cpu import make_param as oracle_param
+    from relativisticgan_amd.config import make_param
+    from relativisticgan_amd.nets import DCGAN_D, DCGAN_G
+    if name == "arch1_spectral":
+        kw = dict(arch=1, image_size=32, batch_size=8, z_size=16, loss_D=8, spectral=True, spectral_G=True)
+    else:
+        kw = {k: v for k, v in vars(param_for(name)).items() if not k.startswith("rgan_")}
+    ours, ref = make_param(**kw), oracle_param(**{k: v for k, v in kw.items() if k != "cuda"})
+    for mine, theirs in ((DCGAN_G(ours), build_G(ref)), (DCGAN_D(ours), build_D(ref))):
+        assert [n for n, _ in mine.named_parameters()] == [n for n, _ in theirs.named_parameters()]
+        assert list(mine.state_dict()) == list(theirs.state_dict())
+        for (n, a), (_, b) in zip(mine.named_parameters(), theirs.named_parameters()):
+            assert a.shape == b.shape, n
+
+
+def test_adam_rejects_mismatched_state():
+    from relativisticgan_amd.optim import Adam
+    a, b = torch.nn.Parameter(torch.zeros(3)), torch.nn.Parameter(torch.zeros(2, 5))
+    src = torch.optim.Adam([b, a])  # reversed order
+    for q in (a, b):
+        q.grad = torch.ones_like(q)
+    src.step()
+    opt = Adam([a, b])
+    with pytest.raises(ValueError):
+        opt.load_state_dict(src.state_dict())
+
+
 def test_product_refuses_cpu_tensors():
     from relativisticgan_amd import kernels as K
     from relativisticgan_amd._lib import RganError

@@ -136,3 +136,69 @@ def test_dp_collectives_and_protocol_gloo_world2():
         pr.join(120)
     res = [q.get() for _ in range(world)]
     assert all(msg == "ok" for _, msg in res), res
+
+
+def _make_params(seed=3):
+    torch.manual_seed(seed)
+    shapes = [(16, 6), (16,), (8, 16), (8,), (1, 8), (1,), (5,)]
+    return [torch.nn.Parameter(torch.randn(sh) * 0.5) for sh in shapes]
+
+
+def _losses(params, rank):
+    """Two losses of rank ``rank``; the last parameter gets a gradient from loss 1 only."""
+    w1, b1, w2, b2, w3, b3, extra = params
+    g = torch.Generator().manual_seed(100 + rank)
+    x1, x2 = torch.randn(4, 6, generator=g), torch.randn(4, 6, generator=g)
+
+    def f(x):
+        h = torch.tanh(x @ w1.t() + b1)
+        h = torch.tanh(h @ w2.t() + b2)
+        return h @ w3.t() + b3
+    return f(x1).pow(2).mean() + (extra * (rank + 1)).sum(), f(x2).sin().mean()
+
+
+def _reducer_worker(rank, world, port, q):
+    try:
+        dp = _init(rank, world, port)
+        params = _make_params()
+        red = dp.GradReducer(params, bucket_bytes=60)  # several buckets
+        assert len(red.buckets) > 2
+        ref = _make_params()
+        want = [torch.zeros_like(prm) for prm in params]
+        for rk in range(world):
+            l1, l2 = _losses(ref, rk)
+            for w_, g_ in zip(want, torch.autograd.grad(l1 + l2, ref)):
+                w_ += g_
+        for step in range(2):  # the reducer re-arms cleanly on the next step
+            for prm in params:
+                prm.grad = None
+            l1, l2 = _losses(params, rank)
+            l1.backward()  # first backward: not armed
+            red.arm()
+            l2.backward()  # last backward: buckets launch from the hooks
+            red.finish()
+            for prm, w_ in zip(params, want):
+                assert torch.allclose(prm.grad, w_, atol=1e-6), (step, prm.shape)
+        q.put((rank, "ok"))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_overlapped_grad_reducer_gloo_world2():
+    """dp.GradReducer: buckets launched from post-accumulate hooks during the last
+    backward (own communicator), grads from earlier backwards included, == global SUM."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_reducer_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(120)
+    res = [q.get() for _ in range(world)]
+    assert all(msg == "ok" for _, msg in res), res

@@ -81,6 +81,39 @@ def test_conv_fwd_dgrad_wgrad_small(K, case, layout):
     assert _rel(dw, w64.grad) < 2e-6
 
 
+@pytest.mark.parametrize("case", [(2, 16, 8, 4), (3, 8, 3, 8), (2, 32, 64, 8), (2, 5, 7, 6), (2, 64, 32, 16)])
+@pytest.mark.parametrize("cached", [False, True])
+def test_nn_conv_upsample_fold(K, case, cached):
+    """--NN_conv: Upsample(x2)+Conv2d(k3,s1,p1)+bias (GLI:351-356,377-382) as one folded
+    k4 s2 p1 transposed conv; fwd/dgrad/wgrad/dbias vs torch fp64 interpolate+conv2d."""
+    B, cin, cout, H = case
+    g = K.ConvGeom(3, 1, 1, False, 2)
+    torch.manual_seed(1)
+    x = _nhwc(torch.randn(B, cin, H, H, device=DEV))
+    w = (torch.randn(cout, cin, 3, 3, device=DEV) * 0.1).requires_grad_(False)
+    b = torch.randn(cout, device=DEV)
+    x64 = x.double().cpu().requires_grad_(True)
+    w64 = w.double().cpu().requires_grad_(True)
+    b64 = b.double().cpu().requires_grad_(True)
+    ref = F.conv2d(F.interpolate(x64, scale_factor=2, mode="nearest"), w64, b64, padding=1)
+    y = K.conv_fwd(x, w, g, bias=b, cache=cached)
+    assert y.shape == ref.shape
+    assert _rel(y, ref.detach()) < 3e-6
+    dy = _nhwc(torch.randn(ref.shape, device=DEV))
+    ref.backward(dy.double().cpu())
+    dx = K.conv_dgrad(dy, w, g, tuple(x.shape), cache=cached)
+    assert _rel(dx, x64.grad) < 3e-6
+    dw, db = K.conv_wgrad(x, dy, g, tuple(w.shape), with_bias=True)
+    assert dw.shape == w.shape
+    assert _rel(dw, w64.grad) < 3e-6
+    assert _rel(db, b64.grad) < 1e-6
+    if cached:  # second call reuses the folded weight; an in-place update must refold
+        w.mul_(0.5)
+        y2 = K.conv_fwd(x, w, g, bias=b, cache=True)
+        ref2 = F.conv2d(F.interpolate(x.double().cpu(), scale_factor=2), w.double().cpu(), b.double().cpu(), padding=1)
+        assert _rel(y2, ref2) < 3e-6
+
+
 def test_conv_bias_act(K):
     g = K.ConvGeom(3, 1, 1, False)
     x = _nhwc(torch.randn(2, 12, 8, 8, device=DEV))
