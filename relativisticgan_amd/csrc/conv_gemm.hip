@@ -119,10 +119,24 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert(TM >= 1 && TN >= 1 && WM * WN == 4, "tile config");
   constexpr bool AK = (MODE == MODE_WGRAD);          // A staged k-major
-  constexpr int A_LD = AK ? (BM + 4) : (BK + 1);
-  constexpr int A_SZ = AK ? BK * (BM + 4) : BM * (BK + 1);
-  constexpr int B_LD = BN + 4;
-  constexpr int B_SZ = BK * B_LD;
+  // KROW (every FAST path): both operands staged as k-contiguous rows ([m][k], [n][k]);
+  // every lane reads 4 consecutive k of its row with one conflict-free ds_read_b128 that
+  // feeds 4 MFMA steps.  The k order inside a BK tile is permuted (MFMA step s of lane
+  // half h takes k = 16h + s), the same for A and B, so only the fp32 summation order
+  // changes.  CONV/CONVT2: the global rows are k-contiguous too (channels; [N][K] weight
+  // pack), stores are ds_write_b128 and the row stride is 36 dwords (9 slots: 16 rows hit
+  // 16 slots).  WGRAD (SWZ): k = pixel is the global outer index, so each float4 (4
+  // consecutive m or n of one pixel) is stored transposed as 4 ds_write_b32 into rows of
+  // 32 dwords whose 16-B quads are XOR-swizzled by (row >> 1) & 7: the reads stay
+  // conflict-free (slot = 8 (row & 1) + quad ^ swz) and each store instruction (8 channel
+  // quads x 4 pixels per half-wave) is at most 2-way (free for ds_write_b32).
+  constexpr bool KROW = FAST;
+  constexpr bool SWZ = FAST && MODE == MODE_WGRAD;
+  constexpr int KROW_LD = SWZ ? BK : BK + 4;
+  constexpr int A_LD = KROW ? KROW_LD : AK ? (BM + 4) : (BK + 1);
+  constexpr int A_SZ = KROW ? BM * KROW_LD : AK ? BK * (BM + 4) : BM * (BK + 1);
+  constexpr int B_LD = KROW ? KROW_LD : BN + 4;
+  constexpr int B_SZ = KROW ? BN * KROW_LD : BK * B_LD;
   constexpr int STAGE = A_SZ + B_SZ;
   __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
 
@@ -188,9 +202,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
 
   // ---------------- FAST-path state ----------------
   static_assert(!FAST || (AV && BV), "FAST needs vector operands");
-  constexpr int FA_TPR = (MODE == MODE_WGRAD) ? BM / 4 : BK / 4;   // threads per A row
-  constexpr int FA_N = (MODE == MODE_WGRAD) ? BK / (256 / FA_TPR) : AR;  // A loads per thread
-  constexpr int FB_TPR = BN / 4, FB_RPP = 256 / FB_TPR, FB_N = BK / FB_RPP;
+  // WGRAD FAST thread map (per operand of R rows = BM or BN): tid -> quad q = (tid&7) +
+  // 8 ((tid>>5) % (R/32)), pixels p = ((tid>>3)&3) + 4 ((tid>>5) / (R/32)) + (32/(R/32)) i
+  constexpr int FA_N = (MODE == MODE_WGRAD) ? BM / 32 : AR;  // A loads per thread
+  constexpr int FB_N = BN / 32;
+  auto sw_q = [&](int R) { return (tid & 7) + 8 * ((tid >> 5) % (R / 32)); };
+  auto sw_p = [&](int R, int i) { return ((tid >> 3) & 3) + 4 * ((tid >> 5) / (R / 32)) + (32 / (R / 32)) * i; };
   __shared__ int ptab[2][BK];   // WGRAD FAST: im2col pixel offsets of the next tiles
   __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g.a.p, (short)0, g.a_bytes, 0x00020000);
   __amdgpu_buffer_rsrc_t brsrc =
@@ -200,17 +217,19 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
   int f_tap = 0, f_c0 = 0, f_cin = 1, w_tab = 0;
   if constexpr (FAST) {
     if constexpr (MODE != MODE_WGRAD) {
-      const int n = n0 + 4 * (tid % FB_TPR), r = tid / FB_TPR;
+      // packed weights [N][K]: rows n = n0 + (tid>>3) + 32i, k quad tid&7 (like A)
 #pragma unroll
-      for (int i = 0; i < FB_N; ++i) boff[i] = n < g.N ? ((r + FB_RPP * i) * g.N + n) * 4 : OOB;
+      for (int i = 0; i < FB_N; ++i) {
+        const int n = n0 + (tid >> 3) + 32 * i;
+        boff[i] = n < g.N ? (n * g.K + 4 * (tid & 7)) * 4 : OOB;
+      }
       f_cin = g.fC.d;
       f_tap = kbeg / f_cin;
       f_c0 = kbeg - f_tap * f_cin;
     } else {
-      const int m = m0 + 4 * (tid % FA_TPR), r = tid / FA_TPR;
-      constexpr int RPP = 256 / FA_TPR;
+      const int m = m0 + 4 * sw_q(BM);
 #pragma unroll
-      for (int i = 0; i < FA_N; ++i) aoff[i] = m < g.M ? ((r + RPP * i) * (int)g.a.sw + m) * 4 : OOB;
+      for (int i = 0; i < FA_N; ++i) aoff[i] = m < g.M ? (sw_p(BM, i) * (int)g.a.sw + m) * 4 : OOB;
       // the block's n tile lies in one tap: n0 -> (kh, kw, ci0), wave-uniform
       const uint32_t t = g.fC.div(n0);
       const int ci0 = n0 - t * g.fC.d;
@@ -273,7 +292,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
         ra[4 * i + 2] = __uint_as_float(v.z); ra[4 * i + 3] = __uint_as_float(v.w);
       }
       f_c0 += BK;
-      const int so = k0 * g.N * 4;
+      const int so = k0 * 4;
 #pragma unroll
       for (int i = 0; i < FB_N; ++i) {
         const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(brsrc, boff[i], so, 0);
@@ -288,10 +307,10 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
         ra[4 * i + 0] = __uint_as_float(v.x); ra[4 * i + 1] = __uint_as_float(v.y);
         ra[4 * i + 2] = __uint_as_float(v.z); ra[4 * i + 3] = __uint_as_float(v.w);
       }
-      const int qb = (tid % FB_TPR) * 16, r = tid / FB_TPR;
+      const int qb = sw_q(BN) * 16;
 #pragma unroll
       for (int i = 0; i < FB_N; ++i) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(brsrc, ptab[slot][r + FB_RPP * i] + qb, 0, 0);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(brsrc, ptab[slot][sw_p(BN, i)] + qb, 0, 0);
         rb[4 * i + 0] = __uint_as_float(v.x); rb[4 * i + 1] = __uint_as_float(v.y);
         rb[4 * i + 2] = __uint_as_float(v.z); rb[4 * i + 3] = __uint_as_float(v.w);
       }
@@ -399,25 +418,13 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
     }
     // ---------------- B ----------------
     if constexpr (MODE != MODE_WGRAD) {
-      if constexpr (BV) {
-        constexpr int TPR = BN / 4, RPP = 256 / TPR, PASSES = BK / RPP;
-        const int q = tid % TPR, r = tid / TPR;
-        const int n = n0 + 4 * q;
+      // packed weights [N][K]: k fastest across threads (coalesced), staged [k][n]
 #pragma unroll
-        for (int i = 0; i < PASSES; ++i) {
-          int k = k0 + r + RPP * i;
-          float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (k < kend && n < g.N) v = *reinterpret_cast<const float4*>(Bw + (size_t)k * g.N + n);
-          rb[4 * i + 0] = v.x; rb[4 * i + 1] = v.y; rb[4 * i + 2] = v.z; rb[4 * i + 3] = v.w;
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < B_ELEMS; ++j) {
-          int e = tid + 256 * j;
-          int row = e / BN, col = e - (e / BN) * BN;
-          int k = k0 + row, n = n0 + col;
-          rb[j] = (k < kend && n < g.N) ? Bw[(size_t)k * g.N + n] : 0.f;
-        }
+      for (int j = 0; j < B_ELEMS; ++j) {
+        int e = tid + 256 * j;
+        int row = e / BK, col = e - row * BK;
+        int k = k0 + col, n = n0 + row;
+        rb[j] = (k < kend && n < g.N) ? Bw[(size_t)n * g.K + k] : 0.f;
       }
     } else {
       // WGRAD B: im2col(img)[p][n]
@@ -472,6 +479,35 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
   auto store_tiles = [&](int buf) {
     float* As = smem + buf * STAGE;
     float* Bs = As + A_SZ;
+    if constexpr (SWZ) {
+      // element (row, k) at row * 32 + 4 ((k >> 2) ^ ((row >> 1) & 7)) + (k & 3)
+      auto put = [&](float* T, int R, const float* v, int nld) {
+        const int q = sw_q(R);
+#pragma unroll
+        for (int i = 0; i < nld; ++i) {
+          const int k = sw_p(R, i);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int row = 4 * q + j;
+            T[row * KROW_LD + 4 * ((k >> 2) ^ ((row >> 1) & 7)) + (k & 3)] = v[4 * i + j];
+          }
+        }
+      };
+      put(As, BM, ra, FA_N);
+      put(Bs, BN, rb, FB_N);
+      return;
+    } else if constexpr (KROW) {
+      const int q = tid & 7;
+#pragma unroll
+      for (int i = 0; i < AR; ++i)
+        *reinterpret_cast<float4*>(As + ((tid >> 3) + 32 * i) * KROW_LD + 4 * q) =
+            make_float4(ra[4 * i], ra[4 * i + 1], ra[4 * i + 2], ra[4 * i + 3]);
+#pragma unroll
+      for (int i = 0; i < FB_N; ++i)
+        *reinterpret_cast<float4*>(Bs + ((tid >> 3) + 32 * i) * KROW_LD + 4 * q) =
+            make_float4(rb[4 * i], rb[4 * i + 1], rb[4 * i + 2], rb[4 * i + 3]);
+      return;
+    }
     if constexpr (MODE != MODE_WGRAD) {
       if constexpr (AV) {
         const int q = tid & 7;
@@ -504,7 +540,14 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
         }
       }
     }
-    if constexpr (BV) {
+    if constexpr (MODE != MODE_WGRAD) {  // [N][K] weights, k fastest (load_tiles)
+#pragma unroll
+      for (int j = 0; j < B_ELEMS; ++j) {
+        int e = tid + 256 * j;
+        int row = e / BK;
+        Bs[(e - row * BK) * B_LD + row] = rb[j];
+      }
+    } else if constexpr (BV) {
       constexpr int TPR = BN / 4, RPP = 256 / TPR, PASSES = BK / RPP;
       const int q = tid % TPR, r = tid / TPR;
 #pragma unroll
@@ -553,6 +596,29 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
     }
     const float* As = smem + cur * STAGE;
     const float* Bs = As + A_SZ;
+    if constexpr (KROW) {
+      // logical quad g = kq + 4 lk of row wm/wn + 32 t + l32; SWZ: physical quad g ^ swz
+      // with swz = (l32 >> 1) & 7 (wm, wn, 32 t are multiples of 32)
+      const int swz = SWZ ? (l32 >> 1) & 7 : 0;
+      const float* Ar = As + (wm + l32) * KROW_LD;
+      const float* Br = Bs + (wn + l32) * KROW_LD;
+#pragma unroll
+      for (int kq = 0; kq < BK / 8; ++kq) {
+        const int qo = 4 * ((kq + 4 * lk) ^ swz);
+        float4 a4[TM], b4[TN];
+#pragma unroll
+        for (int t = 0; t < TM; ++t) a4[t] = *reinterpret_cast<const float4*>(Ar + 32 * t * KROW_LD + qo);
+#pragma unroll
+        for (int t = 0; t < TN; ++t) b4[t] = *reinterpret_cast<const float4*>(Br + 32 * t * KROW_LD + qo);
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[i][s4], b4[j][s4], acc[i][j], 0, 0, 0);
+      }
+    } else {
 #if RGAN_GEMM_FRAGALL
     // all of the tile's MFMA operands to registers first: the LDS reads are in flight
     // together and the MFMA chain waits on them progressively
@@ -616,6 +682,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
 #endif
+    }
     if (kt + 1 < nk) store_tiles(cur ^ 1);
     __syncthreads();
   }
@@ -696,16 +763,17 @@ struct PackArgs {
   int KH, KW, flip, convt2;
 };
 
-// out[phase][k][n]: one block row per k (k-decomposition uniform per block), threads over n
+// out[phase][n][k] (k contiguous: the GEMM B operand's rows): threads over k, one block
+// column per n (n-decomposition uniform per block)
 __global__ __launch_bounds__(256) void pack_weights(PackArgs a) {
   const int phase = blockIdx.z;
-  const int n = blockIdx.x * 256 + threadIdx.x;
-  if (n >= a.N) return;
-  uint32_t tn = a.fnco.div(n);
-  const int co = n - tn * a.fnco.d;
-  uint32_t nh = a.fnkw.div(tn);
-  const int nw = tn - nh * a.fnkw.d;
-  for (int k = blockIdx.y; k < a.K; k += gridDim.y) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= a.K) return;
+  for (int n = blockIdx.y; n < a.N; n += gridDim.y) {
+    uint32_t tn = a.fnco.div(n);
+    const int co = n - tn * a.fnco.d;
+    uint32_t nh = a.fnkw.div(tn);
+    const int nw = tn - nh * a.fnkw.d;
     uint32_t t = a.fpci.div(k);
     const int ci = k - t * a.fpci.d;
     int kh, kw, c_out;
@@ -723,7 +791,7 @@ __global__ __launch_bounds__(256) void pack_weights(PackArgs a) {
         kw = a.KW - 1 - kw;
       }
     }
-    a.out[((size_t)phase * a.K + k) * a.N + n] =
+    a.out[((size_t)phase * a.N + n) * a.K + k] =
         a.W[ci * a.s_in + c_out * a.s_out + kh * a.s_kh + kw * a.s_kw];
   }
 }
@@ -902,7 +970,8 @@ __global__ void pack_narrow(const float* __restrict__ W, float* __restrict__ out
 // Tiled pack for the layouts whose columns are one weight index (n = out_idx) and whose
 // rows are (tap, in_idx) with in_idx fastest -- every pack on the FAST paths: a block
 // moves a 16 in x 16 out x (<= 16 taps) brick through LDS, reading W in its own
-// contiguous order (taps, then the smaller-stride index) and writing 16-column rows.
+// contiguous order (taps, then the smaller-stride index) and writing 16-float k runs of
+// the [N][K] image.
 __global__ __launch_bounds__(256) void pack_tiled(PackArgs a) {
   __shared__ float t[16][16][17];  // [in][out][tap]
   const int KK = a.KH * a.KW;
@@ -920,7 +989,7 @@ __global__ __launch_bounds__(256) void pack_tiled(PackArgs a) {
   __syncthreads();
   const int K = a.K;
   for (int e = threadIdx.x; e < 16 * 16 * 16; e += 256) {
-    const int o = e & 15, i = (e >> 4) & 15, tap = e >> 8;
+    const int i = e & 15, o = (e >> 4) & 15, tap = e >> 8;
     if (tap >= KK || i0 + i >= Nin || o0 + o >= Nout) continue;
     const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
     int phase = 0, kt;
@@ -930,7 +999,7 @@ __global__ __launch_bounds__(256) void pack_tiled(PackArgs a) {
     } else {
       kt = a.flip ? (a.KH - 1 - kh) * a.KW + (a.KW - 1 - kw) : tap;
     }
-    a.out[((size_t)phase * K + (size_t)kt * Nin + i0 + i) * Nout + o0 + o] = t[i][o][tap];
+    a.out[((size_t)phase * Nout + o0 + o) * K + (size_t)kt * Nin + i0 + i] = t[i][o][tap];
   }
 }
 
@@ -1286,8 +1355,8 @@ static void launch_pack(const PackArgs& a, hipStream_t s) {
     pack_tiled<<<dim3(ceil_div((int)a.fpci.d, 16), ceil_div(a.N, 16)), 256, 0, s>>>(a);
     return;
   }
-  const int ky = std::min(a.K, 8192);
-  pack_weights<<<dim3(ceil_div(a.N, 256), ky, a.phases), 256, 0, s>>>(a);
+  const int ny = std::min(a.N, 8192);
+  pack_weights<<<dim3(ceil_div(a.K, 256), ny, a.phases), 256, 0, s>>>(a);
 }
 
 template <int MODE, int BM, int BN, int WM, int WN>
