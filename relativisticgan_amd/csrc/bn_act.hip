@@ -130,37 +130,59 @@ __global__ __launch_bounds__(256) void bn_moments_partial(const float* __restric
   }
 }
 
-// [k][2][C] partial sums -> sums[2][C]; block = 64 channels x 16 lanes, fixed order
-__global__ __launch_bounds__(1024) void bn_sums_merge(const double* __restrict__ part, int chunks, int C,
-                                                      double* __restrict__ sums) {
-  __shared__ double sh[2][16][64];
-  const int lane = threadIdx.x & 63, ml = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+// [k][2][C] partial sums -> per-channel totals in a fixed order (deterministic).  Block =
+// 16 channels x 64 chunk lanes (1024 threads): each lane sums chunks r, r+64, ... and the
+// 64 lane totals are added in lane order -- 8x the channel-parallelism of a 64-channel
+// block, so the merge of C = 128 channels x 1024 chunks runs on 8 CUs, not 2.
+//   FIN 0: sums[2][C] (backward: sum g, sum g*(y-mean))
+//   FIN 1: moments [3][C] (count, mean, M2) of this rank (SyncBN stage 1)
+//   FIN 2: one rank: (mean, invstd) stats + running-stat update, as bn_finalize_kernel
+constexpr int MERGE_CPB = 16, MERGE_ROWS = 64;
+
+template <int FIN>
+__global__ __launch_bounds__(1024) void bn_merge(const double* __restrict__ part, int chunks, int C,
+                                                 double* __restrict__ out, const float* __restrict__ y, long long P,
+                                                 long long sc, float eps, float momentum, float* running_mean,
+                                                 float* running_var, long long* nbt, float* stats) {
+  __shared__ double sh[2][MERGE_ROWS][MERGE_CPB];
+  const int cl = threadIdx.x % MERGE_CPB, r = threadIdx.x / MERGE_CPB;
+  const int c = blockIdx.x * MERGE_CPB + cl;
   double a1 = 0.0, a2 = 0.0;
   if (c < C)
-    for (int k = ml; k < chunks; k += 16) {
+    for (int k = r; k < chunks; k += MERGE_ROWS) {
       a1 += part[((size_t)k * 2 + 0) * C + c];
       a2 += part[((size_t)k * 2 + 1) * C + c];
     }
-  sh[0][ml][lane] = a1; sh[1][ml][lane] = a2;
+  sh[0][r][cl] = a1;
+  sh[1][r][cl] = a2;
   __syncthreads();
-  if (ml == 0 && c < C) {
-    double t1 = 0.0, t2 = 0.0;
-    for (int r = 0; r < 16; ++r) { t1 += sh[0][r][lane]; t2 += sh[1][r][lane]; }
-    sums[c] = t1;
-    sums[C + c] = t2;
+  if constexpr (FIN == 2) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
   }
-}
-
-// shifted sums -> moments (count, mean, M2)
-__global__ void bn_sums_to_moments(const double* __restrict__ sums, const float* __restrict__ y, long long P,
-                                   int C, long long sc, double* __restrict__ mom) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const double n = (double)P, s1 = sums[c], s2 = sums[C + c];
-  mom[c] = n;
-  mom[C + c] = (double)y[(long long)c * sc] + s1 / n;
-  mom[2 * C + c] = fmax(s2 - s1 * s1 / n, 0.0);
+  if (r != 0 || c >= C) return;
+  double s1 = 0.0, s2 = 0.0;
+  for (int q = 0; q < MERGE_ROWS; ++q) { s1 += sh[0][q][cl]; s2 += sh[1][q][cl]; }
+  if constexpr (FIN == 0) {
+    out[c] = s1;
+    out[C + c] = s2;
+  } else {
+    // shifted sums (shift = y[0][c]) -> moments
+    const double n = (double)P, mean = (double)y[(long long)c * sc] + s1 / n, m2 = fmax(s2 - s1 * s1 / n, 0.0);
+    if constexpr (FIN == 1) {
+      out[c] = n;
+      out[C + c] = mean;
+      out[2 * C + c] = m2;
+    } else {
+      const double var = m2 / n;
+      stats[c] = (float)mean;
+      stats[C + c] = (float)(1.0 / sqrt(var + (double)eps));
+      if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+      if (running_var) {
+        const float unb = n > 1.0 ? (float)(m2 / (n - 1.0)) : (float)var;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+      }
+    }
+  }
 }
 
 // merge `nranks` moment blocks [r][3][C] in rank order -> (mean, invstd) float, running stats
@@ -183,23 +205,33 @@ __global__ void bn_finalize_kernel(const double* __restrict__ mom, int nranks, i
   }
 }
 
-extern "C" int rgan_bn_moments(const float* y, long long P, int C, long long sp, long long sc, double* moments,
-                               void* partial, void* stream) {
-  RGAN_REQUIRE(y && moments && partial && P > 0 && C > 0);
-  hipStream_t s = (hipStream_t)stream;
+// partial pass + fused merge (FIN 1: moments into `moments`; FIN 2: stats + running stats)
+static int bn_forward_stats(const float* y, long long P, int C, long long sp, long long sc, int fin,
+                            double* moments, float eps, float momentum, float* running_mean, float* running_var,
+                            long long* nbt, float* stats, void* partial, hipStream_t s) {
   BnGeo g = bn_geo(P, C, sp, sc);
   if (g.vec && ((uintptr_t)y & 15)) g = bn_geo(P, C, 1, 2);
   double* part = (double*)partial;
-  double* sums = part + (size_t)g.chunks * 2 * C;
   dim3 grid(g.chunks, g.cgroups);
   if (g.vec) bn_moments_partial<4><<<grid, 256, 0, s>>>(y, P, C, sp, sc, g.tpr, g.rows, part);
   else bn_moments_partial<1><<<grid, 256, 0, s>>>(y, P, C, sp, sc, g.tpr, g.rows, part);
   RGAN_CHECK_LAUNCH();
-  bn_sums_merge<<<ceil_div(C, 64), 1024, 0, s>>>(part, g.chunks, C, sums);
-  RGAN_CHECK_LAUNCH();
-  bn_sums_to_moments<<<ceil_div(C, 256), 256, 0, s>>>(sums, y, P, C, sc, moments);
+  const int blocks = ceil_div(C, MERGE_CPB);
+  if (fin == 1)
+    bn_merge<1><<<blocks, 1024, 0, s>>>(part, g.chunks, C, moments, y, P, sc, 0.f, 0.f, nullptr, nullptr, nullptr,
+                                        nullptr);
+  else
+    bn_merge<2><<<blocks, 1024, 0, s>>>(part, g.chunks, C, nullptr, y, P, sc, eps, momentum, running_mean,
+                                        running_var, nbt, stats);
   RGAN_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int rgan_bn_moments(const float* y, long long P, int C, long long sp, long long sc, double* moments,
+                               void* partial, void* stream) {
+  RGAN_REQUIRE(y && moments && partial && P > 0 && C > 0);
+  return bn_forward_stats(y, P, C, sp, sc, 1, moments, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr, partial,
+                          (hipStream_t)stream);
 }
 
 extern "C" int rgan_bn_finalize(const double* moments, int nranks, int C, float eps, float momentum,
@@ -217,11 +249,8 @@ extern "C" int rgan_bn_stats(const float* y, long long P, int C, long long sp, l
                              float momentum, float* running_mean, float* running_var,
                              long long* num_batches_tracked, float* stats, void* partial, void* stream) {
   RGAN_REQUIRE(y && stats && partial && P > 0 && C > 0);
-  double* mom = (double*)partial + ((size_t)max_chunks(P, C) * 2 + 2) * C;
-  int rc = rgan_bn_moments(y, P, C, sp, sc, mom, partial, stream);
-  if (rc) return rc;
-  return rgan_bn_finalize(mom, 1, C, eps, momentum, running_mean, running_var, num_batches_tracked, stats,
-                          stream);
+  return bn_forward_stats(y, P, C, sp, sc, 2, nullptr, eps, momentum, running_mean, running_var,
+                          num_batches_tracked, stats, partial, (hipStream_t)stream);
 }
 
 // ------------------------------------------------------------------ apply
@@ -401,7 +430,8 @@ extern "C" int rgan_bn_backward_sums(const float* da, long long dsp, long long d
     bn_bwd_partial<1><<<grid, 256, 0, s>>>(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act, act_alpha,
                                            g.tpr, g.rows, part);
   RGAN_CHECK_LAUNCH();
-  bn_sums_merge<<<ceil_div(C, 64), 1024, 0, s>>>(part, g.chunks, C, sums);
+  bn_merge<0><<<ceil_div(C, MERGE_CPB), 1024, 0, s>>>(part, g.chunks, C, sums, nullptr, 0, 0, 0.f, 0.f, nullptr,
+                                                       nullptr, nullptr, nullptr);
   RGAN_CHECK_LAUNCH();
   return 0;
 }
