@@ -50,8 +50,8 @@ typedef struct RganConv {
  * `prepacked` != 0: the caller passes packed weights (no packing scratch).  0 = unsupported. */
 size_t rgan_conv_workspace(const RganConv* d, int which, int prepacked);
 
-/* Kernel-ready weight layout for which = 0 (fwd) or 1 (dgrad): [phases][K][N] floats for
- * the implicit GEMMs, [Cin][4][4][Cout] for the narrow (<= 4 output channel) transposed
+/* Kernel-ready weight layout for which = 0 (fwd) or 1 (dgrad): [phases][N][K] floats for
+ * the implicit GEMMs (k contiguous: the B operand's LDS rows), [Cin][4][4][Cout] for the narrow (<= 4 output channel) transposed
  * conv.  Packing is separated so callers can cache it per weight version (weights change
  * only at the optimizer step, but each net is run 2-4 times per iteration).
  * rgan_conv_pack_floats returns 0 when the op reads the torch layout directly (narrow
@@ -89,6 +89,20 @@ int rgan_conv_wgrad(const RganConv* d, const float* x, const float* dy, float* d
  * (the Conv2d weight gradient, aten convolution_backward grad_weight). */
 int rgan_nn_fold_weight(const float* w, int cout, int cin, float* wt, void* stream);
 int rgan_nn_unfold_grad(const float* dwt, int cout, int cin, float* dw, void* stream);
+
+/* ---- image export (GLI:563-565 sample grid, GLI:759-768 extra FID images) ----
+ * torchvision.utils.save_image's float -> uint8 step on the device: t = x*scale + shift;
+ * optional normalize with range = device float[2] {min, max} of the batch
+ * (make_grid(normalize=True): t = (clamp(t, lo, hi) - lo) / max(hi - lo, 1e-5)); then
+ * u8 = trunc(clamp(t*255 + 0.5, 0, 255)).  x: [B][C][H][W] with element strides
+ * strides[4]; grid = 0: out [B][H][W][C] (one image per file, padding 0);
+ * grid = 1: make_grid layout [Hg][Wg][C], nrow tiles per row, `padding` pixels of 0.
+ * rgan_minmax: out2 = {min, max} of x[0..n) (ws: rgan_minmax_ws_bytes). */
+size_t rgan_minmax_ws_bytes(long long n);
+int rgan_minmax(const float* x, long long n, float* out2, void* ws, void* stream);
+int rgan_images_to_u8(const float* x, int B, int C, int H, int W, const long long* strides,
+                      float scale, float shift, const float* range, int grid, int nrow, int padding,
+                      unsigned char* out, void* stream);
 
 /* ---- BatchNorm2d, train mode (GLI:341,366,433; arch 1 GLI:204-218,262-297) ----
  * Tensors are [batch*h*w][C] with element strides (sp = pixel stride, sc = channel

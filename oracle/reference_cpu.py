@@ -111,6 +111,19 @@ def synthetic_images(n, size, n_colors=3, seed=1234):
 
 
 # --------------------------------------------------------------------------- models
+def _pac(p):
+    """PacGAN packing degree: 1 for GLI, 2 for code/GAN_losses_iter_PAC.py (D sees
+    n_colors*2 channels: PAC:242,260,408,410)."""
+    return getattr(p, "pac", 1)
+
+
+def pack(t, B, pac):
+    """[pac*B, C, ...] -> [B, pac*C, ...]: torch.cat([t[0:B], t[B:2B]], 1) (PAC:582,609,682)."""
+    if pac == 1:
+        return t
+    return torch.cat([t[k * B:(k + 1) * B] for k in range(pac)], 1)
+
+
 def _maybe_sn(mod, on):
     return spectral_norm(mod) if on else mod
 
@@ -175,7 +188,7 @@ class _D0(nn.Module):
         seq = nn.Sequential()
         sn = p.spectral
         seq.add_module("Start-SpectralConv2d" if sn else "Start-Conv2d",
-                       _maybe_sn(nn.Conv2d(p.n_colors, p.D_h_size, 4, 2, 1, bias=False), sn))
+                       _maybe_sn(nn.Conv2d(p.n_colors * _pac(p), p.D_h_size, 4, 2, 1, bias=False), sn))
         if p.SELU:
             seq.add_module("Start-SELU", nn.SELU(inplace=True))
         elif p.Tanh_GD:
@@ -251,7 +264,7 @@ class _D1(nn.Module):
         self.dense = nn.Linear(512 * 4 * 4, 1)
         layers = []
         for idx, (cin, cout, k, s) in enumerate(self.SPEC):
-            cin = p.n_colors if cin is None else cin
+            cin = p.n_colors * _pac(p) if cin is None else cin
             layers.append(_maybe_sn(nn.Conv2d(cin, cout, k, s, 1, bias=True), p.spectral))
             last = idx == len(self.SPEC) - 1
             if p.spectral:
@@ -386,12 +399,15 @@ class Trainer:
         self.D = build_D(p)
         self.G.apply(weights_init)
         self.D.apply(weights_init)
-        B, C, S = p.batch_size, p.n_colors, p.image_size
+        B, C, S = p.batch_size, p.n_colors * _pac(p), p.image_size
+        self.pac = _pac(p)
         self.x = torch.FloatTensor(B, C, S, S)
         self.x_fake = torch.FloatTensor(B, C, S, S)
         self.y = torch.FloatTensor(B)
         self.y2 = torch.FloatTensor(B)
-        self.z = torch.FloatTensor(B, p.z_size, 1, 1)
+        # PacGAN draws 2B z per step: the reference resizes z's .data (PAC:607), which
+        # reshaped the Variable on the torch it was written for; allocate it 2B here
+        self.z = torch.FloatTensor(B * self.pac, p.z_size, 1, 1)
         self.u = torch.FloatTensor(B, 1, 1, 1)
         self.z_test = torch.FloatTensor(B, p.z_size, 1, 1).normal_(0, 1)
         self.grad_outputs = torch.ones(B)
@@ -410,8 +426,10 @@ class Trainer:
 
     # -- data
     def next_real(self):
-        idx = numpy.random.choice(self.images.shape[0], size=self.p.batch_size, replace=False)
-        return torch.stack([self.images[i] for i in idx], 0)
+        """GLI:176-177 (PAC:176: 2B indices, packed channel-wise at PAC:582/682)."""
+        B = self.p.batch_size
+        idx = numpy.random.choice(self.images.shape[0], size=B * self.pac, replace=False)
+        return pack(torch.stack([self.images[i] for i in idx], 0), B, self.pac)
 
     def _set_D_grad(self, flag):
         for q in self.D.parameters():
@@ -437,9 +455,9 @@ class Trainer:
                 self.y.data.resize_(B).fill_(1)
                 err_real = head_real(p.loss_D, y_pred, self.y)
                 err_real.backward()
-                self._draw_z(B, feed, "z_D")
+                self._draw_z(B * self.pac, feed, "z_D")
                 fake = G(self.z)
-                self.x_fake.data.resize_(fake.data.size()).copy_(fake.data)
+                self.x_fake.data.resize_(pack(fake, B, self.pac).size()).copy_(pack(fake.data, B, self.pac))
                 self.y.data.resize_(B).fill_(0)
                 y_pred_fake = D(self.x_fake.detach())
                 err_fake = head_fake(p.loss_D, y_pred_fake, self.y)
@@ -448,9 +466,9 @@ class Trainer:
             else:
                 self.y.data.resize_(B).fill_(1)
                 self.y2.data.resize_(B).fill_(0)
-                self._draw_z(B, feed, "z_D")
+                self._draw_z(B * self.pac, feed, "z_D")
                 fake = G(self.z)
-                self.x_fake.data.resize_(fake.data.size()).copy_(fake.data)
+                self.x_fake.data.resize_(pack(fake, B, self.pac).size()).copy_(pack(fake.data, B, self.pac))
                 y_pred_fake = D(self.x_fake.detach())
                 errD = head_relativistic_D(p.loss_D, y_pred, y_pred_fake, self.y, self.y2)
                 errD.backward()
@@ -475,8 +493,13 @@ class Trainer:
         for _ in range(p.Giters):
             G.zero_grad()
             self.y.data.resize_(B).fill_(1)
-            self._draw_z(B, feed, "z_G")
-            fake = G(self.z)
+            self._draw_z(B * self.pac, feed, "z_G")
+            if self.pac == 1:
+                fake = G(self.z)
+            else:
+                # PAC:673-674: the fresh z is drawn but unused; the G step reuses the D step's
+                # G(z) output (graph included) -- G's weights have not moved since
+                fake = pack(fake, B, self.pac)
             y_pred_fake = D(fake)
             y_pred = None
             if p.loss_D not in (1, 2, 3, 4):

@@ -4,7 +4,8 @@ Plus this build's own switches (prefixed ``--rgan_``), which the reference lacks
 ``--rgan_rng`` (``host``: draw z/u/batches from the CPU generators in the reference's
 order, bit-compatible inputs; ``device``: draw on the GPU, for throughput runs) and
 ``--rgan_sync_bn`` (SyncBN under data parallelism, default on; off = the reference
-DataParallel's per-shard statistics).
+DataParallel's per-shard statistics) and ``--rgan_pac 2`` (the PacGAN-2 script,
+code/GAN_losses_iter_PAC.py, which shares this CLI).
 """
 import argparse
 
@@ -41,6 +42,9 @@ def make_parser():
             p.add_argument("--" + name, type=typ, default=default)
     p.add_argument("--rgan_rng", choices=("host", "device"), default="host")
     p.add_argument("--rgan_sync_bn", type="bool", default=True)
+    p.add_argument("--rgan_pac", dest="pac", type=int, default=1, choices=(1, 2),
+                   help="2 = PacGAN-2, the reference's code/GAN_losses_iter_PAC.py (D sees 2 samples packed "
+                        "channel-wise)")
     p.add_argument("--rgan_synthetic", type=int, default=0,
                    help="use N synthetic images instead of an image folder (no torchvision here)")
     return p

@@ -76,7 +76,7 @@ struct GemmArgs {
   int KH, KW, stride, pad;
   FastDiv fgw, fghw;      // decomposition of m (CONV/CONVT2) or p (WGRAD)
   FastDiv fC, fKW;        // k (CONV/CONVT2) or n (WGRAD) -> (kh, kw, ci)
-  const float* Bw;        // packed weights [phase][K][N]
+  const float* Bw;        // packed weights [phase][N][K]
   float* C;
   OutMap out;
   const float* bias;
@@ -1039,7 +1039,11 @@ static void choose_tiling(Plan& p) {
   const long long tiles = (long long)tiles_m * tiles_n * p.phases;
   const int nk = ceil_div(g.K, BK);
   int splits = 1;
-  const long long target = 512;  // two resident 256-thread blocks per CU on 256 CUs
+  // two resident 256-thread blocks per CU on 256 CUs (RGAN_SPLIT_TARGET: tuning experiments)
+  static const long long target = [] {
+    const char* e = getenv("RGAN_SPLIT_TARGET");
+    return e ? atoll(e) : 512LL;
+  }();
   if (tiles < target) {
     splits = (int)((target + tiles - 1) / tiles);
     splits = std::min(splits, std::max(1, nk / 4));

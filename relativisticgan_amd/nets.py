@@ -268,7 +268,7 @@ class _D0(_Net):
         plan = []
         sn = p.spectral
         cls = SpectralConv2d if sn else Conv2d
-        start = cls(p.n_colors, p.D_h_size, 4, 2, 1, bias=False)
+        start = cls(p.n_colors * getattr(p, "pac", 1), p.D_h_size, 4, 2, 1, bias=False)  # PAC:408-410
         main.add_module("Start-SpectralConv2d" if sn else "Start-Conv2d", start)
         if p.SELU:
             main.add_module("Start-SELU", _Act("selu"))
@@ -368,7 +368,7 @@ class _D1(_Net):
         layers, plan = [], []
         sn = p.spectral
         for idx, (cin, cout, k, s) in enumerate(self.SPEC):
-            cin = p.n_colors if cin is None else cin
+            cin = p.n_colors * getattr(p, "pac", 1) if cin is None else cin  # PAC:242,260
             conv = (SpectralConv2d if sn else Conv2d)(cin, cout, k, s, 1, bias=True)
             layers.append(conv)
             if sn:

@@ -66,6 +66,8 @@ class Trainer:
         self.redD = dp.GradReducer(self.D.parameters()) if self.world > 1 else None
         self.redG = dp.GradReducer(self.G.parameters()) if self.world > 1 else None
         self.host_rng = getattr(p, "rgan_rng", "host") == "host"
+        self.pac = getattr(p, "pac", 1)  # 2: code/GAN_losses_iter_PAC.py
+        self._fake_D = None
         self.errD = self.errG = None
         self.last = {}
 
@@ -73,26 +75,41 @@ class Trainer:
     def _shard(self, t):
         return t[self.rank * self.B:(self.rank + 1) * self.B]
 
+    def _shard_pac(self, t):
+        """Global [pac*B, ...] draw -> this rank's [pac*B_local, ...] (each packing slot's
+        shard, so packing the local part gives the rank's shard of the packed batch)."""
+        if self.pac == 1:
+            return self._shard(t)
+        B = self.p.batch_size
+        return torch.cat([t[k * B + self.rank * self.B:k * B + (self.rank + 1) * self.B] for k in range(self.pac)])
+
+    def _pack(self, t):
+        """[pac*b, C, ...] -> [b, pac*C, ...]: torch.cat([t[0:b], t[b:2b]], 1) (PAC:582,609,674,682)."""
+        if self.pac == 1:
+            return t
+        b = t.shape[0] // self.pac
+        return torch.cat([t[k * b:(k + 1) * b] for k in range(self.pac)], 1)
+
     def _real(self, feed, key):
         if feed is not None and key in feed:
             return feed[key]
         from .kernels import gather_images
+        n = self.p.batch_size * self.pac
         if self.host_rng:
-            idx = numpy.random.choice(self.images.shape[0], size=self.p.batch_size, replace=False)
-            idx = self._shard(torch.from_numpy(idx.astype(numpy.int64))).to(self.device, non_blocking=True)
+            idx = numpy.random.choice(self.images.shape[0], size=n, replace=False)
+            idx = self._shard_pac(torch.from_numpy(idx.astype(numpy.int64))).to(self.device, non_blocking=True)
         else:
-            idx = torch.randperm(self.images.shape[0], device=self.device)[:self.p.batch_size]
-            idx = self._shard(idx)
-        return gather_images(self.images, idx)
+            idx = self._shard_pac(torch.randperm(self.images.shape[0], device=self.device)[:n])
+        return self._pack(gather_images(self.images, idx))
 
     def _normal(self, feed, key, shape):
         if feed is not None and key in feed:
             return feed[key]
         if self.host_rng:
-            return self._shard(torch.empty(shape).normal_(0, 1)).to(self.device, non_blocking=True)
+            return self._shard_pac(torch.empty(shape).normal_(0, 1)).to(self.device, non_blocking=True)
         # every rank draws the global batch from the same device generator and keeps its
         # shard: ranks see different z, and the union is the 1-process draw
-        return self._shard(torch.randn(shape, device=self.device))
+        return self._shard_pac(torch.randn(shape, device=self.device))
 
     def _uniform(self, feed, key, shape):
         if feed is not None and key in feed:
@@ -100,6 +117,16 @@ class Trainer:
         if self.host_rng:
             return self._shard(torch.empty(shape).uniform_(0, 1)).to(self.device, non_blocking=True)
         return self._shard(torch.rand(shape, device=self.device))
+
+    def _generate_D(self, z):
+        """The D step's fake batch.  Single samples: G(z) without a graph (GLI copies it into
+        x_fake's .data).  PacGAN: keep G's graph for the G step (PAC:674) and pack."""
+        if self.pac == 1:
+            with torch.no_grad():
+                return self.G(z)
+        self._zbuf = z.clone()  # the reference's persistent z buffer (GLI:490)
+        self._fake_D = self.G(self._zbuf)
+        return self._pack(self._fake_D).detach()
 
     @staticmethod
     def _arm(red):
@@ -115,7 +142,7 @@ class Trainer:
         p, D, G = self.p, self.D, self.G
         kind = p.loss_D
         gp_on = kind == 3 or p.grad_penalty
-        zshape = (p.batch_size, p.z_size, 1, 1)
+        zshape = (p.batch_size * self.pac, p.z_size, 1, 1)
         if i % p.print_every == 0:
             with torch.no_grad():
                 self.fake_test = G(self.z_test)  # GLI:564 (sample image; BN running stats move)
@@ -128,8 +155,7 @@ class Trainer:
                 err_real = loss_D_real(kind, y_pred)
                 err_real.backward()
                 z = self._normal(feed, "z_D", zshape)
-                with torch.no_grad():
-                    x_fake = G(z)
+                x_fake = self._generate_D(z)
                 y_pred_fake = D(x_fake)
                 err_fake = loss_D_fake(kind, y_pred_fake)
                 if not gp_on:
@@ -138,8 +164,7 @@ class Trainer:
                 errD = err_real.detach() + err_fake.detach()
             else:
                 z = self._normal(feed, "z_D", zshape)
-                with torch.no_grad():
-                    x_fake = G(z)
+                x_fake = self._generate_D(z)
                 y_pred_fake = D(x_fake)
                 errD = loss_D(kind, y_pred, y_pred_fake)
                 if not gp_on:
@@ -166,7 +191,15 @@ class Trainer:
         for _ in range(p.Giters):
             G.zero_grad()
             z = self._normal(feed, "z_G", zshape)
-            fake = G(z)
+            if self.pac == 1:
+                fake = G(z)
+            else:
+                # PAC:673-674: the G step reuses the D step's G(z) (graph kept; G's weights
+                # have not moved).  The fresh z is written into the persistent z buffer
+                # through .data (PAC:673), which that graph saved for G's first layer without
+                # a version bump: the first layer's weight gradient reads the NEW z.
+                self._zbuf.data.copy_(z)
+                fake, self._fake_D = self._pack(self._fake_D), None
             y_pred_fake = D(fake)
             y_pred = None
             recG = {"z": z}
@@ -196,7 +229,7 @@ class Trainer:
         return {"i": i, "current_set_images": current_set_images, "G_state": self.G.state_dict(),
                 "D_state": self.D.state_dict(), "G_optimizer": self.optG.state_dict(),
                 "D_optimizer": self.optD.state_dict(), "G_scheduler": self.decayG.state_dict(),
-                "D_scheduler": self.decayD.state_dict(), "z_test": self.z_test}
+                "D_scheduler": self.decayD.state_dict(), "z_test": _gather_batch(self.z_test)}
 
     def load(self, ckpt):
         self.G.load_state_dict(ckpt["G_state"])
@@ -215,7 +248,64 @@ class Trainer:
         return '[%d] Diff: %.4f loss_D: %.4f loss_G: %.4f time:%.4f' % (i, -d + g, d, g, elapsed)
 
 
+def _gather_batch(t):
+    """Concatenate every rank's shard along the batch (rank order); identity on one rank."""
+    if not dp.active():
+        return t
+    import torch.distributed as dist
+    parts = [torch.empty_like(t) for _ in range(dp.world())]
+    dist.all_gather(parts, t.contiguous())
+    return torch.cat(parts)
+
+
+def run_dirs(p, title):
+    """GLI:86-100: <output_folder>/<title>-<run> with logs/ and images/ (first free run
+    number); the extra-image folder is created when images will be generated."""
+    run = 0
+    base = f"{p.output_folder}/{title}-{run}"
+    while os.path.exists(base):
+        run += 1
+        base = f"{p.output_folder}/{title}-{run}"
+    os.makedirs(os.path.join(base, "logs"))
+    os.makedirs(os.path.join(base, "images"))
+    if p.gen_extra_images > 0:
+        os.makedirs(p.extra_folder, exist_ok=True)
+    return base
+
+
+def generate_extra_images(G, p, folder, device="cuda"):
+    """GLI:752-768: empty (or create) `folder`, then write gen_extra_images G samples,
+    100 per G call, as fake_samples_%05d.png of fake*.5+.5.  G stays in train mode like the
+    reference (its BN batch statistics and running stats move).  Under data parallelism
+    every rank draws the same 100 z, runs its shard (SyncBN = the 100-batch statistics)
+    and writes its shard's files."""
+    from .images import save_images
+    if dp.rank() == 0:
+        if os.path.exists(folder):
+            for root, _dirs, files in os.walk(folder):
+                for f in files:
+                    os.unlink(os.path.join(root, f))
+        else:
+            os.makedirs(folder)
+    if dp.active():
+        import torch.distributed as dist
+        dist.barrier()
+    world, rank = dp.world(), dp.rank()
+    if 100 % world:
+        raise ValueError(f"extra images are drawn 100 per batch: not divisible by {world} ranks")
+    per = 100 // world
+    ext_curr = 0
+    with torch.no_grad():
+        for _ in range(int(p.gen_extra_images / 100)):
+            z = torch.randn(100, p.z_size, 1, 1, device=device)[rank * per:(rank + 1) * per]
+            fake = G(z)
+            save_images(fake, [os.path.join(folder, "fake_samples_%05d.png" % (ext_curr + rank * per + k))
+                               for k in range(per)])
+            ext_curr += 100
+
+
 def main(argv=None):
+    from .images import save_image
     p = parse(argv)
     start = time.time()
     if not torch.cuda.is_available():
@@ -226,27 +316,45 @@ def main(argv=None):
         dist.init_process_group("nccl")
         dp.setup(sync_bn=p.rgan_sync_bn)
     title = TITLES[p.loss_D] + ("seed%i" % p.seed if p.seed is not None else "")
+    lead = dp.rank() == 0
+    base = run_dirs(p, title) if lead else None
+    log = open(os.path.join(base, "logs", "log.txt"), "w") if lead else None
+
+    def say(s):
+        if lead:
+            print(s, flush=True)
+            print(s, file=log, flush=True)
     n = p.rgan_synthetic or 1024
     images = synthetic_images(n, p.image_size, p.n_colors)
     t = Trainer(p, images)
-    print(p)
-    print(f"Random Seed: {p.seed}")
+    say(p)
+    say(f"Random Seed: {p.seed}")
     iter_offset, current_set_images = 0, 0
     if p.load:
-        iter_offset, current_set_images = t.load(torch.load(p.load, map_location="cuda", weights_only=False))
-    print(t.G)
-    print(t.D)
+        iter_offset, current_set_images = t.load(torch.load(p.load, map_location="cuda", weights_only=True))
+        say(f"Resumed from iteration {current_set_images * p.gen_every}.")
+    say(t.G)
+    say(t.D)
     for i in range(iter_offset, p.n_iter):
         t.iteration(i)
-        if (i + 1) % p.print_every == 0 and dp.rank() == 0:
-            print(t.log_line(i, time.time() - start), flush=True)
+        if i % p.print_every == 0:  # GLI:563-565 (the sample batch was drawn inside the iteration)
+            grid = _gather_batch(t.fake_test)
+            if lead:
+                save_image(grid, os.path.join(base, "images", "fake_samples_iter%05d.png" % i), normalize=True)
+        if (i + 1) % p.print_every == 0:
+            say(t.log_line(i, time.time() - start))
         if (i + 1) % p.gen_every == 0:
             current_set_images += 1
-            if p.save and dp.rank() == 0:
-                os.makedirs(os.path.join(p.extra_folder, "models"), exist_ok=True)
-                torch.save(t.state(i + 1, current_set_images),
-                           os.path.join(p.extra_folder, "models", "state_%02d.pth" % current_set_images))
-                print("Models saved")
+            if p.save:
+                st = t.state(i + 1, current_set_images)  # collective under DP (z_test shards)
+                if lead:
+                    os.makedirs(os.path.join(p.extra_folder, "models"), exist_ok=True)
+                    torch.save(st, os.path.join(p.extra_folder, "models", "state_%02d.pth" % current_set_images))
+                    say("Models saved")
+            if p.gen_extra_images > 0:
+                generate_extra_images(t.G, p, "%s/%01d/" % (p.extra_folder, current_set_images))
+    if log:
+        log.close()
     return t
 
 

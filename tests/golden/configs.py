@@ -42,11 +42,24 @@ CONFIGS = {
     "ralsgan_wd": _cfg(loss_D=7, weight_decay=0.01, decay=0.1),
     "ralsgan_nnconv": _cfg(loss_D=7, NN_conv="True"),
     "rasgan_nnconv_spectralG": _cfg(loss_D=6, NN_conv="True", spectral_G="True"),
+    # PacGAN-2 (code/GAN_losses_iter_PAC.py): no reference fixture -- the script fails at
+    # PAC:609 on the pinned torch (`z.data.resize_(2B)` no longer reshapes the Variable z, so
+    # G(z) returns B samples and the channel-wise packing of fake[B:2B] is empty).  The oracle
+    # restates the script's torch-0.4 semantics (2B z per step, stale D-step fake reused by
+    # the G step at PAC:674); parity of these configs is GPU-vs-oracle only ("unpinned").
+    "ralsgan_pac2": dict(_cfg(loss_D=7), pac=2, golden=False),
+    "sgan_pac2_gp": dict(_cfg(loss_D=1, grad_penalty="True"), pac=2, golden=False),
+    "rahinge_pac2_arch1": {"args": {"image_size": 32, "batch_size": 8, "z_size": 16, "loss_D": 8, "arch": 1,
+                                    "n_iter": 2}, "seed": 1, "n_images": 64, "pac": 2, "golden": False},
     "wgangp_arch1": {"args": {"image_size": 32, "batch_size": 8, "z_size": 16, "loss_D": 3,
                               "arch": 1, "n_iter": 2}, "seed": 1, "n_images": 64},
     "rahinge_arch1": {"args": {"image_size": 32, "batch_size": 8, "z_size": 16, "loss_D": 8,
                                "arch": 1, "n_iter": 2}, "seed": 1, "n_images": 64},
 }
+
+
+# configs with a reference fixture (tests/golden/<name>.npz) pinning the oracle bitwise
+PINNED = [n for n, c in CONFIGS.items() if c.get("golden", True)]
 
 
 def summarize_indices(numel, count=64, seed=97):

@@ -37,9 +37,10 @@ import numpy as np
 import torch
 
 REF_SCRIPT = "/root/reference/code/GAN_losses_iter.py"
+REF_SCRIPT_PAC = "/root/reference/code/GAN_losses_iter_PAC.py"  # PacGAN-2 variant (config key "pac": 2)
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
-from tests.golden.configs import CONFIGS, Recorder  # noqa: E402
+from tests.golden.configs import CONFIGS, PINNED, Recorder  # noqa: E402
 
 THREADS = 1
 
@@ -167,7 +168,8 @@ def run_config(name, cfg):
     torch.optim.Adam.__init__ = init_hook
     torch.optim.Adam.step = step_hook
     tmp = tempfile.mkdtemp(prefix="rgan_golden_")
-    argv = [REF_SCRIPT, "--cuda", "False", "--seed", str(cfg.get("seed", 1)),
+    script = REF_SCRIPT_PAC if cfg.get("pac", 1) == 2 else REF_SCRIPT
+    argv = [script, "--cuda", "False", "--seed", str(cfg.get("seed", 1)),
             "--n_iter", str(n_iter), "--gen_extra_images", "0", "--print_every", "1000",
             "--output_folder", tmp, "--extra_folder", tmp + "/extra", "--input_folder", tmp]
     for k, v in args.items():
@@ -178,14 +180,14 @@ def run_config(name, cfg):
     sys.argv = argv
     os.chdir(tmp)
     try:
-        runpy.run_path(REF_SCRIPT, run_name="__main__")
+        runpy.run_path(script, run_name="__main__")
     finally:
         sys.argv = old_argv
         os.chdir(old_cwd)
         torch.optim.Adam.__init__ = orig_init
         torch.optim.Adam.step = orig_step
     rec.store["meta.json"] = np.frombuffer(json.dumps({
-        "config": name, "args": args, "seed": cfg.get("seed", 1), "n_iter": n_iter,
+        "config": name, "args": args, "seed": cfg.get("seed", 1), "n_iter": n_iter, "pac": cfg.get("pac", 1),
         "n_images": cfg.get("n_images", 64), "threads": THREADS,
         "torch": torch.__version__}).encode(), dtype=np.uint8).copy()
     out = os.path.join(HERE, f"{name}.npz")
@@ -194,7 +196,7 @@ def run_config(name, cfg):
 
 
 if __name__ == "__main__":
-    names = sys.argv[1:] or list(CONFIGS)
+    names = sys.argv[1:] or PINNED
     if len(names) == 1:
         print(names[0], "->", run_config(names[0], CONFIGS[names[0]]), flush=True)
     else:  # one fresh interpreter per config: the reference mutates global torch state

@@ -28,7 +28,7 @@ def golden_meta(g):
 def param_for(name, **extra):
     cfg = CONFIGS[name]
     kw = dict(cfg["args"])
-    kw.update(seed=cfg.get("seed", 1), cuda=False, gen_extra_images=0, print_every=1000)
+    kw.update(seed=cfg.get("seed", 1), cuda=False, gen_extra_images=0, print_every=1000, pac=cfg.get("pac", 1))
     kw.update(extra)
     return make_param(**kw)
 

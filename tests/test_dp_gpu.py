@@ -45,7 +45,15 @@ def _capture(t, store):
     return hooks
 
 
-def _run(name, world, rank, n_iter=2):
+# Free-running trajectories: iteration 1 inherits iteration 0's Adam sign flips (near-zero
+# gradients whose sign depends on the fp32 summation order).  PacGAN's G-step gradient (it
+# reuses the D step's G graph) amplifies those into ~5e-3 at iteration 1, so it is compared
+# on iteration 0 only; teacher-forced parity of every PacGAN iteration is test_parity_gpu's.
+N_ITER = {"ralsgan_pac2": 1}
+
+
+def _run(name, world, rank, n_iter=None):
+    n_iter = n_iter or N_ITER.get(name, 2)
     from relativisticgan_amd.train import Trainer
     p = param_for(name)
     p.rgan_rng = "host"
@@ -86,7 +94,7 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("name", ["ralsgan", "rasgan", "wgangp", "rahinge_spectral", "sgan"])
+@pytest.mark.parametrize("name", ["ralsgan", "rasgan", "wgangp", "rahinge_spectral", "sgan", "ralsgan_pac2"])
 def test_dp2_matches_single_process(name):
     single = _run(name, 1, 0)
     path = os.path.join(tempfile.mkdtemp(), "dp.pt")
