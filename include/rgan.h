@@ -98,6 +98,11 @@ int rgan_nn_unfold_grad(const float* dwt, int cout, int cin, float* dw, void* st
  * strides[4]; grid = 0: out [B][H][W][C] (one image per file, padding 0);
  * grid = 1: make_grid layout [Hg][Wg][C], nrow tiles per row, `padding` pixels of 0.
  * rgan_minmax: out2 = {min, max} of x[0..n) (ws: rgan_minmax_ws_bytes). */
+/* Real-image batch (GLI:173-177 + ToTensor/Normalize GLI:160-166): out[b] = (u8 / 255 - 0.5)
+ * / 0.5 of images[idx[b]], images = decoded uint8 [N][per] resident on the device
+ * (per = C*S*S, a multiple of 4; out 16-byte aligned). */
+int rgan_gather_images_u8(const unsigned char* images, const long long* idx, int batch, long long per,
+                          float* out, void* stream);
 size_t rgan_minmax_ws_bytes(long long n);
 int rgan_minmax(const float* x, long long n, float* out2, void* ws, void* stream);
 int rgan_images_to_u8(const float* x, int B, int C, int H, int W, const long long* strides,

@@ -36,6 +36,7 @@ _SIGS = {
     "rgan_conv_wgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "rgan_nn_fold_weight": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
     "rgan_nn_unfold_grad": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    "rgan_gather_images_u8": (c_int, [c_vp, c_vp, c_int, c_ll, c_vp, c_vp]),
     "rgan_minmax_ws_bytes": (c_sz, [c_ll]),
     "rgan_minmax": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
     "rgan_images_to_u8": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_f, c_f, c_vp, c_int, c_int, c_int, c_vp,

@@ -95,9 +95,35 @@ __global__ __launch_bounds__(256) void to_u8_kernel(ImgArgs a) {
   }
 }
 
+// Real-image batches (GLI:159-179): the dataset lives in HBM as decoded uint8 [N][C][S][S]
+// (ImageFolder + Resize done once at load); a batch is a gather of sampled images fused with
+// ToTensor + Normalize(0.5, 0.5): x = (u8 / 255 - 0.5) / 0.5, each op rounded in fp32 like
+// torchvision's div(255).sub_(0.5).div_(0.5).  4 bytes -> float4 per thread (per % 4 == 0).
+__global__ __launch_bounds__(256) void gather_u8_kernel(const unsigned char* __restrict__ images,
+                                                        const long long* __restrict__ idx, int batch, long long per,
+                                                        float* __restrict__ out) {
+  const long long q = per / 4, total = (long long)batch * q;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long b = i / q, e = i - b * q;
+    const uchar4 v = reinterpret_cast<const uchar4*>(images + idx[b] * per)[e];
+    auto f = [](unsigned char u) { return __fdiv_rn(__fsub_rn(__fdiv_rn((float)u, 255.f), 0.5f), 0.5f); };
+    reinterpret_cast<float4*>(out)[i] = make_float4(f(v.x), f(v.y), f(v.z), f(v.w));
+  }
+}
+
 }  // namespace rgan
 
 using namespace rgan;
+
+extern "C" int rgan_gather_images_u8(const unsigned char* images, const long long* idx, int batch, long long per,
+                                     float* out, void* stream) {
+  RGAN_REQUIRE(images && idx && out && batch > 0 && per > 0 && per % 4 == 0 && ((uintptr_t)out & 15) == 0);
+  const long long total = (long long)batch * per / 4;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 8192);
+  gather_u8_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(images, idx, batch, per, out);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" size_t rgan_minmax_ws_bytes(long long n) {
   (void)n;

@@ -471,10 +471,16 @@ def lr_decay(hyper, gamma):
 
 
 def gather_images(images, idx, out=None):
+    """images[idx] as float32; a uint8 dataset (decoded images, relativisticgan_amd.data) is
+    converted on the fly with ToTensor + Normalize(0.5, 0.5) (GLI:160-166)."""
     B = idx.numel()
     per = images[0].numel()
     if out is None:
         out = torch.empty((B,) + tuple(images.shape[1:]), dtype=torch.float32, device=images.device)
+    if images.dtype == torch.uint8:
+        L.check(L.lib().rgan_gather_images_u8(L.ptr(images), L.ptr(idx), B, per, L.ptr(out), L.stream()),
+                "rgan_gather_images_u8")
+        return out
     L.check(L.lib().rgan_gather_images(L.ptr(images), L.ptr(idx), B, per, L.ptr(out), L.stream()),
             "rgan_gather_images")
     return out

@@ -258,6 +258,19 @@ def _gather_batch(t):
     return torch.cat(parts)
 
 
+def load_images(p, device="cuda"):
+    """The training set in HBM: --rgan_synthetic N synthetic images, or --input_folder as
+    torchvision's ImageFolder + Resize + ToTensor + Normalize would give it (GLI:159-169),
+    decoded once into uint8 (relativisticgan_amd.data)."""
+    if p.rgan_synthetic:
+        return synthetic_images(p.rgan_synthetic, p.image_size, p.n_colors, device=device)
+    if p.CIFAR10:
+        raise SystemExit("--CIFAR10: torchvision's CIFAR-10 loader unpickles python batches; convert the set "
+                         "to an image folder and pass --input_folder instead")
+    from .data import load_image_folder
+    return load_image_folder(p.input_folder, p.image_size, p.n_colors, device=device)
+
+
 def run_dirs(p, title):
     """GLI:86-100: <output_folder>/<title>-<run> with logs/ and images/ (first free run
     number); the extra-image folder is created when images will be generated."""
@@ -324,8 +337,7 @@ def main(argv=None):
         if lead:
             print(s, flush=True)
             print(s, file=log, flush=True)
-    n = p.rgan_synthetic or 1024
-    images = synthetic_images(n, p.image_size, p.n_colors)
+    images = load_images(p)
     t = Trainer(p, images)
     say(p)
     say(f"Random Seed: {p.seed}")

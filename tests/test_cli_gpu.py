@@ -57,3 +57,15 @@ def test_generate_from_checkpoint():
     files = sorted(os.listdir(folder))
     assert len(files) == 100
     assert np.asarray(Image.open(os.path.join(folder, files[-1]))).shape == (32, 32, 3)
+
+
+def test_train_cli_from_image_folder():
+    from tests.test_data import _make_folder
+    from relativisticgan_amd.train import main
+    root = tempfile.mkdtemp()
+    folder = _make_folder(os.path.join(root, "data"))
+    t = main(["--loss_D", "6", "--image_size", "32", "--batch_size", "4", "--z_size", "16", "--G_h_size", "8",
+              "--D_h_size", "8", "--seed", "1", "--n_iter", "2", "--print_every", "1000", "--gen_extra_images", "0",
+              "--output_folder", os.path.join(root, "out"), "--input_folder", folder, "--save", "False"])
+    assert t.images.dtype == torch.uint8 and tuple(t.images.shape) == (5, 3, 32, 32)
+    assert torch.isfinite(t.errD) and torch.isfinite(t.errG)
