@@ -51,8 +51,8 @@ typedef struct RganConv {
 size_t rgan_conv_workspace(const RganConv* d, int which, int prepacked);
 
 /* Kernel-ready weight layout for which = 0 (fwd) or 1 (dgrad): [phases][N][K] floats for
- * the implicit GEMMs (k contiguous: the B operand's LDS rows), [Cin][4][4][Cout] for the narrow (<= 4 output channel) transposed
- * conv.  Packing is separated so callers can cache it per weight version (weights change
+ * the implicit GEMMs (k contiguous: the B operand's LDS rows), [4][Cin][16] for the narrow
+ * (<= 4 output channel) transposed conv.  Packing is separated so callers can cache it per weight version (weights change
  * only at the optimizer step, but each net is run 2-4 times per iteration).
  * rgan_conv_pack_floats returns 0 when the op reads the torch layout directly (narrow
  * 4x4 convs with <= 4 input channels) -- or when the descriptor is unsupported, which

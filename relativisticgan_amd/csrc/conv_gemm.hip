@@ -798,17 +798,13 @@ __global__ __launch_bounds__(256) void pack_weights(PackArgs a) {
 
 
 // ---------------------------------------------------------------- narrow convolutions
-// fp32 MFMA runs at the fp32 VALU rate on gfx950, so a GEMM with N <= 4 (a 32-wide MFMA
-// tile at <= 12% occupancy) or K <= 64 (one or two BK tiles around a full prologue and
-// epilogue) loses to a direct VALU convolution that wastes no lanes:
-//   convt2_narrow   k4 s2 p1 ConvTranspose2d (and the Conv2d dgrad of the same shape)
-//                   with <= 4 output channels: G's image layer (GLI:448) and D's image
-//                   gradient (the backward of GLI:361 into G).  One thread per input-grid
-//                   pixel computes the 4 output phases x NC channels from its 3x3
-//                   neighbourhood; weights are wave-uniform (scalar loads).
-//   conv_narrow_in  Conv2d with <= 4 input channels and a 4x4 kernel: D's image layer
-//                   (GLI:361).  One thread per output pixel x 32 output channels (grid.y
-//                   over channel groups; the weights of a group are wave-uniform).
+// The image layers do not fit the pipelined GEMM: N <= 4 wastes >= 88% of a 32-wide MFMA
+// tile, and K = 16*CI <= 64 is one or two BK tiles around a full prologue and epilogue:
+//   convt2_narrow_mfma   k4 s2 p1 ConvTranspose2d (and the Conv2d dgrad of the same shape)
+//                        with <= 4 output channels: G's image layer (GLI:448) and D's image
+//                        gradient (the backward of GLI:410 into G), on 4x4x1 MFMA blocks.
+//   conv_narrow_in_mfma  Conv2d with <= 4 input channels and a 4x4 kernel: D's image layer
+//                        (GLI:410) as a single-pass MFMA tile (below).
 struct NarrowArgs {
   const float* x;
   long long xsb, xsc, xsh, xsw;
@@ -824,58 +820,192 @@ struct NarrowArgs {
   float alpha;
 };
 
-constexpr int NT_T = 16, NT_HT = NT_T + 2, NT_CH = 32, NT_LDP = NT_CH + 4;
-
-// Block = a 16x16 tile of input-grid pixels of one sample; the (16+2)^2 halo tile is
-// staged through LDS 32 channels at a time with coalesced float4 loads (each pixel's
-// channel chunk is one 128-byte line), then every thread reads its 3x3 neighbourhood
-// from LDS (row stride 36 floats: conflict-free ds_read_b128 across 16 lanes).  The
-// chunk's weights are staged in LDS too and read as wave-uniform broadcasts: loading
-// them as 192 scalar values per step drove hipcc (ROCm 7.2) into SGPR spills that it
-// miscompiled (the spilled weight pointer was overwritten by another kernel argument).
-template <int NC>
-__global__ __launch_bounds__(256) void convt2_narrow(NarrowArgs a) {
-  __shared__ __attribute__((aligned(16))) float xs[NT_HT * NT_HT * NT_LDP];
-  __shared__ __attribute__((aligned(16))) float wl[NT_CH * 16 * NC];
-  const int tid = threadIdx.x;
-  const int tiles_w = (a.W + NT_T - 1) / NT_T, tiles_h = (a.H + NT_T - 1) / NT_T;
-  const int per_img = tiles_w * tiles_h;
-  const int b = blockIdx.x / per_img, trem = blockIdx.x - b * per_img;
-  const int ty = trem / tiles_w, tx = trem - ty * tiles_w;
-  const int ti = tid / NT_T, tj = tid % NT_T;
-  const int i = ty * NT_T + ti, j = tx * NT_T + tj;
-  const float* xb = a.x + (long long)b * a.xsb;
-  float acc[4][NC];
+// Conv2d with a 4x4 kernel and CI <= 4 input channels (D's image layer, GLI:410) as ONE MFMA
+// GEMM tile pass: M = output pixels, N = Cout, K = 16*CI (16..64).  K is too short for the
+// pipelined GEMM (one or two BK tiles around a full prologue/epilogue, and a per-element
+// im2col index decomposition in every tile), so a block builds its whole 128 x K im2col
+// tile once (per-row pixel decomposition, per-k (ci, kh, kw) from bit fields), stages the
+// 128 x K weight tile straight from torch layout ([co][ci][kh][kw] = [n][k], k-contiguous),
+// and runs K/2 MFMA steps per accumulator from k-contiguous LDS rows (row stride K+4 dwords,
+// an odd number of 16-B slots: conflict-free ds_read_b128; lane half h takes k in
+// [h K/2, (h+1) K/2)).  Epilogue: *wscale, +bias, activation, row offsets from an LDS table.
+template <int CI>
+__global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
+  constexpr int K = CI * 16, KH2 = K / 2, LD = K + 4;
+  __shared__ __attribute__((aligned(16))) float As[128 * LD];
+  __shared__ __attribute__((aligned(16))) float Bs[128 * LD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, lk = lane >> 5;
+  const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
+  const int HWo = a.Ho * a.Wo, M = a.B * HWo;
+  const int m0 = blockIdx.x * 128, n0 = blockIdx.y * 128;
+  {
+    // all K/2 weight loads in flight before the first LDS store (a rolled loop would wait
+    // on each load in turn: ~24 serialised L2 round trips per block)
+    float wv[K / 2];
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-#pragma unroll
-    for (int c = 0; c < NC; ++c) acc[q][c] = 0.f;
-  const float* __restrict__ wp = a.w;
-  for (int c0 = 0; c0 < a.C; c0 += NT_CH) {
-    __syncthreads();
-    for (int e = tid; e < NT_HT * NT_HT * (NT_CH / 4); e += 256) {
-      const int pix = e / (NT_CH / 4), q = e % (NT_CH / 4);
-      const int hi = pix / NT_HT, hj = pix - hi * NT_HT;
-      const int ih = ty * NT_T - 1 + hi, iw = tx * NT_T - 1 + hj, c = c0 + 4 * q;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W && c < a.C)
-        v = *reinterpret_cast<const float4*>(xb + (long long)ih * a.xsh + (long long)iw * a.xsw + c);
-      *reinterpret_cast<float4*>(xs + pix * NT_LDP + 4 * q) = v;
+    for (int j = 0; j < K / 2; ++j) {
+      const int e = tid + 256 * j, r = e / K, k = e - r * K, n = n0 + r;
+      wv[j] = n < a.Cout ? a.w[(size_t)n * K + k] : 0.f;
     }
-    const int nw = min(NT_CH, a.C - c0) * 16 * NC;
-    for (int e = tid; e < nw; e += 256) wl[e] = wp[(size_t)c0 * 16 * NC + e];
+#pragma unroll
+    for (int j = 0; j < K / 2; ++j) {
+      const int e = tid + 256 * j, r = e / K, k = e - r * K;
+      Bs[r * LD + k] = wv[j];
+    }
+  }
+  {
+    const int row = tid >> 1, half = tid & 1, m = m0 + row;
+    float* dst = As + row * LD + half * KH2;
+    if (m < M) {
+      const int b = m / HWo, rem = m - b * HWo, oi = rem / a.Wo, oj = rem - oi * a.Wo;
+      const int ih0 = oi * a.stride - a.pad, iw0 = oj * a.stride - a.pad;
+      const float* xb = a.x + (long long)b * a.xsb;
+#pragma unroll
+      for (int kk = 0; kk < KH2; ++kk) {
+        const int k = half * KH2 + kk, ci = k >> 4, ih = ih0 + ((k >> 2) & 3), iw = iw0 + (k & 3);
+        dst[kk] = ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                      ? xb[(long long)ci * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
+                      : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < KH2; ++kk) dst[kk] = 0.f;
+    }
+  }
+  __syncthreads();
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  const float* Ar = As + (wm + l32) * LD + lk * KH2;
+  const float* Br = Bs + (wn + l32) * LD + lk * KH2;
+#pragma unroll
+  for (int q = 0; q < KH2 / 4; ++q) {
+    float4 a4[2], b4[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      a4[t] = *reinterpret_cast<const float4*>(Ar + 32 * t * LD + 4 * q);
+      b4[t] = *reinterpret_cast<const float4*>(Br + 32 * t * LD + 4 * q);
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[i][s4], b4[j][s4], acc[i][j], 0, 0, 0);
+  }
+  __syncthreads();  // As is reused for the row-offset table
+  long long* moff = reinterpret_cast<long long*>(As);
+  if (tid < 128) {
+    const int m = m0 + tid;
+    long long o = -1;
+    if (m < M) {
+      const int b = m / HWo, rem = m - b * HWo, oi = rem / a.Wo, oj = rem - oi * a.Wo;
+      o = (long long)b * a.ysb + (long long)oi * a.ysh + (long long)oj * a.ysw;
+    }
+    moff[tid] = o;
+  }
+  __syncthreads();
+  const float wsc = a.wscale ? a.wscale[0] : 1.f;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn + 32 * j + l32;
+      if (col >= a.Cout) continue;
+      const float bv = a.bias ? a.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const long long o = moff[wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk];
+        if (o >= 0) a.y[o + (long long)col * a.ysc] = act_fwd(acc[i][j][r] * wsc + bv, a.act, a.alpha);
+      }
+    }
+}
+
+// k4 s2 p1 ConvTranspose2d with NC <= 4 output channels on v_mfma_f32_4x4x1_16b_f32: 16
+// independent 4x4 outer products per instruction, so the 4 output channels fill the N
+// dimension (75% useful at NC = 3 against 9% for a 32-wide tile) and the 64 lanes are 64
+// input-grid pixels: lane 4b+i supplies pixel 4b+i's input value (A row i of block b),
+// lane 4b+j the weight of output channel j (B column j, the same in every block); lane
+// 4b+j receives D[b][i][j] = pixel 4b+i, channel j.  Each of the 16 (phase, tap) pairs is
+// one K=1 step per input channel: output (2i+ph, 2j+pw) <- input (i+ph-th, j+pw-tw) through
+// tap (2th+1-ph, 2tw+1-pw), th, tw in {0, 1}.
+// Block: 16 x 32 input pixels (4 waves x 2 groups of 4 x 16), the (18 x 34)-pixel halo
+// staged through LDS 16 channels at a time (pixel stride 20 dwords: ds_read_b128 of 4
+// channels), weights [co][c][tap] staged beside it; per 4 channels a wave reads 18 + 16
+// ds_read_b128 and issues 128 MFMAs.
+constexpr int NM_TR = 16, NM_TC = 32, NM_HR = NM_TR + 2, NM_HC = NM_TC + 2, NM_CH = 16, NM_LD = NM_CH + 4;
+constexpr int NM_XQ = NM_HR * NM_HC * (NM_CH / 4);  // float4 slots of one staged chunk
+constexpr int NM_XPT = (NM_XQ + 255) / 256;         // ... per thread
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int NC>
+__global__ __launch_bounds__(256, 2) void convt2_narrow_mfma(NarrowArgs a) {
+  __shared__ __attribute__((aligned(16))) float xs[NM_HR * NM_HC * NM_LD];
+  __shared__ __attribute__((aligned(16))) float wl[4 * NM_CH * 16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tiles_c = (a.W + NM_TC - 1) / NM_TC, tiles_r = (a.H + NM_TR - 1) / NM_TR;
+  const int per_img = tiles_c * tiles_r;
+  const int b = blockIdx.x / per_img, trem = blockIdx.x - b * per_img;
+  const int tr = trem / tiles_c, tc = trem - tr * tiles_c;
+  const int r0 = tr * NM_TR, c0p = tc * NM_TC;
+  const float* xb = a.x + (long long)b * a.xsb;
+  const int co = lane & 3;
+  // this lane's pixel in each group (tile coords): row 4 wid + lane / 16, col 16 g + lane % 16
+  const int pr = 4 * wid + (lane >> 4), pc = lane & 15;
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[g][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int ch0 = 0; ch0 < a.C; ch0 += NM_CH) {
+    const int nch = min(NM_CH, a.C - ch0);
+    float4 stage[NM_XPT];
+#pragma unroll
+    for (int t = 0; t < NM_XPT; ++t) {
+      const int e = tid + 256 * t, pix = e >> 2, q = e & 3;
+      const int hr = pix / NM_HC, hc = pix - hr * NM_HC;
+      const int ih = r0 - 1 + hr, iw = c0p - 1 + hc, c = ch0 + 4 * q;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < NM_XQ && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W && c < a.C)
+        v = *reinterpret_cast<const float4*>(xb + (long long)ih * a.xsh + (long long)iw * a.xsw + c);
+      stage[t] = v;
+    }
+    // weights: packed [4][C][16]; this chunk's [co][c][tap] (c >= nch -> 0)
+    const int wc = tid >> 4, wq = (tid >> 2) & 3, wco = tid & 3;  // 16 ch x 4 quads x 4 co = 256
+    float4 wv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (wc < nch) wv = *reinterpret_cast<const float4*>(a.w + ((size_t)wco * a.C + ch0 + wc) * 16 + 4 * wq);
+    __syncthreads();  // previous chunk's reads are done
+#pragma unroll
+    for (int t = 0; t < NM_XPT; ++t) {
+      const int e = tid + 256 * t;
+      if (e < NM_XQ) *reinterpret_cast<float4*>(xs + (e >> 2) * NM_LD + 4 * (e & 3)) = stage[t];
+    }
+    *reinterpret_cast<float4*>(wl + (wco * NM_CH + wc) * 16 + 4 * wq) = wv;
     __syncthreads();
-    const int nq = min(NT_CH, a.C - c0) / 4;
-    for (int c4 = 0; c4 < nq; ++c4) {
-      float4 xv[3][3];
+    for (int c4 = 0; c4 < nch / 4; ++c4) {
+      float4 xv[2][3][3];
 #pragma unroll
-      for (int u = 0; u < 3; ++u)
+      for (int g = 0; g < 2; ++g)
 #pragma unroll
-        for (int v = 0; v < 3; ++v)
-          xv[u][v] = *reinterpret_cast<const float4*>(xs + ((ti + u) * NT_HT + tj + v) * NT_LDP + 4 * c4);
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+          for (int v = 0; v < 3; ++v)
+            xv[g][u][v] = *reinterpret_cast<const float4*>(xs + ((pr + u) * NM_HC + 16 * g + pc + v) * NM_LD + 4 * c4);
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) {
-        const float* wr = wl + (4 * c4 + cc) * 16 * NC;
+        const float* wr = wl + (co * NM_CH + 4 * c4 + cc) * 16;
+        float wt[16];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float4 t4 = *reinterpret_cast<const float4*>(wr + 4 * q);
+          wt[4 * q] = t4.x; wt[4 * q + 1] = t4.y; wt[4 * q + 2] = t4.z; wt[4 * q + 3] = t4.w;
+        }
 #pragma unroll
         for (int ph = 0; ph < 2; ++ph)
 #pragma unroll
@@ -884,87 +1014,46 @@ __global__ __launch_bounds__(256) void convt2_narrow(NarrowArgs a) {
             for (int th = 0; th < 2; ++th)
 #pragma unroll
               for (int tw = 0; tw < 2; ++tw) {
-                // output (2i+ph, 2j+pw) <- input (i+ph-th, j+pw-tw) through tap (2th+1-ph, 2tw+1-pw)
-                const float4 xq = xv[ph - th + 1][pw - tw + 1];
-                const float xsv = cc == 0 ? xq.x : cc == 1 ? xq.y : cc == 2 ? xq.z : xq.w;
                 const int tap = (2 * th + 1 - ph) * 4 + (2 * tw + 1 - pw);
 #pragma unroll
-                for (int c = 0; c < NC; ++c)
-                  acc[ph * 2 + pw][c] = fmaf(xsv, wr[tap * NC + c], acc[ph * 2 + pw][c]);
+                for (int g = 0; g < 2; ++g) {
+                  const float4 xq = xv[g][ph - th + 1][pw - tw + 1];
+                  const float xa = cc == 0 ? xq.x : cc == 1 ? xq.y : cc == 2 ? xq.z : xq.w;
+                  acc[g][ph * 2 + pw] = __builtin_amdgcn_mfma_f32_4x4x1f32(xa, wt[tap], acc[g][ph * 2 + pw], 0, 0, 0);
+                }
               }
       }
     }
   }
-  if (i >= a.H || j >= a.W) return;
+  if (co >= NC) return;
   const float wsc = a.wscale ? a.wscale[0] : 1.f;
-  float* yb = a.y + (long long)b * a.ysb;
+  const float bv = a.bias ? a.bias[co] : 0.f;
+  float* yb = a.y + (long long)b * a.ysb + (long long)co * a.ysc;
+  const int blk = lane >> 2;  // this lane holds pixels 4 blk + i of each group, channel co
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const long long o = (long long)(2 * i + (q >> 1)) * a.ysh + (long long)(2 * j + (q & 1)) * a.ysw;
+  for (int g = 0; g < 2; ++g)
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const float v = acc[q][c] * wsc + (a.bias ? a.bias[c] : 0.f);
-      yb[o + (long long)c * a.ysc] = act_fwd(v, a.act, a.alpha);
+    for (int i = 0; i < 4; ++i) {
+      const int q = 4 * blk + i;  // pixel index within the group (lane order)
+      const int gi = r0 + 4 * wid + (q >> 4), gj = c0p + 16 * g + (q & 15);
+      if (gi >= a.H || gj >= a.W) continue;
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph)
+#pragma unroll
+        for (int pw = 0; pw < 2; ++pw)
+          yb[(long long)(2 * gi + ph) * a.ysh + (long long)(2 * gj + pw) * a.ysw] =
+              act_fwd(acc[g][ph * 2 + pw][i] * wsc + bv, a.act, a.alpha);
     }
-  }
 }
 
-constexpr int NARROW_CG = 32;  // output channels per thread in conv_narrow_in
-
-template <int CI>
-__global__ __launch_bounds__(256) void conv_narrow_in(NarrowArgs a) {
-  constexpr int KP = CI * 16;  // patch (ci, kh, kw) of a 4x4 kernel
-  const int HWo = a.Ho * a.Wo;
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= a.B * HWo) return;
-  const int b = idx / HWo, rem = idx - b * HWo, oh = rem / a.Wo, ow = rem - (rem / a.Wo) * a.Wo;
-  float patch[KP];
-  const float* xb = a.x + (long long)b * a.xsb;
-#pragma unroll
-  for (int ci = 0; ci < CI; ++ci)
-#pragma unroll
-    for (int kh = 0; kh < 4; ++kh)
-#pragma unroll
-      for (int kw = 0; kw < 4; ++kw) {
-        const int ih = oh * a.stride - a.pad + kh, iw = ow * a.stride - a.pad + kw;
-        patch[(ci * 4 + kh) * 4 + kw] =
-            ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
-                ? xb[(long long)ci * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
-                : 0.f;
-      }
-  const int co0 = blockIdx.y * NARROW_CG;
-  const float* __restrict__ wg = a.w + (size_t)co0 * KP;
-  const float wsc = a.wscale ? a.wscale[0] : 1.f;
-  float* yp = a.y + (long long)b * a.ysb + (long long)oh * a.ysh + (long long)ow * a.ysw;
-  const int ncg = min(NARROW_CG, a.Cout - co0);
-  float out[NARROW_CG];
-#pragma unroll
-  for (int c = 0; c < NARROW_CG; ++c) {
-    float s = 0.f;
-    if (c < ncg) {
-#pragma unroll
-      for (int k = 0; k < KP; ++k) s = fmaf(patch[k], wg[c * KP + k], s);
-    }
-    out[c] = act_fwd(s * wsc + (a.bias && c < ncg ? a.bias[co0 + c] : 0.f), a.act, a.alpha);
-  }
-  if (a.ysc == 1 && ncg == NARROW_CG && ((uintptr_t)(yp + co0) & 15) == 0) {
-#pragma unroll
-    for (int c = 0; c < NARROW_CG; c += 4)
-      *reinterpret_cast<float4*>(yp + co0 + c) = make_float4(out[c], out[c + 1], out[c + 2], out[c + 3]);
-  } else {
-#pragma unroll
-    for (int c = 0; c < NARROW_CG; ++c)
-      if (c < ncg) yp[(long long)(co0 + c) * a.ysc] = out[c];
-  }
-}
-
-// packed narrow-ConvT weights: out[ci][kh][kw][co] = W[ci * s_in + co * s_out + kh * 4 + kw]
+// packed narrow-ConvT weights [4][C][16]: out[co][ci][kh*4+kw] = W[ci * s_in + co * s_out + kh * 4 + kw]
+// (rows co >= NC are zero: the MFMA's fourth column)
 __global__ void pack_narrow(const float* __restrict__ W, float* __restrict__ out, int C, int NC, long long s_in,
                             long long s_out) {
   const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= C * 16 * NC) return;
-  const int co = e % NC, t = (e / NC) % 16, ci = e / (16 * NC);
-  out[e] = W[ci * s_in + co * s_out + t];
+  if (e >= 4 * C * 16) return;
+  const int t = e & 15, ci = (e >> 4) % C, co = e / (16 * C);
+  out[e] = co < NC ? W[ci * s_in + co * s_out + t] : 0.f;
 }
 
 // Tiled pack for the layouts whose columns are one weight index (n = out_idx) and whose
@@ -1174,7 +1263,7 @@ static bool plan_narrow_t(Plan& p, int batch, const float* x, const long long* x
   a.Ho = 2 * H; a.Wo = 2 * W; a.Cout = nc; a.stride = 2; a.pad = 1;
   a.bias = bias; a.wscale = wscale; a.act = act; a.alpha = alpha;
   p.pack = true;
-  p.pack_floats = (size_t)C * 16 * nc;
+  p.pack_floats = (size_t)4 * C * 16;
   p.pn_s_in = s_in; p.pn_s_out = s_out;
   p.pk.W = w;
   return true;
@@ -1424,15 +1513,15 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
                  bm[c], bn[c], wmv[c], wnv[c]);
         g_kernel_names[36 + m * 3 + c] = buf;
       }
-    g_kernel_names[45] = "void rgan::convt2_narrow<NC>(rgan::NarrowArgs)";
-    g_kernel_names[46] = "void rgan::conv_narrow_in<CI>(rgan::NarrowArgs)";
+    g_kernel_names[45] = "void rgan::convt2_narrow_mfma<NC>(rgan::NarrowArgs)";
+    g_kernel_names[46] = "void rgan::conv_narrow_in_mfma<CI>(rgan::NarrowArgs)";
   }
   return id;
 }
 
 static void launch_pack_plan(Plan& p, float* out, hipStream_t s) {
   if (p.mode == MODE_NARROW_T) {
-    const int n = p.na.C * 16 * p.na.Cout;
+    const int n = 4 * p.na.C * 16;
     pack_narrow<<<ceil_div(n, 256), 256, 0, s>>>(p.pk.W, out, p.na.C, p.na.Cout, p.pn_s_in, p.pn_s_out);
   } else {
     p.pk.out = out;
@@ -1444,20 +1533,20 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
   NarrowArgs a = p.na;
   if (p.mode == MODE_NARROW_T) {
     a.w = packed;
-    const int blocks = a.B * ceil_div(a.H, NT_T) * ceil_div(a.W, NT_T);
+    const int blocks = a.B * ceil_div(a.H, NM_TR) * ceil_div(a.W, NM_TC);
     switch (a.Cout) {
-      case 1: convt2_narrow<1><<<blocks, 256, 0, s>>>(a); break;
-      case 2: convt2_narrow<2><<<blocks, 256, 0, s>>>(a); break;
-      case 3: convt2_narrow<3><<<blocks, 256, 0, s>>>(a); break;
-      default: convt2_narrow<4><<<blocks, 256, 0, s>>>(a); break;
+      case 1: convt2_narrow_mfma<1><<<blocks, 256, 0, s>>>(a); break;
+      case 2: convt2_narrow_mfma<2><<<blocks, 256, 0, s>>>(a); break;
+      case 3: convt2_narrow_mfma<3><<<blocks, 256, 0, s>>>(a); break;
+      default: convt2_narrow_mfma<4><<<blocks, 256, 0, s>>>(a); break;
     }
   } else {
-    dim3 grid(ceil_div(a.B * a.Ho * a.Wo, 256), ceil_div(a.Cout, NARROW_CG));
+    dim3 grid(ceil_div(a.B * a.Ho * a.Wo, 128), ceil_div(a.Cout, 128));
     switch (a.C) {
-      case 1: conv_narrow_in<1><<<grid, 256, 0, s>>>(a); break;
-      case 2: conv_narrow_in<2><<<grid, 256, 0, s>>>(a); break;
-      case 3: conv_narrow_in<3><<<grid, 256, 0, s>>>(a); break;
-      default: conv_narrow_in<4><<<grid, 256, 0, s>>>(a); break;
+      case 1: conv_narrow_in_mfma<1><<<grid, 256, 0, s>>>(a); break;
+      case 2: conv_narrow_in_mfma<2><<<grid, 256, 0, s>>>(a); break;
+      case 3: conv_narrow_in_mfma<3><<<grid, 256, 0, s>>>(a); break;
+      default: conv_narrow_in_mfma<4><<<grid, 256, 0, s>>>(a); break;
     }
   }
   return 0;

@@ -147,6 +147,10 @@ def test_conv_narrow_paths(K, nc):
     for cache in (False, True):
         y = K.conv_fwd(img, wc, gc, bias=bc, act="lrelu", alpha=0.2, wscale=s, cache=cache)
         assert _rel(y, F.leaky_relu(_ref_conv(img, wc * 0.5, gc, bc), 0.2)) < 3e-6
+        if nc == 3:  # > 128 output channels: several channel tiles, the last one partial
+            wc2 = torch.randn(200, nc, 4, 4, device=DEV) * 0.1
+            y2 = K.conv_fwd(img, wc2, gc, act="lrelu", alpha=0.2)
+            assert _rel(y2, F.leaky_relu(_ref_conv(img, wc2, gc), 0.2)) < 3e-6
         dy = _nhwc(torch.randn(3, 40, 6, 6, device=DEV))
         dx = K.conv_dgrad(dy, wc, gc, img.shape, wscale=s, like=img, cache=cache)
         x64 = img.double().cpu().requires_grad_(True)
