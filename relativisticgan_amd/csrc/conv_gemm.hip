@@ -828,7 +828,12 @@ struct NarrowArgs {
 // 128 x K weight tile straight from torch layout ([co][ci][kh][kw] = [n][k], k-contiguous),
 // and runs K/2 MFMA steps per accumulator from k-contiguous LDS rows (row stride K+4 dwords,
 // an odd number of 16-B slots: conflict-free ds_read_b128; lane half h takes k in
-// [h K/2, (h+1) K/2)).  Epilogue: *wscale, +bias, activation, row offsets from an LDS table.
+// [h K/2, (h+1) K/2)).  Persistent over M tiles (next tile's im2col loads in flight during
+// this tile's MFMAs); the product is formed transposed (rows = channels) so the NHWC
+// epilogue is one float4 store per 4 channels.  Measured (C2 D image layer, 64x3x128^2 ->
+// 128 ch): 100 us as one VALU thread per pixel, 76 us here; without the stores 53 us --
+// fp32 MFMA and VALU share one issue pipe on gfx950, so the im2col/epilogue VALU is paid
+// in MFMA time.
 template <int CI>
 __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
   constexpr int K = CI * 16, KH2 = K / 2, LD = K + 4;
@@ -836,8 +841,9 @@ __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
   __shared__ __attribute__((aligned(16))) float Bs[128 * LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, lk = lane >> 5;
   const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
-  const int HWo = a.Ho * a.Wo, M = a.B * HWo;
-  const int m0 = blockIdx.x * 128, n0 = blockIdx.y * 128;
+  __shared__ long long moff[128];
+  const int HWo = a.Ho * a.Wo, M = a.B * HWo, tiles = (M + 127) / 128;
+  const int n0 = blockIdx.y * 128;
   {
     // all K/2 weight loads in flight before the first LDS store (a rolled loop would wait
     // on each load in turn: ~24 serialised L2 round trips per block)
@@ -853,9 +859,11 @@ __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
       Bs[r * LD + k] = wv[j];
     }
   }
-  {
-    const int row = tid >> 1, half = tid & 1, m = m0 + row;
-    float* dst = As + row * LD + half * KH2;
+  // im2col of one tile into registers: thread = (row tid/2, half tid%2 of the K columns)
+  const int row = tid >> 1, half = tid & 1;
+  float av[KH2];
+  auto gather = [&](int m0) {
+    const int m = m0 + row;
     if (m < M) {
       const int b = m / HWo, rem = m - b * HWo, oi = rem / a.Wo, oj = rem - oi * a.Wo;
       const int ih0 = oi * a.stride - a.pad, iw0 = oj * a.stride - a.pad;
@@ -863,67 +871,90 @@ __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
 #pragma unroll
       for (int kk = 0; kk < KH2; ++kk) {
         const int k = half * KH2 + kk, ci = k >> 4, ih = ih0 + ((k >> 2) & 3), iw = iw0 + (k & 3);
-        dst[kk] = ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
-                      ? xb[(long long)ci * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
-                      : 0.f;
+        av[kk] = ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                     ? xb[(long long)ci * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
+                     : 0.f;
       }
     } else {
 #pragma unroll
-      for (int kk = 0; kk < KH2; ++kk) dst[kk] = 0.f;
+      for (int kk = 0; kk < KH2; ++kk) av[kk] = 0.f;
     }
-  }
-  __syncthreads();
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  };
+  const float wsc = a.wscale ? a.wscale[0] : 1.f;
   const float* Ar = As + (wm + l32) * LD + lk * KH2;
   const float* Br = Bs + (wn + l32) * LD + lk * KH2;
+  // persistent over M tiles: the next tile's im2col loads are in flight during this tile's
+  // MFMAs and stores (one block per tile spent most of its life waiting on them)
+  int t = blockIdx.x;
+  if (t < tiles) gather(t * 128);
+  for (; t < tiles; t += gridDim.x) {
+    const int m0 = t * 128;
 #pragma unroll
-  for (int q = 0; q < KH2 / 4; ++q) {
-    float4 a4[2], b4[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      a4[t] = *reinterpret_cast<const float4*>(Ar + 32 * t * LD + 4 * q);
-      b4[t] = *reinterpret_cast<const float4*>(Br + 32 * t * LD + 4 * q);
-    }
-#pragma unroll
-    for (int s4 = 0; s4 < 4; ++s4)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[i][s4], b4[j][s4], acc[i][j], 0, 0, 0);
-  }
-  __syncthreads();  // As is reused for the row-offset table
-  long long* moff = reinterpret_cast<long long*>(As);
-  if (tid < 128) {
-    const int m = m0 + tid;
-    long long o = -1;
-    if (m < M) {
-      const int b = m / HWo, rem = m - b * HWo, oi = rem / a.Wo, oj = rem - oi * a.Wo;
-      o = (long long)b * a.ysb + (long long)oi * a.ysh + (long long)oj * a.ysw;
-    }
-    moff[tid] = o;
-  }
-  __syncthreads();
-  const float wsc = a.wscale ? a.wscale[0] : 1.f;
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = n0 + wn + 32 * j + l32;
-      if (col >= a.Cout) continue;
-      const float bv = a.bias ? a.bias[col] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const long long o = moff[wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk];
-        if (o >= 0) a.y[o + (long long)col * a.ysc] = act_fwd(acc[i][j][r] * wsc + bv, a.act, a.alpha);
+    for (int kk = 0; kk < KH2; ++kk) As[row * LD + half * KH2 + kk] = av[kk];
+    if (tid < 128) {
+      const int m = m0 + tid;
+      long long o = -1;
+      if (m < M) {
+        const int b = m / HWo, rem = m - b * HWo, oi = rem / a.Wo, oj = rem - oi * a.Wo;
+        o = (long long)b * a.ysb + (long long)oi * a.ysh + (long long)oj * a.ysw;
       }
+      moff[tid] = o;
     }
+    __syncthreads();
+    if (t + (int)gridDim.x < tiles) gather((t + gridDim.x) * 128);
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    // transposed product: rows = output channels (A = weights), columns = pixels (B =
+    // im2col), so each lane holds 4 consecutive channels of one pixel per register quad
+    // and the NHWC store is one float4
+#pragma unroll
+    for (int q = 0; q < KH2 / 4; ++q) {
+      float4 a4[2], b4[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        a4[u] = *reinterpret_cast<const float4*>(Ar + 32 * u * LD + 4 * q);
+        b4[u] = *reinterpret_cast<const float4*>(Br + 32 * u * LD + 4 * q);
+      }
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(b4[j][s4], a4[i][s4], acc[i][j], 0, 0, 0);
+    }
+    const bool vec4 = a.ysc == 1 && (a.Cout & 3) == 0;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long long o = moff[wm + 32 * i + l32];  // this lane's pixel
+      if (o < 0) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int cb = n0 + wn + 32 * j + 8 * g + 4 * lk;  // channels cb .. cb+3
+          if (cb >= a.Cout) continue;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[e] = act_fwd(acc[i][j][4 * g + e] * wsc + (a.bias && cb + e < a.Cout ? a.bias[cb + e] : 0.f), a.act,
+                           a.alpha);
+          if (vec4) {
+            *reinterpret_cast<float4*>(a.y + o + cb) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (cb + e < a.Cout) a.y[o + (long long)(cb + e) * a.ysc] = v[e];
+          }
+        }
+    }
+    __syncthreads();  // As / moff are rewritten for the next tile
+  }
 }
 
 // k4 s2 p1 ConvTranspose2d with NC <= 4 output channels on v_mfma_f32_4x4x1_16b_f32: 16
@@ -1541,7 +1572,8 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
       default: convt2_narrow_mfma<4><<<blocks, 256, 0, s>>>(a); break;
     }
   } else {
-    dim3 grid(ceil_div(a.B * a.Ho * a.Wo, 128), ceil_div(a.Cout, 128));
+    // persistent: two resident blocks per CU loop over the M tiles
+    dim3 grid(std::min(ceil_div(a.B * a.Ho * a.Wo, 128), 512), ceil_div(a.Cout, 128));
     switch (a.C) {
       case 1: conv_narrow_in_mfma<1><<<grid, 256, 0, s>>>(a); break;
       case 2: conv_narrow_in_mfma<2><<<grid, 256, 0, s>>>(a); break;

@@ -1,6 +1,6 @@
 """Build an experimental librgan variant with extra -D flags (GEMM tuning A/B runs).
 
-usage: python tools/build_variant.py NAME -DFOO=1 ...   -> relativisticgan_amd/build/variants/librgan_NAME.so
+usage: python tools/build_variant.py NAME -DFOO=1 ...   -> tools/variants/librgan_NAME.so (ships with gpurun)
 Run with RGAN_LIB=<that path> to load it instead of the in-tree library.
 """
 import os
@@ -14,7 +14,7 @@ import build as B  # noqa: E402
 
 def main():
     name, defs = sys.argv[1], sys.argv[2:]
-    out_dir = os.path.join(B.BUILD, "variants")
+    out_dir = os.path.join(ROOT, "tools", "variants")
     os.makedirs(out_dir, exist_ok=True)
     B.build()
     obj = os.path.join(out_dir, f"conv_gemm_{name}.o")
