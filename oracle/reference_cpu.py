@@ -478,6 +478,8 @@ class Trainer:
                 self.u.data.resize_(B, 1, 1, 1)
                 if feed:
                     self.u.data.copy_(feed["u"])
+                elif self.u.dtype != torch.float32:
+                    self.u.data.copy_(torch.empty(B, 1, 1, 1).uniform_(0, 1))
                 else:
                     self.u.uniform_(0, 1)
                 gp = gradient_penalty(D, self.x, self.x_fake, self.u, p.penalty, self.grad_outputs)
@@ -529,6 +531,8 @@ class Trainer:
     def _draw_z(self, B, feed, key):
         if feed:
             self.z.data.resize_(B, self.p.z_size, 1, 1).copy_(feed[key])
+        elif self.z.dtype != torch.float32:  # envelope runs: the fp32 draws, cast
+            self.z.data.resize_(B, self.p.z_size, 1, 1).copy_(torch.empty(B, self.p.z_size, 1, 1).normal_(0, 1))
         else:
             self.z.data.resize_(B, self.p.z_size, 1, 1).normal_(0, 1)
 
