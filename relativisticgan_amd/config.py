@@ -4,8 +4,9 @@ Plus this build's own switches (prefixed ``--rgan_``), which the reference lacks
 ``--rgan_rng`` (``host``: draw z/u/batches from the CPU generators in the reference's
 order, bit-compatible inputs; ``device``: draw on the GPU, for throughput runs) and
 ``--rgan_sync_bn`` (SyncBN under data parallelism, default on; off = the reference
-DataParallel's per-shard statistics) and ``--rgan_pac 2`` (the PacGAN-2 script,
-code/GAN_losses_iter_PAC.py, which shares this CLI).
+DataParallel's per-shard statistics), ``--rgan_pac 2`` (the PacGAN-2 script,
+code/GAN_losses_iter_PAC.py, which shares this CLI) and ``--rgan_script`` (the defaults of
+GAN_losses_iter / GAN_losses_iter_art / GAN_losses_iter_PAC).
 """
 import argparse
 
@@ -32,17 +33,34 @@ _FLAGS = [
 ]
 
 
-def make_parser():
+# code/GAN_losses_iter_art.py is GLI with these defaults (its only differences, art:20-60)
+ART_DEFAULTS = {
+    "image_size": 128, "loss_D": 7, "gen_extra_images": 2000, "gen_every": 2000,
+    "input_folder": "/home/ubuntu/datasets/meow_128x128", "output_folder": "/home/ubuntu/RelativisticGAN/output",
+    "inception_folder": "/home/ubuntu/models/Inception", "extra_folder": "/home/ubuntu/RelativisticGAN/extra",
+    "CIFAR10_input_folder": "/home/ubuntu/datasets/CIFAR10",
+}
+SCRIPTS = ("GAN_losses_iter", "GAN_losses_iter_art", "GAN_losses_iter_PAC")
+
+
+def make_parser(script="GAN_losses_iter"):
+    """The CLI of one of the reference's three training scripts (same flags; the art script
+    changes defaults, the PAC script packs 2 samples for D)."""
     p = argparse.ArgumentParser(description="RelativisticGAN training (MI355X build)")
     p.register("type", "bool", str_to_bool)
     for name, typ, default in _FLAGS:
+        if script == "GAN_losses_iter_art":
+            default = ART_DEFAULTS.get(name, default)
         if typ is str:
             p.add_argument("--" + name, default=default)
         else:
             p.add_argument("--" + name, type=typ, default=default)
+    p.add_argument("--rgan_script", choices=SCRIPTS, default=script,
+                   help="which reference script's defaults/behaviour to follow")
     p.add_argument("--rgan_rng", choices=("host", "device"), default="host")
     p.add_argument("--rgan_sync_bn", type="bool", default=True)
-    p.add_argument("--rgan_pac", dest="pac", type=int, default=1, choices=(1, 2),
+    p.add_argument("--rgan_pac", dest="pac", type=int, default=2 if script == "GAN_losses_iter_PAC" else 1,
+                   choices=(1, 2),
                    help="2 = PacGAN-2, the reference's code/GAN_losses_iter_PAC.py (D sees 2 samples packed "
                         "channel-wise)")
     p.add_argument("--rgan_synthetic", type=int, default=0,
@@ -51,7 +69,10 @@ def make_parser():
 
 
 def parse(argv=None):
-    return make_parser().parse_args(argv)
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--rgan_script", choices=SCRIPTS, default="GAN_losses_iter")
+    script = pre.parse_known_args(argv)[0].rgan_script
+    return make_parser(script).parse_args(argv)
 
 
 def make_param(**overrides):

@@ -97,6 +97,17 @@ def test_nets_state_dict_and_init_match_reference(name):
                 assert sha == bytes(g[full + "@sha1"]).decode(), k
 
 
+def test_cli_script_profiles():
+    """--rgan_script: the art script is GLI with other defaults (art:20-60), PAC packs 2."""
+    from relativisticgan_amd.config import parse
+    art = parse(["--rgan_script", "GAN_losses_iter_art"])
+    assert (art.image_size, art.loss_D, art.gen_every, art.gen_extra_images, art.pac) == (128, 7, 2000, 2000, 1)
+    assert parse(["--rgan_script", "GAN_losses_iter_art", "--loss_D", "6"]).loss_D == 6
+    assert parse(["--rgan_script", "GAN_losses_iter_PAC"]).pac == 2
+    gli = parse([])
+    assert (gli.image_size, gli.loss_D, gli.pac) == (64, 1, 1)
+
+
 ORDER_CASES = list(CONFIGS) + ["arch1_spectral"]
 
 
