@@ -34,7 +34,7 @@ constexpr int OOB = (int)0x80000000;
 // fast-path tensors must fit a buffer descriptor with this margin
 constexpr long long FAST_MAX_BYTES = (1LL << 31) - (1LL << 24);
 
-enum { MODE_CONV = 0, MODE_CONVT2 = 1, MODE_WGRAD = 2, MODE_NARROW_T = 3, MODE_NARROW_IN = 4 };
+enum { MODE_CONV = 0, MODE_CONVT2 = 1, MODE_WGRAD = 2, MODE_NARROW_T = 3, MODE_NARROW_IN = 4, MODE_DENSE1 = 5 };
 constexpr int BK = 32;
 
 // n / d for 0 <= n < 2^31 via multiply-high (host-computed magic numbers)
@@ -733,23 +733,198 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
     }
 }
 
-template <int MODE>
-__global__ void splitk_reduce(GemmArgs g, int phases) {
-  const size_t MN = (size_t)g.M * g.N;
-  const size_t total = MN * phases;
-  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total;
-       idx += (size_t)gridDim.x * blockDim.x) {
-    const int phase = (int)(idx / MN);
-    const size_t e = idx - (size_t)phase * MN;
-    const int m = (int)(e / g.N), n = (int)(e - (size_t)m * g.N);
-    const float* s = g.slab + (size_t)phase * g.splits * MN + e;
-    float v = 0.f;
-    for (int sp = 0; sp < g.splits; ++sp) v += s[(size_t)sp * MN];
-    if (g.wscale) v *= g.wscale[0];
-    if (g.bias) v += g.bias[n];
-    g.C[row_offset(g.out, m, MODE == MODE_CONVT2 ? phase : 0) + col_offset(g.out, n)] =
-        act_fwd(v, g.act, g.alpha);
+// Split-K reduce: out = act(sum_sp slab[sp] * wscale + bias), slabs summed in split order
+// (deterministic; loads issued 4 splits ahead of the adds).  Three shapes, chosen on the
+// host:
+//  RED_VEC  channel-contiguous outputs (tc == 1, 16-B aligned): one thread per (phase, m,
+//           4 consecutive n), float4 loads and stores;
+//  RED_TAPS torch weight layout (WGRAD, n = (kh, kw, c) over a 4x4 kernel, out[m][c][kh][kw]):
+//           one thread per (m, c, 4 taps), 4 taps of a channel = one float4 store (lanes on
+//           consecutive tap quads write contiguously);
+//  RED_ANY  anything else, one element per thread.
+enum { RED_ANY = 0, RED_VEC = 1, RED_TAPS = 2 };
+
+__device__ __forceinline__ float red_epi(const GemmArgs& g, float v, float wsc, int n) {
+  v *= wsc;
+  if (g.bias) v += g.bias[n];
+  return act_fwd(v, g.act, g.alpha);
+}
+
+// sum over splits of V-wide vectors at s + sp * stride, in split order
+template <int V>
+__device__ __forceinline__ void red_sum(const float* s, size_t stride, int splits, float (&v)[V]) {
+  float t[4][V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) v[i] = 0.f;
+  int sp = 0;
+  for (; sp + 4 <= splits; sp += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if constexpr (V == 4) {
+        const float4 q = *reinterpret_cast<const float4*>(s + (size_t)(sp + u) * stride);
+        t[u][0] = q.x; t[u][1] = q.y; t[u][2] = q.z; t[u][3] = q.w;
+      } else {
+#pragma unroll
+        for (int i = 0; i < V; ++i) t[u][i] = s[(size_t)(sp + u) * stride + i];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < V; ++i) v[i] = sp + u == 0 ? t[u][i] : v[i] + t[u][i];
   }
+  for (; sp < splits; ++sp)
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = sp == 0 ? s[(size_t)sp * stride + i] : v[i] + s[(size_t)sp * stride + i];
+}
+
+template <int MODE, int KIND>
+__global__ __launch_bounds__(256) void splitk_reduce(GemmArgs g, FastDiv fdiv, uint32_t per_phase) {
+  const int phase = blockIdx.y;
+  const size_t MN = (size_t)g.M * g.N;
+  const float* base = g.slab + (size_t)phase * g.splits * MN;
+  // the unsplit epilogue computes acc * wsc + bias; wsc = 1 multiplies exactly
+  const float wsc = g.wscale ? g.wscale[0] : 1.f;
+  for (uint32_t idx = blockIdx.x * 256u + threadIdx.x; idx < per_phase; idx += gridDim.x * 256u) {
+    if constexpr (KIND == RED_VEC) {
+      const uint32_t m = fdiv.div(idx);               // fdiv = N / 4
+      const int n = 4 * (int)(idx - m * fdiv.d);
+      float v[4];
+      red_sum<4>(base + (size_t)m * g.N + n, MN, g.splits, v);
+      const float4 o = make_float4(red_epi(g, v[0], wsc, n), red_epi(g, v[1], wsc, n + 1),
+                                   red_epi(g, v[2], wsc, n + 2), red_epi(g, v[3], wsc, n + 3));
+      *reinterpret_cast<float4*>(g.C + row_offset(g.out, (int)m, MODE == MODE_CONVT2 ? phase : 0) +
+                                 col_offset(g.out, n)) = o;
+    } else if constexpr (KIND == RED_TAPS) {
+      const uint32_t mc = idx >> 2;                   // fdiv = channels c
+      const int q = (int)(idx & 3);                   // taps 4q .. 4q+3 (kh = q)
+      const uint32_t m = fdiv.div(mc);
+      const int c = (int)(mc - m * fdiv.d);
+      const float* s = base + (size_t)m * g.N + c;
+      const int nc = (int)fdiv.d;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float w[1];
+        red_sum<1>(s + (size_t)(4 * q + i) * nc, MN, g.splits, w);
+        v[i] = red_epi(g, w[0], wsc, (4 * q + i) * nc + c);
+      }
+      *reinterpret_cast<float4*>(g.C + (long long)m * g.out.sb + (long long)c * 16 + 4 * q) =
+          make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      const uint32_t m = fdiv.div(idx);               // fdiv = N
+      const int n = (int)(idx - m * fdiv.d);
+      float v[1];
+      red_sum<1>(base + (size_t)m * g.N + n, MN, g.splits, v);
+      g.C[row_offset(g.out, (int)m, MODE == MODE_CONVT2 ? phase : 0) + col_offset(g.out, n)] =
+          red_epi(g, v[0], wsc, n);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- one-output dense layer
+// D's closing Conv2d(C, 1, k, 1, 0) over a k x k map (GLI:455, GLI:306) covers the whole
+// map: per sample a dot product of C*k*k inputs with the single filter.  As an implicit GEMM
+// it is N = 1 (one 32-wide tile column, 1/32 used, split-K 256 ways); here:
+//   fwd   one block per sample, y[b] = act(wsc * <x[b], W> + bias)  (fixed-order block sum)
+//   dgrad dx[b][e] = (dy[b] * W[e]) * wsc                            (elementwise, NHWC stores)
+//   wgrad dW[e] = sum_b dy[b] * x[b][e], b in order                  (thread per filter tap)
+// e runs over (h, w, c) with c fastest, so NHWC activations are read/written coalesced; fwd
+// and dgrad read the filter packed in the same order (the conv forward pack, [1][(kh,kw,ci)]),
+// wgrad writes it in torch order c*k*k + h*k + w.
+struct DenseArgs {
+  const float* x;             // fwd/wgrad: input.  dgrad: unused
+  long long xsb, xsc, xsh, xsw;
+  const float* w;
+  const float* wscale;
+  const float* bias;
+  float* y;                   // fwd: output [b * ysb].  dgrad/wgrad: dy (read)
+  long long ysb;
+  float* out;                 // dgrad: dx (strides xs*).  wgrad: dW (torch layout)
+  int B, C, HW, E;            // E = C * HW
+  FastDiv fc, fw;             // e -> (hw, c); hw -> (h, w)
+  int act;
+  float alpha;
+  int vec;
+};
+
+__device__ __forceinline__ long long dense_x_off(const DenseArgs& a, int e, int& widx) {
+  const uint32_t hw = a.fc.div(e);
+  const int c = e - (int)(hw * a.fc.d);
+  const uint32_t h = a.fw.div(hw);
+  const int w = (int)(hw - h * a.fw.d);
+  widx = c * a.HW + (int)hw;
+  return (long long)c * a.xsc + (long long)h * a.xsh + (long long)w * a.xsw;
+}
+
+// VEC (host-checked: channel stride 1, C % 4 == 0, 16-B aligned rows): thread items are
+// channel quads, one float4 of activations + 4 filter taps.
+// VEC (host-checked: channel stride 1, C % 4 == 0, 16-B aligned rows): thread items are
+// channel quads, one float4 of activations and one of packed filter.
+template <bool VEC>
+__global__ __launch_bounds__(1024) void dense1_fwd(DenseArgs a) {
+  __shared__ float red[16];
+  const int b = blockIdx.x;
+  const float* xb = a.x + (long long)b * a.xsb;
+  float acc = 0.f;
+  if constexpr (VEC) {
+#pragma unroll 8
+    for (int e = 4 * threadIdx.x; e < a.E; e += 4 * 1024) {
+      int wi;
+      const float4 xv = *reinterpret_cast<const float4*>(xb + dense_x_off(a, e, wi));
+      const float4 wv = *reinterpret_cast<const float4*>(a.w + e);
+      acc = fmaf(xv.x, wv.x, acc);
+      acc = fmaf(xv.y, wv.y, acc);
+      acc = fmaf(xv.z, wv.z, acc);
+      acc = fmaf(xv.w, wv.w, acc);
+    }
+  } else {
+#pragma unroll 8
+    for (int e = threadIdx.x; e < a.E; e += 1024) {
+      int wi;
+      const long long xo = dense_x_off(a, e, wi);
+      acc = fmaf(xb[xo], a.w[e], acc);
+    }
+  }
+  const float t = block_sum(acc, red);
+  if (threadIdx.x == 0) {
+    const float wsc = a.wscale ? a.wscale[0] : 1.f;
+    const float v = t * wsc + (a.bias ? a.bias[0] : 0.f);
+    a.y[(long long)b * a.ysb] = act_fwd(v, a.act, a.alpha);
+  }
+}
+
+// fe = E / (VEC ? 4 : 1): item -> (b, e)
+template <bool VEC>
+__global__ __launch_bounds__(256) void dense1_dgrad(DenseArgs a, FastDiv fe) {
+  const uint32_t total = (uint32_t)a.B * fe.d;
+  const float wsc = a.wscale ? a.wscale[0] : 1.f;
+  for (uint32_t idx = blockIdx.x * 256u + threadIdx.x; idx < total; idx += gridDim.x * 256u) {
+    const uint32_t b = fe.div(idx);
+    const int e = (int)(idx - b * fe.d) * (VEC ? 4 : 1);
+    int wi;
+    const long long xo = dense_x_off(a, e, wi);
+    const float g = a.y[(long long)b * a.ysb];
+    float* o = a.out + (long long)b * a.xsb + xo;
+    if constexpr (VEC) {
+      const float4 wv = *reinterpret_cast<const float4*>(a.w + e);
+      *reinterpret_cast<float4*>(o) = make_float4((g * wv.x) * wsc, (g * wv.y) * wsc, (g * wv.z) * wsc,
+                                                  (g * wv.w) * wsc);
+    } else {
+      *o = (g * a.w[e]) * wsc;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void dense1_wgrad(DenseArgs a) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.E) return;
+  int wi;
+  const long long xo = dense_x_off(a, e, wi);
+  float acc = 0.f;
+#pragma unroll 16
+  for (int b = 0; b < a.B; ++b) acc = fmaf(a.y[(long long)b * a.ysb], a.x[(long long)b * a.xsb + xo], acc);
+  a.out[wi] = acc;
 }
 
 // ---------------------------------------------------------------- weight packing
@@ -1140,6 +1315,9 @@ struct Plan {
   // narrow kernels (MODE_NARROW_T / MODE_NARROW_IN)
   NarrowArgs na{};
   long long pn_s_in = 0, pn_s_out = 0;  // narrow pack strides
+  // one-output dense layer (MODE_DENSE1): which = 0 fwd, 1 dgrad, 2 wgrad
+  DenseArgs da{};
+  int dense_op = 0;
 };
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
@@ -1315,6 +1493,31 @@ static bool plan_narrow_in(Plan& p, const RganConv* d, const float* x, const flo
   return true;
 }
 
+// Conv2d(C, 1, k, 1, 0) over exactly a k x k map (x strides d->xs; y / dy at b * ys[0])
+static bool plan_dense1(Plan& p, const RganConv* d, int op, const float* x, const float* w, const float* wscale,
+                        const float* bias, float* y, float* out, int act, float alpha) {
+  if (d->transposed || d->cout != 1 || d->hout != 1 || d->wout != 1 || d->pad != 0 || d->kh != d->hin ||
+      d->kw != d->win)
+    return false;
+  if ((long long)d->batch * d->cin * d->hin * d->win >= (1LL << 31)) return false;
+  p.mode = MODE_DENSE1;
+  p.dense_op = op;
+  p.pack = false;
+  if (op != 2) {
+    // filter packed in e order: Wp[(kh,kw,ci)] = W[0][ci][kh][kw] (the conv forward pack)
+    const int KK = d->kh * d->kw;
+    set_pack(p, w, wscale, KK * d->cin, 1, d->cin, d->kw, 1, 1, KK, (long long)d->cin * KK, d->kw, 1, d->kh,
+             d->kw, 0, 0);
+  }
+  DenseArgs& a = p.da;
+  a.x = x; a.xsb = d->xs[0]; a.xsc = d->xs[1]; a.xsh = d->xs[2]; a.xsw = d->xs[3];
+  a.w = w; a.wscale = wscale; a.bias = bias; a.y = y; a.ysb = d->ys[0]; a.out = out;
+  a.B = d->batch; a.C = d->cin; a.HW = d->hin * d->win; a.E = a.C * a.HW;
+  a.fc = FastDiv(d->cin); a.fw = FastDiv(d->win);
+  a.act = act; a.alpha = alpha;
+  return true;
+}
+
 // forward GEMM over the conv's input x producing y (conv or transposed conv)
 static int plan_fwd(const RganConv* d, const float* x, const float* w, const float* wscale,
                     const float* bias, float* y, int act, float alpha, Plan& p) {
@@ -1326,6 +1529,7 @@ static int plan_fwd(const RganConv* d, const float* x, const float* w, const flo
                     wscale, bias, act, alpha))
     return 0;
   if (plan_narrow_in(p, d, x, w, wscale, bias, y, act, alpha)) return 0;
+  if (plan_dense1(p, d, 0, x, w, wscale, bias, y, nullptr, act, alpha)) return 0;
   g.a = make_img(x, d->hin, d->win, d->cin, d->xs);
   g.C = y; g.bias = bias; g.act = act; g.alpha = alpha;
   if (!d->transposed) {
@@ -1391,6 +1595,17 @@ static int plan_dgrad(const RganConv* d, const float* dy, const float* w, const 
       plan_narrow_t(p, d->batch, dy, d->ys, d->hout, d->wout, d->cout, w, (long long)d->cin * 16, 16, d->cin, dx,
                     d->xs, wscale, nullptr, RGAN_ACT_NONE, 0.f))
     return 0;
+  if (plan_dense1(p, d, 1, nullptr, w, wscale, nullptr, const_cast<float*>(dy), dx, RGAN_ACT_NONE, 0.f)) return 0;
+  // ConvT k4 s2 p1 with <= 4 outputs (G's image layer): its dgrad is a Conv2d over the
+  // image with <= 4 input channels, W[ci][co] read as [out=ci][in=co] -- the narrow-in kernel
+  if (d->transposed && is_k4s2p1(d) && d->hout == 2 * d->hin && d->wout == 2 * d->win) {
+    RganConv c = *d;
+    c.transposed = 0;
+    c.cin = d->cout; c.hin = d->hout; c.win = d->wout;
+    c.cout = d->cin; c.hout = d->hin; c.wout = d->win;
+    for (int i = 0; i < 4; ++i) { c.xs[i] = d->ys[i]; c.ys[i] = d->xs[i]; }
+    if (plan_narrow_in(p, &c, dy, w, wscale, nullptr, dx, RGAN_ACT_NONE, 0.f)) return 0;
+  }
   g.a = make_img(dy, d->hout, d->wout, d->cout, d->ys);
   g.C = dx; g.bias = nullptr; g.act = RGAN_ACT_NONE; g.alpha = 0.f;
   g.out = make_out(d->hin, d->win, 1, d->xs[0], d->xs[2], d->xs[3], 1, 1, d->cin, 0, 0, d->xs[1]);
@@ -1437,6 +1652,7 @@ static int plan_dgrad(const RganConv* d, const float* dy, const float* w, const 
 // weight gradient, written in torch weight layout
 static int plan_wgrad(const RganConv* d, const float* x, const float* dy, float* dw, Plan& p) {
   if (!desc_ok(d)) return RGAN_EINVAL;
+  if (plan_dense1(p, d, 2, x, nullptr, nullptr, nullptr, const_cast<float*>(dy), dw, RGAN_ACT_NONE, 0.f)) return 0;
   GemmArgs& g = p.g;
   const int KK = d->kh * d->kw;
   p.mode = MODE_WGRAD;
@@ -1518,11 +1734,12 @@ static std::vector<ProfRec> g_recs;
 static std::vector<std::string> g_kernel_names;
 static double g_cur_flops = 0.0;
 
-constexpr int N_KERNEL_IDS = 47;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow
+constexpr int N_KERNEL_IDS = 50;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense
 
 static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
   const int id = mode == MODE_NARROW_T ? 45
                  : mode == MODE_NARROW_IN ? 46
+                 : mode == MODE_DENSE1 ? 47 + cfg
                  : fast ? 36 + mode * 3 + cfg
                         : ((mode * 3 + cfg) * 2 + (av ? 1 : 0)) * 2 + (bv ? 1 : 0);
   if (g_kernel_names.empty()) {
@@ -1546,6 +1763,9 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
       }
     g_kernel_names[45] = "void rgan::convt2_narrow_mfma<NC>(rgan::NarrowArgs)";
     g_kernel_names[46] = "void rgan::conv_narrow_in_mfma<CI>(rgan::NarrowArgs)";
+    g_kernel_names[47] = "void rgan::dense1_fwd<VEC>(rgan::DenseArgs)";
+    g_kernel_names[48] = "void rgan::dense1_dgrad<VEC>(rgan::DenseArgs, rgan::FastDiv)";
+    g_kernel_names[49] = "rgan::dense1_wgrad(rgan::DenseArgs)";
   }
   return id;
 }
@@ -1584,9 +1804,29 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
   return 0;
 }
 
+static void run_dense1(const Plan& p, const float* packed, hipStream_t s) {
+  DenseArgs a = p.da;
+  if (p.dense_op != 2) a.w = packed;
+  if (p.dense_op != 2) {
+    const float* t = p.dense_op == 0 ? a.x : a.out;
+    a.vec = a.xsc == 1 && a.C % 4 == 0 && a.xsb % 4 == 0 && a.xsh % 4 == 0 && a.xsw % 4 == 0 && aligned16(t);
+  }
+  if (p.dense_op == 0) {
+    if (a.vec) dense1_fwd<true><<<a.B, 1024, 0, s>>>(a);
+    else dense1_fwd<false><<<a.B, 1024, 0, s>>>(a);
+  } else if (p.dense_op == 1) {
+    const uint32_t per = a.vec ? a.E / 4 : a.E, total = (uint32_t)a.B * per;
+    const unsigned blocks = std::min<uint32_t>((total + 255) / 256, 8192);
+    if (a.vec) dense1_dgrad<true><<<blocks, 256, 0, s>>>(a, FastDiv(per));
+    else dense1_dgrad<false><<<blocks, 256, 0, s>>>(a, FastDiv(per));
+  } else {
+    dense1_wgrad<<<ceil_div(a.E, 256), 256, 0, s>>>(a);
+  }
+}
+
 static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   if (ws_bytes < plan_ws_bytes(p)) return RGAN_EINVAL;
-  if (p.mode == MODE_NARROW_T || p.mode == MODE_NARROW_IN) {
+  if (p.mode == MODE_NARROW_T || p.mode == MODE_NARROW_IN || p.mode == MODE_DENSE1) {
     const float* packed = p.prepacked;
     if (p.pack && !packed) {
       if (!ws) return RGAN_EINVAL;
@@ -1600,10 +1840,11 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
       rec.a = g_pool[g_recs.size() * 2];
       rec.b = g_pool[g_recs.size() * 2 + 1];
       rec.flops = g_cur_flops;
-      rec.kid = kernel_id(p.mode, 0, false, false);
+      rec.kid = kernel_id(p.mode, p.mode == MODE_DENSE1 ? p.dense_op : 0, false, false);
       hipEventRecord(rec.a, s);
     }
-    run_narrow(p, packed, s);
+    if (p.mode == MODE_DENSE1) run_dense1(p, packed, s);
+    else run_narrow(p, packed, s);
     RGAN_CHECK_LAUNCH();
     if (prof) {
       hipEventRecord(rec.b, s);
@@ -1647,13 +1888,36 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     g_recs.push_back(rec);
   }
   if (p.g.splits > 1) {
-    const size_t total = (size_t)p.g.M * p.g.N * p.phases;
-    const int blocks = (int)std::min<size_t>((total + 255) / 256, 8192);
-    switch (p.mode) {
-      case MODE_CONV: splitk_reduce<MODE_CONV><<<blocks, 256, 0, s>>>(p.g, p.phases); break;
-      case MODE_CONVT2: splitk_reduce<MODE_CONVT2><<<blocks, 256, 0, s>>>(p.g, p.phases); break;
-      default: splitk_reduce<MODE_WGRAD><<<blocks, 256, 0, s>>>(p.g, p.phases); break;
+    const GemmArgs& g = p.g;
+    const OutMap& o = g.out;
+    auto al4 = [](long long v) { return (v & 3) == 0; };
+    int kind = RED_ANY;
+    uint32_t per = (uint32_t)g.M * g.N, d = g.N;
+    if (p.mode != MODE_WGRAD && o.tc == 1 && o.fnc.d % 4 == 0 && g.N % 4 == 0 && al4(o.th) &&
+        al4(o.tw) && al4(o.sb) && al4(o.sh) && al4(o.sw) && ((uintptr_t)g.C & 15) == 0) {
+      kind = RED_VEC;
+      per /= 4;
+      d = g.N / 4;
+    } else if (p.mode == MODE_WGRAD && o.fnkw.d == 4 && (uint32_t)g.N == 16 * o.fnc.d && o.th == 4 &&
+               o.tw == 1 && o.tc == 16 && al4(o.sb) && ((uintptr_t)g.C & 15) == 0) {
+      kind = RED_TAPS;
+      per /= 4;
+      d = o.fnc.d;
     }
+    const dim3 rgrid((unsigned)std::min<uint32_t>((per + 255) / 256, 8192), p.phases);
+    const FastDiv fd(d);
+#define RGAN_RED(MD)                                                                   \
+  switch (kind) {                                                                      \
+    case RED_VEC: splitk_reduce<MD, RED_VEC><<<rgrid, 256, 0, s>>>(g, fd, per); break;  \
+    case RED_TAPS: splitk_reduce<MD, RED_TAPS><<<rgrid, 256, 0, s>>>(g, fd, per); break; \
+    default: splitk_reduce<MD, RED_ANY><<<rgrid, 256, 0, s>>>(g, fd, per); break;       \
+  }
+    switch (p.mode) {
+      case MODE_CONV: RGAN_RED(MODE_CONV) break;
+      case MODE_CONVT2: RGAN_RED(MODE_CONVT2) break;
+      default: RGAN_RED(MODE_WGRAD) break;
+    }
+#undef RGAN_RED
     RGAN_CHECK_LAUNCH();
   }
   return 0;
@@ -1710,6 +1974,7 @@ extern "C" int rgan_conv_fwd(const RganConv* d, const float* x, const float* w, 
   Plan p;
   int rc = plan_fwd(d, x, w, wscale, bias, y, act, act_alpha, p);
   if (rc) return rc;
+  if (!p.pack && !w) return RGAN_EINVAL;  // kernels that read the torch layout
   p.prepacked = wpacked;
   return run_plan(p, ws, ws_bytes, (hipStream_t)stream);
 }
@@ -1721,6 +1986,7 @@ extern "C" int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* 
   Plan p;
   int rc = plan_dgrad(d, dy, w, wscale, dx, p);
   if (rc) return rc;
+  if (!p.pack && !w) return RGAN_EINVAL;  // kernels that read the torch layout
   p.prepacked = wpacked;
   return run_plan(p, ws, ws_bytes, (hipStream_t)stream);
 }

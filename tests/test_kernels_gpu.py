@@ -128,6 +128,37 @@ def test_conv_bias_act(K):
     assert _rel(db, dy.double().sum((0, 2, 3))) < 1e-6
 
 
+@pytest.mark.parametrize("case", [(64, 2048, 4, "nhwc"), (3, 20, 5, "nhwc"), (5, 7, 3, "nchw"), (1, 1, 1, "nchw")])
+def test_conv_dense_one_output(K, case):
+    """D's closing Conv2d(C, 1, k, 1, 0) over a k x k map (dense1 kernels): fwd with bias,
+    wscale and activation, dgrad with wscale, wgrad + dbias, vs torch fp64."""
+    B, C, k, layout = case
+    g = K.ConvGeom(k, 1, 0, False)
+    torch.manual_seed(k)
+    x = torch.randn(B, C, k, k, device=DEV)
+    if layout == "nhwc":
+        x = _nhwc(x)
+    w = torch.nn.Parameter(torch.randn(1, C, k, k, device=DEV) * 0.1)
+    b = torch.randn(1, device=DEV)
+    ws = torch.tensor([0.7], device=DEV)
+    ref = F.conv2d(x.double().cpu(), w.detach().double().cpu() * 0.7, b.double().cpu())
+    for act, fn in [("none", lambda t: t), ("sigmoid", torch.sigmoid), ("lrelu", lambda t: F.leaky_relu(t, 0.2))]:
+        for cache in (False, True):
+            y = K.conv_fwd(x, w, g, bias=b, act=act, alpha=0.2, wscale=ws, cache=cache)
+            assert y.shape == (B, 1, 1, 1)
+            assert _rel(y, fn(ref)) < 3e-6, (act, cache)
+    dy = torch.randn(B, 1, 1, 1, device=DEV)
+    x64 = x.double().cpu().requires_grad_(True)
+    w64 = w.detach().double().cpu().requires_grad_(True)
+    F.conv2d(x64, w64).backward(dy.double().cpu())
+    dx = K.conv_dgrad(dy, w, g, x.shape, wscale=ws, like=x)
+    assert dx.stride() == x.stride()
+    assert _rel(dx, x64.grad * 0.7) < 2e-6
+    dw, db = K.conv_wgrad(x, dy, g, w.shape, with_bias=True)
+    assert _rel(dw, w64.grad) < 2e-6
+    assert _rel(db, dy.double().cpu().sum((0, 2, 3))) < 1e-6
+
+
 @pytest.mark.parametrize("nc", [1, 2, 3, 4])
 def test_conv_narrow_paths(K, nc):
     """Narrow kernels: ConvT k4s2p1 with nc outputs (and the Conv2d dgrad of that shape),
@@ -141,6 +172,12 @@ def test_conv_narrow_paths(K, nc):
     for cache in (False, True, True):
         y = K.conv_fwd(x, w, gt, bias=b, act="tanh", wscale=s, nchw_out=True, cache=cache)
         assert _rel(y, torch.tanh(_ref_conv(x, w * 0.5, gt, b))) < 3e-6
+    # the ConvT's dgrad (a Conv2d over the nc-channel image: narrow-in kernel), NCHW image grad
+    gy = torch.randn(3, nc, 12, 12, device=DEV)
+    x64 = x.double().cpu().requires_grad_(True)
+    F.conv_transpose2d(x64, (w * 0.5).detach().double().cpu(), stride=2, padding=1).backward(gy.double().cpu())
+    for cache in (False, True):
+        assert _rel(K.conv_dgrad(gy, w, gt, x.shape, wscale=s, cache=cache), x64.grad) < 3e-6
     img = torch.randn(3, nc, 12, 12, device=DEV)
     wc = torch.nn.Parameter(torch.randn(40, nc, 4, 4, device=DEV) * 0.1)
     bc = torch.randn(40, device=DEV)
