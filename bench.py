@@ -112,6 +112,8 @@ def main():
     ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="SyncBN over ranks (default: per-shard BN = the reference's DataParallel)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -124,7 +126,7 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        dp.setup(sync_bn=True)
+        dp.setup(sync_bn=args.sync_bn)
     loss_D, size, bpg, h = WORKLOADS[args.workload]
     spectral = args.workload == "C5"
     p = make_param(loss_D=loss_D, image_size=size, batch_size=bpg * world, G_h_size=h, D_h_size=h, seed=1,
@@ -181,7 +183,8 @@ def main():
         "config": {"workload": f"{args.workload}: loss_D {loss_D} DCGAN arch0 {size}x{size}, h={h}, "
                                f"batch {bpg}/GPU{', spectral D' if spectral else ''}",
                    "loss_D": loss_D, "image_size": size, "batch_per_gpu": bpg, "global_batch": bpg * world,
-                   "G_h_size": h, "D_h_size": h, "parallelism": f"dp{world}"},
+                   "G_h_size": h, "D_h_size": h, "parallelism": f"dp{world}",
+                   "batchnorm": "SyncBN" if args.sync_bn else "per-shard (reference DataParallel)"},
         "step_mfma_util": flops_iter * args.steps / elapsed / (world * FP32_MFMA_PEAK),
         "conv_tflop_per_step": flops_iter / 1e12,
         "roofline": roofline,

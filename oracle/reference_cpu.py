@@ -124,6 +124,37 @@ def pack(t, B, pac):
     return torch.cat([t[k * B:(k + 1) * B] for k in range(pac)], 1)
 
 
+def _dp_shards(p):
+    """Replicas of the reference's ``data_parallel`` forward (GLI:393, GLI:455: arch 0 with
+    ``--n_gpu > 1`` on CUDA); the CPU oracle emulates it when ``p.dp_shards > 1``."""
+    return int(getattr(p, "dp_shards", 1) or 1)
+
+
+def data_parallel_emulated(main, x, n):
+    """torch.nn.parallel.data_parallel(main, x, range(n)) restated on one CPU device:
+    scatter = ``x.chunk(n)``, one replica per chunk, gather = ``cat`` on dim 0, gradients of
+    the shared parameters summed over replicas.  Buffers: replica 0 shares the module's
+    buffers (broadcast_coalesced hands the source device its own tensors), so only its
+    BatchNorm running-stat and spectral-norm u/v updates persist; every other replica starts
+    from the pre-forward buffers and its updates are discarded."""
+    if n <= 1:
+        return main(x)
+    chunks = x.chunk(n)
+    bufs = list(main.buffers())
+    with torch.no_grad():
+        pre = [b.clone() for b in bufs]
+    outs = [main(chunks[0])]
+    with torch.no_grad():
+        post = [b.clone() for b in bufs]
+    for c in chunks[1:]:
+        for b, v in zip(bufs, pre):
+            b.data.copy_(v)  # .data: the autograd graph keeps the buffers' version counters
+        outs.append(main(c))
+    for b, v in zip(bufs, post):
+        b.data.copy_(v)
+    return torch.cat(outs)
+
+
 def _maybe_sn(mod, on):
     return spectral_norm(mod) if on else mod
 
@@ -163,6 +194,7 @@ class _G0(nn.Module):
                                                             bias=False), sn))
         seq.add_module("End-Tanh", nn.Tanh())
         self.main = seq
+        self.dp = _dp_shards(p)
 
     @staticmethod
     def _act_block(seq, p, part, suffix, ch):
@@ -177,7 +209,7 @@ class _G0(nn.Module):
             seq.add_module(part + "-ReLU" + suffix, nn.ReLU())
 
     def forward(self, z):
-        return self.main(z)
+        return data_parallel_emulated(self.main, z, self.dp)
 
 
 class _D0(nn.Module):
@@ -218,9 +250,10 @@ class _D0(nn.Module):
         if p.loss_D == 1:
             seq.add_module("End-Sigmoid", nn.Sigmoid())
         self.main = seq
+        self.dp = _dp_shards(p)
 
     def forward(self, x):
-        return self.main(x).view(-1)
+        return data_parallel_emulated(self.main, x, self.dp).view(-1)
 
 
 def _act1(p, slope):

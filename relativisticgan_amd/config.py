@@ -3,8 +3,9 @@
 Plus this build's own switches (prefixed ``--rgan_``), which the reference lacks:
 ``--rgan_rng`` (``host``: draw z/u/batches from the CPU generators in the reference's
 order, bit-compatible inputs; ``device``: draw on the GPU, for throughput runs) and
-``--rgan_sync_bn`` (SyncBN under data parallelism, default on; off = the reference
-DataParallel's per-shard statistics), ``--rgan_pac 2`` (the PacGAN-2 script,
+``--rgan_sync_bn`` (BatchNorm statistics under data parallelism: default off = the
+reference's DataParallel, each rank normalises with its own shard; on = SyncBN over the
+global batch), ``--rgan_pac 2`` (the PacGAN-2 script,
 code/GAN_losses_iter_PAC.py, which shares this CLI) and ``--rgan_script`` (the defaults of
 GAN_losses_iter / GAN_losses_iter_art / GAN_losses_iter_PAC).
 """
@@ -58,7 +59,7 @@ def make_parser(script="GAN_losses_iter"):
     p.add_argument("--rgan_script", choices=SCRIPTS, default=script,
                    help="which reference script's defaults/behaviour to follow")
     p.add_argument("--rgan_rng", choices=("host", "device"), default="host")
-    p.add_argument("--rgan_sync_bn", type="bool", default=True)
+    p.add_argument("--rgan_sync_bn", type="bool", default=False)
     p.add_argument("--rgan_pac", dest="pac", type=int, default=2 if script == "GAN_losses_iter_PAC" else 1,
                    choices=(1, 2),
                    help="2 = PacGAN-2, the reference's code/GAN_losses_iter_PAC.py (D sees 2 samples packed "

@@ -67,6 +67,9 @@ extern "C" size_t rgan_bn_partial_bytes(long long P, int C) {
   return ((size_t)max_chunks(P, C) * 2 + 5) * C * sizeof(double) + 256;
 }
 
+// pixel rows whose loads each thread issues before consuming the first (bytes in flight)
+constexpr int BN_UNR = 4;
+
 template <int Q>
 __device__ __forceinline__ void load_q(const float* __restrict__ y, long long off, float (&v)[Q]) {
   if constexpr (Q == 4) {
@@ -103,15 +106,26 @@ __global__ __launch_bounds__(256) void bn_moments_partial(const float* __restric
   for (int q = 0; q < Q; ++q) { s1[q] = 0.0; s2[q] = 0.0; sft[q] = 0.f; }
   if (c0 < C) {
     load_q<Q>(y, (long long)c0 * sc, sft);
-    for (long long p = p0 + rl; p < p1; p += rp) {
-      float v[Q];
-      load_q<Q>(y, p * sp + (long long)c0 * sc, v);
+    auto acc = [&](const float (&v)[Q]) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const double d = (double)(v[q] - sft[q]);
         s1[q] += d;
         s2[q] += d * d;
       }
+    };
+    long long p = p0 + rl;
+    for (; p + (BN_UNR - 1) * rp < p1; p += BN_UNR * rp) {  // loads issued ahead, summed in p order
+      float v[BN_UNR][Q];
+#pragma unroll
+      for (int u = 0; u < BN_UNR; ++u) load_q<Q>(y, (p + u * rp) * sp + (long long)c0 * sc, v[u]);
+#pragma unroll
+      for (int u = 0; u < BN_UNR; ++u) acc(v[u]);
+    }
+    for (; p < p1; p += rp) {
+      float v[Q];
+      load_q<Q>(y, p * sp + (long long)c0 * sc, v);
+      acc(v);
     }
   }
 #pragma unroll
@@ -273,9 +287,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
     be[q] = (beta ? beta[c] : 0.f) - stats[c] * al[q];
   }
   const long long step = (long long)gridDim.y * rp;
-  for (long long p = (long long)blockIdx.y * rp + rl; p < P; p += step) {
-    float v[Q];
-    load_q<Q>(y, p * sp + (long long)c0 * sc, v);
+  auto out = [&](long long p, float (&v)[Q]) {
 #pragma unroll
     for (int q = 0; q < Q; ++q) v[q] = act_fwd(v[q] * al[q] + be[q], act, alpha);
     if constexpr (Q == 4) {
@@ -283,6 +295,19 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
     } else {
       a[p * asp + (long long)c0 * asc] = v[0];
     }
+  };
+  long long p = (long long)blockIdx.y * rp + rl;
+  for (; p + (BN_UNR - 1) * step < P; p += BN_UNR * step) {
+    float v[BN_UNR][Q];
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) load_q<Q>(y, (p + u * step) * sp + (long long)c0 * sc, v[u]);
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) out(p + u * step, v[u]);
+  }
+  for (; p < P; p += step) {
+    float v[Q];
+    load_q<Q>(y, p * sp + (long long)c0 * sc, v);
+    out(p, v);
   }
 }
 
@@ -334,16 +359,30 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ 
     be[q] = (beta ? beta[c] : 0.f) - mean[q] * al[q];
   }
   if (c0 < C) {
-    for (long long p = p0 + rl; p < p1; p += rp) {
-      float v[Q], g[Q];
-      load_q<Q>(y, p * sp + (long long)c0 * sc, v);
-      load_q<Q>(da, p * dsp + (long long)c0 * dsc, g);
+    auto acc = [&](const float (&v)[Q], const float (&g)[Q]) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const double gz = (double)(g[q] * act_grad_from_in(v[q] * al[q] + be[q], act, alpha));
         s1[q] += gz;
         s2[q] += gz * (double)(v[q] - mean[q]);
       }
+    };
+    long long p = p0 + rl;
+    for (; p + (BN_UNR - 1) * rp < p1; p += BN_UNR * rp) {
+      float v[BN_UNR][Q], g[BN_UNR][Q];
+#pragma unroll
+      for (int u = 0; u < BN_UNR; ++u) {
+        load_q<Q>(y, (p + u * rp) * sp + (long long)c0 * sc, v[u]);
+        load_q<Q>(da, (p + u * rp) * dsp + (long long)c0 * dsc, g[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < BN_UNR; ++u) acc(v[u], g[u]);
+    }
+    for (; p < p1; p += rp) {
+      float v[Q], g[Q];
+      load_q<Q>(y, p * sp + (long long)c0 * sc, v);
+      load_q<Q>(da, p * dsp + (long long)c0 * dsc, g);
+      acc(v, g);
     }
   }
 #pragma unroll
@@ -391,10 +430,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ da
     }
   }
   const long long step = (long long)gridDim.y * rp;
-  for (long long p = (long long)blockIdx.y * rp + rl; p < P; p += step) {
-    float v[Q], g[Q];
-    load_q<Q>(y, p * sp + (long long)c0 * sc, v);
-    load_q<Q>(da, p * dsp + (long long)c0 * dsc, g);
+  auto out = [&](long long p, float (&v)[Q], const float (&g)[Q]) {
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const float gz = g[q] * act_grad_from_in(v[q] * al[q] + be[q], act, alpha);
@@ -405,6 +441,23 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ da
     } else {
       dy[p * ysp + (long long)c0 * ysc] = v[0];
     }
+  };
+  long long p = (long long)blockIdx.y * rp + rl;
+  for (; p + (BN_UNR - 1) * step < P; p += BN_UNR * step) {
+    float v[BN_UNR][Q], g[BN_UNR][Q];
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) {
+      load_q<Q>(y, (p + u * step) * sp + (long long)c0 * sc, v[u]);
+      load_q<Q>(da, (p + u * step) * dsp + (long long)c0 * dsc, g[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) out(p + u * step, v[u], g[u]);
+  }
+  for (; p < P; p += step) {
+    float v[Q], g[Q];
+    load_q<Q>(y, p * sp + (long long)c0 * sc, v);
+    load_q<Q>(da, p * dsp + (long long)c0 * dsc, g);
+    out(p, v, g);
   }
 }
 

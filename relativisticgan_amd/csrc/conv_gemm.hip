@@ -1264,27 +1264,29 @@ __global__ void pack_narrow(const float* __restrict__ W, float* __restrict__ out
 
 // Tiled pack for the layouts whose columns are one weight index (n = out_idx) and whose
 // rows are (tap, in_idx) with in_idx fastest -- every pack on the FAST paths: a block
-// moves a 16 in x 16 out x (<= 16 taps) brick through LDS, reading W in its own
-// contiguous order (taps, then the smaller-stride index) and writing 16-float k runs of
-// the [N][K] image.
+// moves a 32 in x 8 out x (<= 16 taps) brick through LDS, reading W in its own contiguous
+// order (taps, then the smaller-stride index: 512 or 128 contiguous floats) and writing
+// whole 128-B lines (32-float k runs) of the [N][K] image.
+constexpr int PK_I = 32, PK_O = 8, PK_LD = PK_O * 17 + 1;  // odd row stride: conflict-free reads
 __global__ __launch_bounds__(256) void pack_tiled(PackArgs a) {
-  __shared__ float t[16][16][17];  // [in][out][tap]
+  __shared__ float t[PK_I * PK_LD];  // [in][out][tap]
   const int KK = a.KH * a.KW;
   const int Nin = (int)a.fpci.d, Nout = a.N;
-  const int i0 = blockIdx.x * 16, o0 = blockIdx.y * 16;
+  const int i0 = blockIdx.x * PK_I, o0 = blockIdx.y * PK_O;
   const bool in_fast = a.s_in < a.s_out;
-  for (int e = threadIdx.x; e < 16 * 16 * 16; e += 256) {
-    const int tap = e & 15, u = (e >> 4) & 15, v = e >> 8;
-    const int i = in_fast ? u : v, o = in_fast ? v : u;
+  for (int e = threadIdx.x; e < PK_I * PK_O * 16; e += 256) {
+    const int tap = e & 15;
+    const int i = in_fast ? (e >> 4) & (PK_I - 1) : e >> 7;
+    const int o = in_fast ? e >> 9 : (e >> 4) & (PK_O - 1);
     float val = 0.f;
     if (tap < KK && i0 + i < Nin && o0 + o < Nout)
       val = a.W[(long long)(i0 + i) * a.s_in + (long long)(o0 + o) * a.s_out + tap];
-    t[i][o][tap] = val;
+    t[i * PK_LD + o * 17 + tap] = val;
   }
   __syncthreads();
   const int K = a.K;
-  for (int e = threadIdx.x; e < 16 * 16 * 16; e += 256) {
-    const int i = e & 15, o = (e >> 4) & 15, tap = e >> 8;
+  for (int e = threadIdx.x; e < PK_I * PK_O * 16; e += 256) {
+    const int i = e & (PK_I - 1), o = (e >> 5) & (PK_O - 1), tap = e >> 8;
     if (tap >= KK || i0 + i >= Nin || o0 + o >= Nout) continue;
     const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
     int phase = 0, kt;
@@ -1294,7 +1296,7 @@ __global__ __launch_bounds__(256) void pack_tiled(PackArgs a) {
     } else {
       kt = a.flip ? (a.KH - 1 - kh) * a.KW + (a.KW - 1 - kw) : tap;
     }
-    a.out[((size_t)phase * Nout + o0 + o) * K + (size_t)kt * Nin + i0 + i] = t[i][o][tap];
+    a.out[((size_t)phase * Nout + o0 + o) * K + (size_t)kt * Nin + i0 + i] = t[i * PK_LD + o * 17 + tap];
   }
 }
 
@@ -1692,7 +1694,7 @@ static void launch_pack(const PackArgs& a, hipStream_t s) {
   // tiled when n is one weight index and the taps are contiguous in W
   if (a.fnco.d == (uint32_t)a.N && a.fnkw.d == 1 && a.s_kw == 1 && a.s_kh == a.KW && a.KH * a.KW <= 16 &&
       (!a.convt2 || (a.KH == 4 && a.KW == 4))) {
-    pack_tiled<<<dim3(ceil_div((int)a.fpci.d, 16), ceil_div(a.N, 16)), 256, 0, s>>>(a);
+    pack_tiled<<<dim3(ceil_div((int)a.fpci.d, PK_I), ceil_div(a.N, PK_O)), 256, 0, s>>>(a);
     return;
   }
   const int ny = std::min(a.N, 8192);

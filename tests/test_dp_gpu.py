@@ -68,15 +68,15 @@ def _run(name, world, rank, n_iter=None):
     return out
 
 
-def _worker(rank, world, port, name, path):
+def _worker(rank, world, port, name, path, sync_bn=True, n_iter=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from relativisticgan_amd import dp
-    dp.setup(sync_bn=True)
+    dp.setup(sync_bn=sync_bn)
     try:
-        res = _run(name, world, rank)
+        res = _run(name, world, rank, n_iter)
         # gather the per-rank D outputs so rank 0 holds the global vectors
         for st in res:
             for k in ("y_pred", "y_pred_fake"):
@@ -94,19 +94,67 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("name", ["ralsgan", "rasgan", "wgangp", "rahinge_spectral", "sgan", "ralsgan_pac2"])
-def test_dp2_matches_single_process(name):
-    single = _run(name, 1, 0)
+def _spawn(name, sync_bn=True, n_iter=None):
     path = os.path.join(tempfile.mkdtemp(), "dp.pt")
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, path)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, path, sync_bn, n_iter)) for r in range(2)]
     for pr in procs:
         pr.start()
     for pr in procs:
         pr.join(300)
         assert pr.exitcode == 0
-    dpres = torch.load(path, weights_only=True)
+    return torch.load(path, weights_only=True)
+
+
+@pytest.mark.parametrize("name", ["ralsgan", "rasgan", "wgangp", "rahinge_spectral", "sgan", "ralsgan_pac2"])
+def test_dp2_matches_single_process(name):
+    single = _run(name, 1, 0)
+    dpres = _spawn(name)
+    _compare(name, dpres, single)
+
+
+def _oracle_data_parallel(name, shards, n_iter=1):
+    """The reference's --n_gpu data_parallel step (GLI:393, GLI:455) on the CPU oracle."""
+    from oracle.reference_cpu import Trainer as OracleTrainer
+    torch.set_num_threads(8)
+    p = param_for(name, dp_shards=shards)
+    holder, out = {}, []
+
+    def hooks(tag, r):
+        t, st = holder["t"], out[-1]
+        if tag == "D":
+            st["errD"] = r["errD"].detach().clone()
+            st["y_pred"] = r["y_pred"].detach().clone()
+            st["y_pred_fake"] = r["y_pred_fake"].detach().clone()
+            st["gradD"] = {n: q.grad.detach().clone() for n, q in t.D.named_parameters()}
+        elif tag == "G":
+            st["errG"] = r["errG"].detach().clone()
+            st["gradG"] = {n: q.grad.detach().clone() for n, q in t.G.named_parameters()}
+    t = OracleTrainer(p, dataset_for(name), hooks=hooks)
+    holder["t"] = t
+    for i in range(n_iter):
+        out.append({})
+        t.iteration(i)
+        out[-1]["G"] = {k: v.detach().clone() for k, v in t.G.state_dict().items()}
+        out[-1]["D"] = {k: v.detach().clone() for k, v in t.D.state_dict().items()}
+    return out
+
+
+@pytest.mark.parametrize("name", ["ralsgan", "rasgan", "wgangp", "rahinge_spectral"])
+def test_dp2_per_shard_bn_matches_reference_data_parallel(name):
+    """--rgan_sync_bn False: every rank normalises with its own shard's statistics, the
+    reference's DataParallel semantics (replica BN on its scatter chunk, loss on the
+    gathered outputs, gradients summed, replica 0's running statistics kept).  Compared
+    with the oracle's restatement of data_parallel over 2 replicas, iteration 0 (free
+    running after it: Adam sign flips).  PacGAN is excluded: the ranks shard each packing
+    slot, DataParallel would chunk the 2B z rows."""
+    dpres = _spawn(name, sync_bn=False, n_iter=1)
+    ref = _oracle_data_parallel(name, 2)
+    _compare(name, dpres, ref)
+
+
+def _compare(name, dpres, single):
     p = param_for(name)
     errs = []
     for i, (a, b) in enumerate(zip(dpres, single)):
