@@ -119,13 +119,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RGAN_BENCH_BACKEND=gloo + more ranks than GPUs: rehearsal of the N>1 path on one GPU
+    backend = os.environ.get("RGAN_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     from relativisticgan_amd import dp, kernels as K
     from relativisticgan_amd.config import make_param
     from relativisticgan_amd.train import Trainer, synthetic_images
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
         dp.setup(sync_bn=args.sync_bn)
     loss_D, size, bpg, h = WORKLOADS[args.workload]
     spectral = args.workload == "C5"
@@ -137,6 +144,7 @@ def main():
 
     for i in range(args.warmup):
         t.iteration(i + 1)
+    t.flush()
 
     def barrier():
         if world > 1:
@@ -148,6 +156,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         t.iteration(args.warmup + 1 + i)
+    t.flush()  # the last G step (deferred under DP) is inside the timed region
     barrier()
     elapsed = time.perf_counter() - t0
     prof = K.profile_end()

@@ -65,6 +65,7 @@ class Trainer:
         # gradient SUM all-reduce overlapped with the last backward of each step (world > 1)
         self.redD = dp.GradReducer(self.D.parameters()) if self.world > 1 else None
         self.redG = dp.GradReducer(self.G.parameters()) if self.world > 1 else None
+        self._pending_G, self._pending_decay_G = None, False
         self.host_rng = getattr(p, "rgan_rng", "host") == "host"
         self.pac = getattr(p, "pac", 1)  # 2: code/GAN_losses_iter_PAC.py
         self._fake_D = None
@@ -144,6 +145,7 @@ class Trainer:
         gp_on = kind == 3 or p.grad_penalty
         zshape = (p.batch_size * self.pac, p.z_size, 1, 1)
         if i % p.print_every == 0:
+            self.flush()
             with torch.no_grad():
                 self.fake_test = G(self.z_test)  # GLI:564 (sample image; BN running stats move)
         self._set_D_grad(True)
@@ -155,6 +157,7 @@ class Trainer:
                 err_real = loss_D_real(kind, y_pred)
                 err_real.backward()
                 z = self._normal(feed, "z_D", zshape)
+                self.flush()
                 x_fake = self._generate_D(z)
                 y_pred_fake = D(x_fake)
                 err_fake = loss_D_fake(kind, y_pred_fake)
@@ -164,6 +167,7 @@ class Trainer:
                 errD = err_real.detach() + err_fake.detach()
             else:
                 z = self._normal(feed, "z_D", zshape)
+                self.flush()
                 x_fake = self._generate_D(z)
                 y_pred_fake = D(x_fake)
                 errD = loss_D(kind, y_pred, y_pred_fake)
@@ -189,6 +193,7 @@ class Trainer:
         self.last["D"] = rec
         self._set_D_grad(False)
         for _ in range(p.Giters):
+            self.flush()
             G.zero_grad()
             z = self._normal(feed, "z_G", zshape)
             if self.pac == 1:
@@ -212,26 +217,50 @@ class Trainer:
             self._arm(self.redG)
             errG.backward()
             recG.update(y_pred_fake=y_pred_fake.detach(), errG=errG.detach())
-            if self.redG is not None:
-                self.redG.finish()
-            if hooks:
-                hooks("G", recG)
-            self.optG.step()
-            if hooks:
-                hooks("G.post", recG)
+            self._pending_G = (hooks, recG)
+            if self.redG is None:
+                self._step_G()
         self.errG = errG
         self.last["G"] = recG
         self.decayD.step()
-        self.decayG.step()
+        if self._pending_G is None:
+            self.decayG.step()
+        else:
+            self._pending_decay_G = True
+
+    def _step_G(self):
+        hooks, recG = self._pending_G
+        self._pending_G = None
+        if self.redG is not None:
+            self.redG.finish()
+        if hooks:
+            hooks("G", recG)
+        self.optG.step()
+        if hooks:
+            hooks("G.post", recG)
+
+    def flush(self):
+        """Under data parallelism G's optimizer step (and its LR decay) is deferred to the
+        next use of G: the G gradients' all-reduce then overlaps the next iteration's
+        real-batch D forward, which does not read G (GLI:580-590 draw x and run D(x) before
+        G(z)).  The order of every draw and every result is unchanged.  Called before any
+        G forward, before checkpoints, and by callers that stop iterating."""
+        if self._pending_G is not None:
+            self._step_G()
+        if self._pending_decay_G:
+            self._pending_decay_G = False
+            self.decayG.step()
 
     # -- checkpoint (GLI:536-552, 733-747): same dict keys as the reference
     def state(self, i, current_set_images=0):
+        self.flush()
         return {"i": i, "current_set_images": current_set_images, "G_state": self.G.state_dict(),
                 "D_state": self.D.state_dict(), "G_optimizer": self.optG.state_dict(),
                 "D_optimizer": self.optD.state_dict(), "G_scheduler": self.decayG.state_dict(),
                 "D_scheduler": self.decayD.state_dict(), "z_test": _gather_batch(self.z_test)}
 
     def load(self, ckpt):
+        self.flush()
         self.G.load_state_dict(ckpt["G_state"])
         self.D.load_state_dict(ckpt["D_state"])
         self.optG.load_state_dict(ckpt["G_optimizer"])
@@ -364,7 +393,9 @@ def main(argv=None):
                     torch.save(st, os.path.join(p.extra_folder, "models", "state_%02d.pth" % current_set_images))
                     say("Models saved")
             if p.gen_extra_images > 0:
+                t.flush()
                 generate_extra_images(t.G, p, "%s/%01d/" % (p.extra_folder, current_set_images))
+    t.flush()
     if log:
         log.close()
     return t

@@ -62,6 +62,7 @@ def _run(name, world, rank, n_iter=None):
     for i in range(n_iter):
         st = {}
         t.iteration(i, hooks=_capture(t, st))
+        t.flush()  # under DP the G step waits for the next G use
         st["G"] = {k: v.detach().cpu().clone() for k, v in t.G.state_dict().items()}
         st["D"] = {k: v.detach().cpu().clone() for k, v in t.D.state_dict().items()}
         out.append(st)
