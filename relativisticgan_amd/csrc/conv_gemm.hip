@@ -86,6 +86,7 @@ struct GemmArgs {
   float* slab;
   // FAST paths (raw buffer loads, scalar per-tile offsets): descriptor sizes in bytes
   int a_bytes, im_bytes, bw_bytes;
+  int vec_out;            // output n-quads contiguous and 16-B aligned (host-checked)
 };
 
 __device__ __forceinline__ long long row_offset(const OutMap& o, int m, int phase) {
@@ -138,7 +139,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
   constexpr int B_LD = KROW ? KROW_LD : BN + 4;
   constexpr int B_SZ = KROW ? BN * KROW_LD : BK * B_LD;
   constexpr int STAGE = A_SZ + B_SZ;
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE];
+  constexpr int EPI_SZ = KROW ? 4 * 64 * 72 : 0;  // vector epilogue staging (4 waves x 64 x 72)
+  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE > EPI_SZ ? 2 * STAGE : EPI_SZ];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = (wid / WN) * (BM / WM), wn = (wid % WN) * (BN / WN);
@@ -688,6 +690,59 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
   }
 
   // ---------------- epilogue ----------------
+  if constexpr (KROW && BM / WM == 64 && BN / WN == 64) {
+    // Vector epilogue (FAST, 64x64 per wave): each wave stages its finished sub-tile in LDS
+    // (row stride 72: the two lane halves' rows 4 apart land 32 banks apart) and writes it
+    // back as float4 rows -- 16 b128 stores per lane instead of 64 scalar ones, 256
+    // contiguous bytes per output row.  The scalar stores' bursts at the end of every tile
+    // (all blocks finish together) held the MFMA pipes idle on short-K layers.
+    const bool slab_out = g.splits > 1;
+    if ((slab_out && g.N % 4 == 0) || (!slab_out && g.vec_out)) {
+      constexpr int EP_LD = 72;
+      __shared__ long long emoff[BM];
+      float* T = smem + wid * (64 * EP_LD);
+      const float wsc = (!slab_out && g.wscale) ? g.wscale[0] : 1.f;
+      if (!slab_out) {
+        for (int i = tid; i < BM; i += 256) {
+          const int m = m0 + i;
+          emoff[i] = m < g.M ? row_offset(g.out, m, MODE == MODE_CONVT2 ? phase : 0) : 0;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int cl = 32 * j + l32, col = n0 + wn + cl;
+        const float bv = (!slab_out && g.bias && col < g.N) ? g.bias[col] : 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int rl = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+            float v = acc[i][j][r];
+            if (!slab_out) v = act_fwd(v * wsc + bv, g.act, g.alpha);
+            T[rl * EP_LD + cl] = v;
+          }
+      }
+      __syncthreads();
+      const int q = lane & 15, n = n0 + wn + 4 * q;
+      if (n < g.N) {
+        float* slab = slab_out ? g.slab + (size_t)z * g.M * g.N : nullptr;
+        const long long noff = slab_out ? 0 : col_offset(g.out, n);
+#pragma unroll
+        for (int s4 = 0; s4 < 16; ++s4) {
+          const int rl = 4 * s4 + (lane >> 4), m = m0 + wm + rl;
+          if (m < g.M) {
+            const float4 v = *reinterpret_cast<const float4*>(T + rl * EP_LD + 4 * q);
+            float* dst = slab_out ? slab + (size_t)m * g.N + n : g.C + emoff[wm + rl] + noff;
+#if RGAN_EXP_NOSTORE
+            if (v.x == 1234.5f)
+#endif
+            *reinterpret_cast<float4*>(dst) = v;
+          }
+        }
+      }
+      return;
+    }
+  }
   if (g.splits > 1) {
     float* slab = g.slab + (size_t)z * g.M * g.N;
 #pragma unroll
@@ -727,6 +782,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
         const int rl = wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
         if (m0 + rl < g.M && col < g.N) {
           float v = acc[i][j][r] * wsc + bv;
+#if RGAN_EXP_NOSTORE  // timing-only experiment: drop the output stores
+          if (v == 1234.5f)
+#endif
           g.C[moff[rl] + noff[cl]] = act_fwd(v, g.act, g.alpha);
         }
       }
@@ -1867,6 +1925,12 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     RGAN_CHECK_LAUNCH();
   }
   p.g.slab = p.slab_floats ? (float*)w : nullptr;
+  {
+    const OutMap& o = p.g.out;
+    auto al4 = [](long long v) { return (v & 3) == 0; };
+    p.g.vec_out = p.mode != MODE_WGRAD && o.tc == 1 && o.fnc.d % 4 == 0 && p.g.N % 4 == 0 && al4(o.th) &&
+                  al4(o.tw) && al4(o.sb) && al4(o.sh) && al4(o.sw) && aligned16(p.g.C);
+  }
   int bm, bn;
   tile_dims(p.cfg, bm, bn);
   dim3 grid(ceil_div(p.g.M, bm) * p.g.tiles_n, 1, p.phases * p.g.splits);
