@@ -697,7 +697,11 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
     // contiguous bytes per output row.  The scalar stores' bursts at the end of every tile
     // (all blocks finish together) held the MFMA pipes idle on short-K layers.
     const bool slab_out = g.splits > 1;
+#if RGAN_EXP_SCALAR_SLAB
+    if (!slab_out && g.vec_out) {
+#else
     if ((slab_out && g.N % 4 == 0) || (!slab_out && g.vec_out)) {
+#endif
       constexpr int EP_LD = 72;
       __shared__ long long emoff[BM];
       float* T = smem + wid * (64 * EP_LD);
@@ -736,7 +740,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
 #if RGAN_EXP_NOSTORE
             if (v.x == 1234.5f)
 #endif
-            *reinterpret_cast<float4*>(dst) = v;
+*reinterpret_cast<float4*>(dst) = v;
           }
         }
       }
@@ -983,6 +987,32 @@ __global__ __launch_bounds__(256) void dense1_wgrad(DenseArgs a) {
 #pragma unroll 16
   for (int b = 0; b < a.B; ++b) acc = fmaf(a.y[(long long)b * a.ysb], a.x[(long long)b * a.xsb + xo], acc);
   a.out[wi] = acc;
+}
+
+// WGRAD with 4x4 taps: the GEMM writes C[co][(tap, ci)] with whole-row float4 stores
+// (tap-major staging) and this pass turns it into torch layout dW[co][ci][tap].  Writing
+// torch layout from the GEMM directly scatters 4-B stores at a 64-B stride (a tile covers
+// one tap); on the deep layers (N = 16 Cin up to 16384) that cost ~20 % of the GEMM.
+// 16 taps x 64 channels per block through LDS; reads 256-B rows, writes 4 KiB runs.
+constexpr int TT_LD = 68;  // (16 t + ci) distinct mod 64 on the read side
+__global__ __launch_bounds__(256) void taps_transpose(const float* __restrict__ T, float* __restrict__ O, int Cin,
+                                                      long long osb) {
+  __shared__ float sh[16 * TT_LD];
+  const int co = blockIdx.y, c0 = blockIdx.x * 64;
+  const float* src = T + (size_t)co * 16 * Cin;
+  {
+    const int t = threadIdx.x >> 4, q = threadIdx.x & 15, c = c0 + 4 * q;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < Cin) v = *reinterpret_cast<const float4*>(src + (size_t)t * Cin + c);
+    sh[t * TT_LD + 4 * q] = v.x; sh[t * TT_LD + 4 * q + 1] = v.y;
+    sh[t * TT_LD + 4 * q + 2] = v.z; sh[t * TT_LD + 4 * q + 3] = v.w;
+  }
+  __syncthreads();
+  const int ci = threadIdx.x >> 2, tq = threadIdx.x & 3;
+  if (c0 + ci < Cin)
+    *reinterpret_cast<float4*>(O + (long long)co * osb + (long long)(c0 + ci) * 16 + 4 * tq) =
+        make_float4(sh[(4 * tq) * TT_LD + ci], sh[(4 * tq + 1) * TT_LD + ci], sh[(4 * tq + 2) * TT_LD + ci],
+                    sh[(4 * tq + 3) * TT_LD + ci]);
 }
 
 // ---------------------------------------------------------------- weight packing
@@ -1372,6 +1402,9 @@ struct Plan {
   const float* prepacked = nullptr;  // caller-owned packed weights (skip packing)
   PackArgs pk{};
   size_t pack_floats = 0, slab_floats = 0;
+  // WGRAD tap-major staging (taps_transpose): C of the GEMM -> workspace, then torch layout
+  bool tap_stage = false;
+  size_t tap_floats = 0;
   // narrow kernels (MODE_NARROW_T / MODE_NARROW_IN)
   NarrowArgs na{};
   long long pn_s_in = 0, pn_s_out = 0;  // narrow pack strides
@@ -1740,12 +1773,19 @@ static int plan_wgrad(const RganConv* d, const float* x, const float* dy, float*
   p.bv = vec_img_ok(g.im);
   choose_tiling(p);
   set_fast(p, d->batch);
+  // unsplit FAST wgrads with 4x4 taps: row-contiguous staging + taps_transpose
+  const OutMap& o = g.out;
+  if (p.fast && g.splits == 1 && p.cfg == CFG_L && o.fnkw.d == 4 && (uint32_t)g.N == 16 * o.fnc.d &&
+      o.th == 4 && o.tw == 1 && o.tc == 16 && o.sb % 4 == 0 && o.fnc.d % 4 == 0) {
+    p.tap_stage = true;
+    p.tap_floats = (size_t)g.M * g.N;
+  }
   return 0;
 }
 
 static size_t plan_ws_bytes(const Plan& p) {
   const size_t pack = p.prepacked ? 0 : align_up(p.pack_floats * 4, 256);
-  return pack + align_up(p.slab_floats * 4, 256);
+  return pack + align_up(p.slab_floats * 4, 256) + align_up(p.tap_floats * 4, 256);
 }
 
 static void launch_pack(const PackArgs& a, hipStream_t s) {
@@ -1925,6 +1965,15 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     RGAN_CHECK_LAUNCH();
   }
   p.g.slab = p.slab_floats ? (float*)w : nullptr;
+  float* tap_dst = nullptr;
+  long long tap_osb = 0;
+  if (p.tap_stage && !aligned16(p.g.C)) p.tap_stage = false;  // workspace stays sized for it
+  if (p.tap_stage) {
+    tap_dst = p.g.C;
+    tap_osb = p.g.out.sb;
+    p.g.C = (float*)(w + align_up(p.slab_floats * 4, 256));
+    p.g.out = make_out(1, 1, 1, p.g.N, 0, 0, 1, 1, p.g.N, 0, 0, 1);  // [M][N], n contiguous
+  }
   {
     const OutMap& o = p.g.out;
     auto al4 = [](long long v) { return (v & 3) == 0; };
@@ -1952,6 +2001,11 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   if (prof) {
     hipEventRecord(rec.b, s);
     g_recs.push_back(rec);
+  }
+  if (p.tap_stage) {
+    const int cin = p.g.N / 16;
+    taps_transpose<<<dim3(ceil_div(cin, 64), p.g.M), 256, 0, s>>>(p.g.C, tap_dst, cin, tap_osb);
+    RGAN_CHECK_LAUNCH();
   }
   if (p.g.splits > 1) {
     const GemmArgs& g = p.g;
@@ -1995,7 +2049,7 @@ using namespace rgan;
 
 extern "C" size_t rgan_conv_workspace(const RganConv* d, int which, int prepacked) {
   Plan p;
-  static const float dummy[4] = {0, 0, 0, 0};
+  alignas(16) static const float dummy[4] = {0, 0, 0, 0};
   int rc;
   if (which == 0) rc = plan_fwd(d, dummy, dummy, nullptr, nullptr, (float*)dummy, 0, 0.f, p);
   else if (which == 1) rc = plan_dgrad(d, dummy, dummy, nullptr, (float*)dummy, p);
@@ -2007,7 +2061,7 @@ extern "C" size_t rgan_conv_workspace(const RganConv* d, int which, int prepacke
 
 extern "C" size_t rgan_conv_pack_floats(const RganConv* d, int which) {
   Plan p;
-  static const float dummy[4] = {0, 0, 0, 0};
+  alignas(16) static const float dummy[4] = {0, 0, 0, 0};
   int rc = which == 0 ? plan_fwd(d, dummy, dummy, nullptr, nullptr, (float*)dummy, 0, 0.f, p)
                       : plan_dgrad(d, dummy, dummy, nullptr, (float*)dummy, p);
   if (rc || which > 1 || !p.pack) return 0;  // 0: no packed layout (or unsupported)
@@ -2017,7 +2071,7 @@ extern "C" size_t rgan_conv_pack_floats(const RganConv* d, int which) {
 extern "C" int rgan_conv_pack(const RganConv* d, int which, const float* w, float* packed, void* stream) {
   if (!w || !packed || which < 0 || which > 1) return RGAN_EINVAL;
   Plan p;
-  static const float dummy[4] = {0, 0, 0, 0};
+  alignas(16) static const float dummy[4] = {0, 0, 0, 0};
   int rc = which == 0 ? plan_fwd(d, dummy, w, nullptr, nullptr, (float*)dummy, 0, 0.f, p)
                       : plan_dgrad(d, dummy, w, nullptr, (float*)dummy, p);
   if (rc) return rc;

@@ -40,6 +40,8 @@ def main():
     ops = (sys.argv[2] if len(sys.argv) > 2 else "fwd,dgrad,wgrad,convt,convtd,convtw,small").split(",")
     B = 64
     layers = [(128, 256, 64), (512, 1024, 16)]  # (cin, cout, H_in) of D convs k4s2p1
+    if "deep" in ops:
+        layers = [(1024, 2048, 8)]
     for cin, cout, H in layers:
         x = nhwc(B, cin, H, H)
         w = torch.nn.Parameter(torch.randn(cout, cin, 4, 4, device="cuda") * 0.02)
@@ -50,7 +52,7 @@ def main():
             run(f"conv dgrad {cin}->{cout} @{H}", lambda: K.conv_dgrad(dy, w, G, tuple(x.shape), cache=True), reps)
         if "wgrad" in ops:
             run(f"conv wgrad {cin}->{cout} @{H}", lambda: K.conv_wgrad(x, dy, G, tuple(w.shape)), reps)
-    for cin, cout, H in [(256, 128, 32), (1024, 512, 8)]:  # G ConvT k4s2p1
+    for cin, cout, H in ([(2048, 1024, 4)] if "deep" in ops else [(256, 128, 32), (1024, 512, 8)]):  # G ConvT
         x = nhwc(B, cin, H, H)
         w = torch.nn.Parameter(torch.randn(cin, cout, 4, 4, device="cuda") * 0.02)
         dy = nhwc(B, cout, 2 * H, 2 * H)
