@@ -26,6 +26,8 @@ from . import kernels as K
 # discontinuous at 0 (ReLU, LeakyReLU, SELU) appends the sign mask of its output, in call
 # order, so parity tests can count sign flips against an exact (fp64) forward.
 ACT_TRACE = None
+ACT_TAGS = []      # per ACT_TRACE entry: the net that produced it ("G" / "D", set by nets._Net)
+TRACE_NET = None
 _KINKED = ("relu", "lrelu", "selu")
 
 
@@ -150,11 +152,24 @@ class _AllReduceSum(torch.autograd.Function):
 
 
 # ---------------------------------------------------------------- fused layer
+def _train_stats(y, spec, rm, rv, nbt):
+    if dp.sync_bn():
+        mom = dp.all_gather_cat(K.bn_moments(y))
+        return K.bn_finalize(mom, dp.world(), y.shape[1], spec.eps, spec.momentum, rm, rv, nbt)
+    return K.bn_stats(y, spec.eps, spec.momentum, rm, rv, nbt)
+
+
 class ConvLayerFn(torch.autograd.Function):
-    """a = act(BN(conv(x, w_eff) + bias)); see module docstring."""
+    """a = act(BN(conv(x, w_eff) + bias)); see module docstring.
+
+    ``segs`` > 1: the batch holds that many equal segments which the reference runs as
+    separate forward calls of the same net (D(x) and D(x_fake), GLI:580-605): one conv
+    GEMM over all of them, BatchNorm statistics and running-stat updates per segment in
+    segment order, one dgrad and one wgrad in the backward (the weight gradient of both
+    calls in a single K-doubled GEMM instead of two GEMMs and a gradient add)."""
 
     @staticmethod
-    def forward(ctx, x, w, bias, gamma, beta, spec, bufs, sn):
+    def forward(ctx, x, w, bias, gamma, beta, spec, bufs, sn, segs=1):
         # bufs = (running_mean, running_var, num_batches_tracked, training)
         # sn   = (u, v, inv_sigma) clones for spectral layers, else None
         wscale = sn[2] if spec.spectral else None
@@ -163,16 +178,22 @@ class ConvLayerFn(torch.autograd.Function):
             y = K.conv_fwd(x, w, spec.geom, bias=bias, wscale=wscale, cache=True)
             rm, rv, nbt, training = bufs
             C = y.shape[1]
-            if training:
-                if dp.sync_bn():
-                    mom = dp.all_gather_cat(K.bn_moments(y))
-                    stats = K.bn_finalize(mom, dp.world(), C, spec.eps, spec.momentum, rm, rv, nbt)
-                else:
-                    stats = K.bn_stats(y, spec.eps, spec.momentum, rm, rv, nbt)
+            if training and segs > 1:
+                Bs = y.shape[0] // segs
+                a = torch.empty_like(y)
+                st = []
+                for s_ in range(segs):
+                    sl = slice(s_ * Bs, (s_ + 1) * Bs)
+                    st.append(_train_stats(y[sl], spec, rm, rv, nbt))
+                    K.bn_apply(y[sl], st[-1], gamma, beta, spec.act, spec.alpha, out=a[sl])
+                stats = torch.stack(st)
             else:
-                stats = torch.cat([rm, torch.rsqrt(rv + spec.eps)])
-                stats_eval = (rm, stats[C:])
-            a = K.bn_apply(y, stats, gamma, beta, spec.act, spec.alpha)
+                if training:
+                    stats = _train_stats(y, spec, rm, rv, nbt)
+                else:
+                    stats = torch.cat([rm, torch.rsqrt(rv + spec.eps)])
+                    stats_eval = (rm, stats[C:])
+                a = K.bn_apply(y, stats, gamma, beta, spec.act, spec.alpha)
             ctx.save_for_backward(x, w, bias, gamma, beta, y, stats, *(sn if spec.spectral else ()))
         else:
             a = K.conv_fwd(x, w, spec.geom, bias=bias, act=spec.act, alpha=spec.alpha, wscale=wscale,
@@ -180,9 +201,11 @@ class ConvLayerFn(torch.autograd.Function):
             ctx.save_for_backward(x, w, bias, gamma, beta, a, None, *(sn if spec.spectral else ()))
         if ACT_TRACE is not None and spec.act in _KINKED:
             ACT_TRACE.append((a.detach() > 0).cpu())
+            ACT_TAGS.append(TRACE_NET)
         ctx.spec = spec
         ctx.stats_eval = stats_eval
         ctx.training = bufs[3] if bufs is not None else True
+        ctx.segs = segs
         return a
 
     @staticmethod
@@ -193,6 +216,8 @@ class ConvLayerFn(torch.autograd.Function):
         sn = saved[7:10] if spec.spectral else None
         nx, nw, nb, ng, nbeta = ctx.needs_input_grad[:5]
         if torch.is_grad_enabled():
+            if ctx.segs > 1:
+                raise NotImplementedError("double backward through a segmented (batched) layer call")
             return ConvLayerFn._create_graph_backward(ctx, da, x, w, bias, gamma, beta, sn)
         wscale = sn[2] if spec.spectral else None
         dgamma = dbeta = None
@@ -203,7 +228,9 @@ class ConvLayerFn(torch.autograd.Function):
                 # eval-mode BN is a per-channel affine map: dy = da * act' * gamma * invstd
                 dy, _, _ = K.bn_backward(da, y, stats, gamma, beta, spec.act, spec.alpha, need_affine=False)
                 raise NotImplementedError("backward through eval-mode BatchNorm is not on the training path")
-            if dp.sync_bn():
+            if stats.dim() == 2:  # segmented call: BN backward per segment, one dy
+                dy, dgamma, dbeta = ConvLayerFn._seg_bn_backward(ctx, da, y, stats, gamma, beta, ng, nbeta)
+            elif dp.sync_bn():
                 sums, da_c = K.bn_backward_sums(da, y, stats, gamma, beta, spec.act, spec.alpha)
                 # dgamma/dbeta stay shard-local (from the pre-all-reduce sums): the bucketed
                 # gradient all-reduce sums them like every other parameter gradient
@@ -231,7 +258,33 @@ class ConvLayerFn(torch.autograd.Function):
                 dw = K.spectral_backward(w, dw, u, v, inv_sigma, spec.geom.transposed)
             if not nw:
                 dw = None
-        return dx, dw, db, dgamma, dbeta, None, None, None
+        return dx, dw, db, dgamma, dbeta, None, None, None, None
+
+    @staticmethod
+    def _seg_bn_backward(ctx, da, y, stats, gamma, beta, ng, nbeta):
+        spec = ctx.spec
+        if not K.is_nhwc(da):
+            da = da.contiguous(memory_format=torch.channels_last)
+        dy = torch.empty_like(y)
+        Bs = y.shape[0] // ctx.segs
+        P = Bs * y.shape[2] * y.shape[3]
+        C = y.shape[1]
+        dgamma = dbeta = None
+        for s_ in range(ctx.segs):
+            sl = slice(s_ * Bs, (s_ + 1) * Bs)
+            if dp.sync_bn():
+                sums, da_c = K.bn_backward_sums(da[sl], y[sl], stats[s_], gamma, beta, spec.act, spec.alpha)
+                dg = (sums[C:] * stats[s_, C:2 * C].double()).float() if ng and gamma is not None else None
+                db = sums[:C].float() if nbeta and beta is not None else None
+                dp.all_reduce_sum(sums)
+                K.bn_backward_apply(da_c, y[sl], stats[s_], gamma, beta, spec.act, spec.alpha, sums,
+                                    P * dp.world(), need_affine=False, out=dy[sl])
+            else:
+                _, dg, db = K.bn_backward(da[sl], y[sl], stats[s_], gamma, beta, spec.act, spec.alpha,
+                                          need_affine=ng or nbeta, out=dy[sl])
+            dgamma = dg if dgamma is None or dg is None else dgamma + dg
+            dbeta = db if dbeta is None or db is None else dbeta + db
+        return dy, dgamma, dbeta
 
     @staticmethod
     def _create_graph_backward(ctx, da, x, w, bias, gamma, beta, sn):
@@ -241,7 +294,7 @@ class ConvLayerFn(torch.autograd.Function):
         spec = ctx.spec
         slots = [i for i, t in enumerate((x, w, bias, gamma, beta))
                  if t is not None and ctx.needs_input_grad[i]]
-        out = [None] * 8
+        out = [None] * 9
         if not slots:
             return tuple(out)
         src = (x, w, bias, gamma, beta)

@@ -311,10 +311,12 @@ def bn_backward_sums(da, y, stats, gamma, beta, act="none", alpha=0.0):
     return sums, da
 
 
-def bn_backward_apply(da, y, stats, gamma, beta, act, alpha, sums, P_global, need_affine=True):
+def bn_backward_apply(da, y, stats, gamma, beta, act, alpha, sums, P_global, need_affine=True, out=None):
     P, C, sp, sc = _pc(y)
     _, _, dsp, dsc = _pc(da)
-    dy = torch.empty_like(y)
+    dy = torch.empty_like(y) if out is None else out
+    if dy.stride() != y.stride():
+        raise L.RganError("bn_backward_apply: out must have y's strides")
     dgamma = torch.empty(C, dtype=torch.float32, device=y.device) if need_affine and gamma is not None else None
     dbeta = torch.empty(C, dtype=torch.float32, device=y.device) if need_affine and beta is not None else None
     L.check(L.lib().rgan_bn_backward_apply(L.ptr(da), dsp, dsc, L.ptr(y), P, C, sp, sc, L.ptr(stats),
@@ -334,12 +336,14 @@ def bn_apply(y, stats, gamma, beta, act="none", alpha=0.0, out=None):
     return out
 
 
-def bn_backward(da, y, stats, gamma, beta, act="none", alpha=0.0, need_affine=True):
+def bn_backward(da, y, stats, gamma, beta, act="none", alpha=0.0, need_affine=True, out=None):
     if not is_nhwc(da):
         da = da.contiguous(memory_format=torch.channels_last)
     P, C, sp, sc = _pc(y)
     _, _, dsp, dsc = _pc(da)
-    dy = torch.empty_like(y)
+    dy = torch.empty_like(y) if out is None else out
+    if dy.stride() != y.stride():
+        raise L.RganError("bn_backward: out must have y's strides")
     dgamma = torch.empty(C, dtype=torch.float32, device=y.device) if need_affine and gamma is not None else None
     dbeta = torch.empty(C, dtype=torch.float32, device=y.device) if need_affine and beta is not None else None
     lib = L.lib()

@@ -22,6 +22,7 @@ import math
 import torch
 import torch.nn as nn
 
+from . import autograd as AG
 from .autograd import ConvLayerFn, LayerSpec
 from .kernels import ConvGeom, spectral_power
 
@@ -163,7 +164,7 @@ class _Layer:
                                nchw_out=nchw_out) if geom is not None else None)
         self.w_view, self.in_view, self.out_view = w_view, in_view, out_view
 
-    def run(self, h, training):
+    def run(self, h, training, segs=1):
         conv, bn = self.conv, self.bn
         w = conv.w if isinstance(conv, _ConvBase) else conv.weight
         if self.w_view is not None:
@@ -178,7 +179,7 @@ class _Layer:
             sn = (conv.weight_u.clone(), conv.weight_v.clone(), inv_sigma)
         bufs = (bn.running_mean, bn.running_var, bn.num_batches_tracked, training) if bn is not None else None
         out = ConvLayerFn.apply(h, w, conv.bias, bn.weight if bn is not None else None,
-                                bn.bias if bn is not None else None, self.spec, bufs, sn)
+                                bn.bias if bn is not None else None, self.spec, bufs, sn, segs)
         if self.out_view is not None:
             out = out.reshape(out.shape[0], *self.out_view)
         return out
@@ -190,11 +191,46 @@ def _lin_spec(layer, geom, act, alpha=0.0, nchw_out=False):
 
 
 class _Net(nn.Module):
+    @property
+    def _tag(self):
+        return type(self).__name__[1]  # "G" / "D": activation-trace tag (parity tests)
+
     def _run(self, x):
+        AG.TRACE_NET = self._tag
         h = x
         for layer in self._plan:
             h = layer.run(h, self.training)
         return h
+
+    @property
+    def segmentable(self):
+        """Several forward calls can share one batched pass (no spectral layer: the
+        reference runs one power iteration per call, so each call has its own sigma)."""
+        return not any(layer.spec is not None and layer.spec.spectral for layer in self._plan)
+
+    def forward_segments(self, xs):
+        """``[self(x) for x in xs]`` as ONE pass over the concatenated batch: every layer's
+        GEMMs run once over all segments, BatchNorm normalises (and updates its running
+        statistics) per segment in list order, exactly as the separate calls would."""
+        if not self.segmentable:
+            raise ValueError("forward_segments: a spectral-norm layer needs one call per forward")
+        n = len(xs)
+        B = xs[0].shape[0]
+        if any(x.shape != xs[0].shape for x in xs):
+            raise ValueError("forward_segments: segments must have equal shapes")
+        trace0 = len(AG.ACT_TRACE) if AG.ACT_TRACE is not None else 0
+        AG.TRACE_NET = self._tag
+        h = torch.cat(xs)
+        for layer in self._plan:
+            h = layer.run(h, self.training, n)
+        if AG.ACT_TRACE is not None:  # activation masks in the separate calls' order
+            masks = AG.ACT_TRACE[trace0:]
+            del AG.ACT_TRACE[trace0:]
+            del AG.ACT_TAGS[trace0:]
+            for s_ in range(n):
+                AG.ACT_TRACE.extend(m[s_ * B:(s_ + 1) * B] for m in masks)
+                AG.ACT_TAGS.extend(self._tag for _ in masks)
+        return list(h.split(B))
 
 
 # ---------------------------------------------------------------- arch 0 (DCGAN)
@@ -314,6 +350,11 @@ class _D0(_Net):
     def forward(self, x):
         return self._run(x).view(-1)
 
+    def forward_pair(self, x, x_fake):
+        """(D(x), D(x_fake)) in one batched pass (see ``forward_segments``)."""
+        a, b = self.forward_segments([x, x_fake])
+        return a.reshape(-1), b.reshape(-1)
+
 
 # ---------------------------------------------------------------- arch 1 ("standard CNN", 32x32)
 class _G1(_Net):
@@ -392,6 +433,10 @@ class _D1(_Net):
 
     def forward(self, x):
         return self._run(x).view(-1)
+
+    def forward_pair(self, x, x_fake):
+        a, b = self.forward_segments([x, x_fake])
+        return a.reshape(-1), b.reshape(-1)
 
 
 def DCGAN_G(param):

@@ -68,6 +68,8 @@ class Trainer:
         self._pending_G, self._pending_decay_G = None, False
         self.host_rng = getattr(p, "rgan_rng", "host") == "host"
         self.pac = getattr(p, "pac", 1)  # 2: code/GAN_losses_iter_PAC.py
+        # one batched D pass per D step where the nets allow it (--rgan_batch_D)
+        self.batch_D = bool(getattr(p, "rgan_batch_D", True)) and self.pac == 1 and self.D.segmentable
         self._fake_D = None
         self.errD = self.errG = None
         self.last = {}
@@ -152,8 +154,28 @@ class Trainer:
         for _ in range(p.Diters):
             D.zero_grad()
             x = self._real(feed, "x_D")
-            y_pred = D(x)
-            if kind <= 4:
+            if self.batch_D:
+                # D(x) and D(x_fake) as one batched pass (per-call BN statistics kept):
+                # the draws keep the reference's order (x, then z); D(x) does not read G
+                z = self._normal(feed, "z_D", zshape)
+                self.flush()
+                x_fake = self._generate_D(z)
+                y_pred, y_pred_fake = D.forward_pair(x, x_fake)
+                if kind <= 4:
+                    # err_real.backward(); err_fake.backward() accumulate = one backward of the sum
+                    err_real = loss_D_real(kind, y_pred)
+                    err_fake = loss_D_fake(kind, y_pred_fake)
+                    if not gp_on:
+                        self._arm(self.redD)
+                    (err_real + err_fake).backward()
+                    errD = err_real.detach() + err_fake.detach()
+                else:
+                    errD = loss_D(kind, y_pred, y_pred_fake)
+                    if not gp_on:
+                        self._arm(self.redD)
+                    errD.backward()
+            elif kind <= 4:
+                y_pred = D(x)
                 err_real = loss_D_real(kind, y_pred)
                 err_real.backward()
                 z = self._normal(feed, "z_D", zshape)
@@ -166,6 +188,7 @@ class Trainer:
                 err_fake.backward()
                 errD = err_real.detach() + err_fake.detach()
             else:
+                y_pred = D(x)
                 z = self._normal(feed, "z_D", zshape)
                 self.flush()
                 x_fake = self._generate_D(z)

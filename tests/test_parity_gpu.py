@@ -103,8 +103,8 @@ def oracle_exact_step(name, st):
         t.optG.load_state_dict(st["pre"]["optG"])
         t.optD.load_state_dict(st["pre"]["optD"])
     masks = []
-    hooks = [m.register_forward_hook(lambda mod, inp, out: masks.append((out.detach() > 0).clone()))
-             for net in (t.G, t.D) for m in net.modules()
+    hooks = [m.register_forward_hook(lambda mod, inp, out, tag=tag: masks.append((tag, (out.detach() > 0).clone())))
+             for net, tag in ((t.G, "G"), (t.D, "D")) for m in net.modules()
              if isinstance(m, (torch.nn.ReLU, torch.nn.LeakyReLU, torch.nn.SELU))]
     t.iteration(st["i"], feed={k: v.double() for k, v in _feed(st).items()})
     for h in hooks:
@@ -117,6 +117,7 @@ def gpu_step(t, st):
     from relativisticgan_amd import autograd
     got = {}
     autograd.ACT_TRACE = []
+    autograd.ACT_TAGS = []
     t.G.load_state_dict(st["pre"]["G"])
     t.D.load_state_dict(st["pre"]["D"])
     if st["pre"]["optG"]["state"]:
@@ -125,7 +126,7 @@ def gpu_step(t, st):
     try:
         t.iteration(st["i"], feed={k: v.to(DEV) for k, v in _feed(st).items()},
                     hooks=lambda tag, r: _cap(got, t, tag, r))
-        masks = autograd.ACT_TRACE
+        masks = list(zip(autograd.ACT_TAGS, autograd.ACT_TRACE))
     finally:
         autograd.ACT_TRACE = None
     got["postG"] = {k: v.detach().clone() for k, v in t.G.state_dict().items()}
@@ -136,13 +137,21 @@ def gpu_step(t, st):
     return out
 
 
+def per_net(trace):
+    """(tag, mask) entries -> per-net mask streams, call order kept within each net (the
+    GPU D step runs G(z) before its one batched D pass; the reference interleaves them)."""
+    return {tag: [m for t, m in trace if t == tag] for tag in ("G", "D")}
+
+
 def count_flips(ours, exact):
     """Activation-sign disagreements between the GPU and the exact forward passes."""
-    assert len(ours) == len(exact), f"activation trace length {len(ours)} vs {len(exact)}"
+    ours, exact = per_net(ours), per_net(exact)
     n = 0
-    for a, b in zip(ours, exact):
-        assert a.shape == b.shape, (a.shape, b.shape)
-        n += int((a != b).sum())
+    for tag in ("G", "D"):
+        assert len(ours[tag]) == len(exact[tag]), f"{tag} activation trace length {len(ours[tag])} vs {len(exact[tag])}"
+        for a, b in zip(ours[tag], exact[tag]):
+            assert a.shape == b.shape, (tag, a.shape, b.shape)
+            n += int((a != b).sum())
     return n
 
 

@@ -26,7 +26,7 @@ for net, nn_ in ((tt.G, "G"), (tt.D, "D")):
 tt.iteration(0, feed={k: v.double() for k, v in _feed(st).items()})
 for h in hooks:
     h.remove()
-ours = got["masks"]
+ours = [m for _, m in got["masks"]]  # (net tag, mask) entries
 print(len(ours), len(pre_acts))
 for k, ((key, z), m) in enumerate(zip(pre_acts, ours)):
     e = (z > 0)

@@ -31,7 +31,8 @@ def main():
     for st in steps:
         got = T.gpu_step(t, st)
         exact = T.oracle_exact_step(name, st)
-        per = [int((a != b).sum()) for a, b in zip(got["masks"], exact["masks"])]
+        go, ex = T.per_net(got["masks"]), T.per_net(exact["masks"])
+        per = [int((a != b).sum()) for tag in ("G", "D") for a, b in zip(go[tag], ex[tag])]
         print(f"== it{st['i']} flips per activation call: {per}")
         report = []
         errs = T.compare(p, st, got, exact, report, sum(per))
