@@ -1388,6 +1388,53 @@ __global__ __launch_bounds__(256) void pack_tiled(PackArgs a) {
   }
 }
 
+// 4x4 taps, Nin % 32 == 0, Nout % 8 == 0 (every C2 pack): the same brick moved with
+// float4s -- 4 taps per load (taps are the weight's contiguous index), 4 in-indices per
+// store (the packed row's contiguous index) -- 4 loads + 4 stores per thread, all issued
+// before their first use.
+constexpr int P4_LD = PK_O * 16 + 4;  // [in][out][16 taps], 16-B aligned rows
+__global__ __launch_bounds__(256) void pack_tiled16(PackArgs a) {
+  __shared__ __attribute__((aligned(16))) float t[PK_I * P4_LD];
+  const int Nin = (int)a.fpci.d, Nout = a.N, K = a.K;
+  const int i0 = blockIdx.x * PK_I, o0 = blockIdx.y * PK_O;
+  const bool in_fast = a.s_in < a.s_out;
+  float4 v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int e = threadIdx.x + 256 * r;  // float4 index in the brick
+    const int tq = e & 3;
+    const int i = in_fast ? (e >> 2) & (PK_I - 1) : e >> 5;
+    const int o = in_fast ? e >> 7 : (e >> 2) & (PK_O - 1);
+    v[r] = *reinterpret_cast<const float4*>(a.W + (long long)(i0 + i) * a.s_in + (long long)(o0 + o) * a.s_out +
+                                            4 * tq);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int e = threadIdx.x + 256 * r;
+    const int tq = e & 3;
+    const int i = in_fast ? (e >> 2) & (PK_I - 1) : e >> 5;
+    const int o = in_fast ? e >> 7 : (e >> 2) & (PK_O - 1);
+    *reinterpret_cast<float4*>(t + i * P4_LD + o * 16 + 4 * tq) = v[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int e = threadIdx.x + 256 * r;
+    const int iq = e & 7, o = (e >> 3) & (PK_O - 1), tap = e >> 6;
+    const int kh = tap >> 2, kw = tap & 3;
+    int phase = 0, kt;
+    if (a.convt2) {  // tap (kh, kw) of phase (ph, pw) = (2th+1-ph, 2tw+1-pw)
+      phase = (1 - (kh & 1)) * 2 + (1 - (kw & 1));
+      kt = (kh >> 1) * 2 + (kw >> 1);
+    } else {
+      kt = a.flip ? 15 - tap : tap;
+    }
+    const float* src = t + (4 * iq) * P4_LD + o * 16 + tap;
+    *reinterpret_cast<float4*>(a.out + ((size_t)phase * Nout + o0 + o) * K + (size_t)kt * Nin + i0 + 4 * iq) =
+        make_float4(src[0], src[P4_LD], src[2 * P4_LD], src[3 * P4_LD]);
+  }
+}
+
 // ---------------------------------------------------------------- host planning
 enum { CFG_L = 0, CFG_M = 1, CFG_N = 2 };
 
@@ -1792,7 +1839,11 @@ static void launch_pack(const PackArgs& a, hipStream_t s) {
   // tiled when n is one weight index and the taps are contiguous in W
   if (a.fnco.d == (uint32_t)a.N && a.fnkw.d == 1 && a.s_kw == 1 && a.s_kh == a.KW && a.KH * a.KW <= 16 &&
       (!a.convt2 || (a.KH == 4 && a.KW == 4))) {
-    pack_tiled<<<dim3(ceil_div((int)a.fpci.d, PK_I), ceil_div(a.N, PK_O)), 256, 0, s>>>(a);
+    if (a.KH == 4 && a.KW == 4 && a.fpci.d % PK_I == 0 && a.N % PK_O == 0 && a.s_in % 4 == 0 && a.s_out % 4 == 0 &&
+        aligned16(a.W) && aligned16(a.out))
+      pack_tiled16<<<dim3((int)a.fpci.d / PK_I, a.N / PK_O), 256, 0, s>>>(a);
+    else
+      pack_tiled<<<dim3(ceil_div((int)a.fpci.d, PK_I), ceil_div(a.N, PK_O)), 256, 0, s>>>(a);
     return;
   }
   const int ny = std::min(a.N, 8192);
