@@ -36,6 +36,9 @@ constexpr long long FAST_MAX_BYTES = (1LL << 31) - (1LL << 24);
 
 enum { MODE_CONV = 0, MODE_CONVT2 = 1, MODE_WGRAD = 2, MODE_NARROW_T = 3, MODE_NARROW_IN = 4, MODE_DENSE1 = 5 };
 constexpr int BK = 32;
+#ifndef RGAN_XGROUP
+#define RGAN_XGROUP 1
+#endif
 
 // n / d for 0 <= n < 2^31 via multiply-high (host-computed magic numbers)
 struct FastDiv {
@@ -87,6 +90,7 @@ struct GemmArgs {
   // FAST paths (raw buffer loads, scalar per-tile offsets): descriptor sizes in bytes
   int a_bytes, im_bytes, bw_bytes;
   int vec_out;            // output n-quads contiguous and 16-B aligned (host-checked)
+  int xgroup, nph;        // XCD-grouped tile order (blocks sharing A rows on one XCD); phases
 };
 
 __device__ __forceinline__ long long row_offset(const OutMap& o, int m, int phase) {
@@ -144,11 +148,28 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = (wid / WN) * (BM / WM), wn = (wid % WN) * (BN / WN);
-  const int tile = blockIdx.x;
-  const int tm_i = tile / g.tiles_n, tn_i = tile - tm_i * g.tiles_n;
+  // Tile order.  Default: x = (m tile, n tile), z = (phase, split).  xgroup: blocks are
+  // dispatched round-robin over the 8 XCDs, so the blocks that read the same A rows (the
+  // n tiles and sub-pixel phases of one m tile) are put 8 dispatch slots apart -- one XCD,
+  // one L2 -- instead of on 4-8 different L2s.
+  int tm_i, tn_i, phase, split, z;
+  if (g.xgroup) {
+    const int b = blockIdx.x, r = b >> 3, per = g.tiles_n * g.nph;
+    const int q = r % per;
+    tm_i = (r / per) * 8 + (b & 7);
+    tn_i = q % g.tiles_n;
+    phase = q / g.tiles_n;
+    split = blockIdx.z;
+    z = phase * g.splits + split;
+  } else {
+    const int tile = blockIdx.x;
+    tm_i = tile / g.tiles_n;
+    tn_i = tile - tm_i * g.tiles_n;
+    z = blockIdx.z;
+    phase = z / g.splits;
+    split = z - phase * g.splits;
+  }
   const int m0 = tm_i * BM, n0 = tn_i * BN;
-  const int z = blockIdx.z;
-  const int phase = z / g.splits, split = z - phase * g.splits;
   const int kbeg = split * g.ksplit;
   const int kend = min(g.K, kbeg + g.ksplit);
   const int nk = (kend - kbeg + BK - 1) / BK;
@@ -2033,7 +2054,11 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   }
   int bm, bn;
   tile_dims(p.cfg, bm, bn);
-  dim3 grid(ceil_div(p.g.M, bm) * p.g.tiles_n, 1, p.phases * p.g.splits);
+  const int tiles_m = ceil_div(p.g.M, bm);
+  p.g.nph = p.phases;
+  p.g.xgroup = RGAN_XGROUP && p.fast && p.mode != MODE_WGRAD && tiles_m % 8 == 0 && p.g.tiles_n * p.phases > 1;
+  dim3 grid = p.g.xgroup ? dim3(tiles_m * p.g.tiles_n * p.phases, 1, p.g.splits)
+                         : dim3(tiles_m * p.g.tiles_n, 1, p.phases * p.g.splits);
   ProfRec rec{};
   const bool prof = g_prof && g_recs.size() * 2 + 2 <= g_pool.size();
   if (prof) {
