@@ -60,8 +60,9 @@ def make_parser(script="GAN_losses_iter"):
                    help="which reference script's defaults/behaviour to follow")
     p.add_argument("--rgan_rng", choices=("host", "device"), default="host")
     p.add_argument("--rgan_sync_bn", type="bool", default=False)
-    p.add_argument("--rgan_batch_D", type="bool", default=True,
-                   help="run the D step's D(x) and D(x_fake) as one batched pass (per-call BN kept)")
+    p.add_argument("--rgan_batch_D", type="bool", default=None,
+                   help="run the D step's D(x) and D(x_fake) as one batched pass (per-call BN kept); "
+                        "default: on for 1 process, off under data parallelism")
     p.add_argument("--rgan_pac", dest="pac", type=int, default=2 if script == "GAN_losses_iter_PAC" else 1,
                    choices=(1, 2),
                    help="2 = PacGAN-2, the reference's code/GAN_losses_iter_PAC.py (D sees 2 samples packed "

@@ -68,8 +68,12 @@ class Trainer:
         self._pending_G, self._pending_decay_G = None, False
         self.host_rng = getattr(p, "rgan_rng", "host") == "host"
         self.pac = getattr(p, "pac", 1)  # 2: code/GAN_losses_iter_PAC.py
-        # one batched D pass per D step where the nets allow it (--rgan_batch_D)
-        self.batch_D = bool(getattr(p, "rgan_batch_D", True)) and self.pac == 1 and self.D.segmentable
+        # one batched D pass per D step where the nets allow it (--rgan_batch_D).  Default
+        # (auto): single process only -- under DP the separate D(x) forward is what hides
+        # G's deferred gradient all-reduce (flush), and the batched pass needs G(z) first
+        bd = getattr(p, "rgan_batch_D", None)
+        bd = (self.world == 1) if bd is None else bool(bd)
+        self.batch_D = bd and self.pac == 1 and self.D.segmentable
         self._fake_D = None
         self.errD = self.errG = None
         self.last = {}
