@@ -90,6 +90,20 @@ int rgan_conv_wgrad(const RganConv* d, const float* x, const float* dy, float* d
 int rgan_nn_fold_weight(const float* w, int cout, int cin, float* wt, void* stream);
 int rgan_nn_unfold_grad(const float* dwt, int cout, int cin, float* dw, void* stream);
 
+/* ---- image layers (k4 s2 p1 with <= 4 image channels: GLI:404 D start, GLI:386 G end) ----
+ * rgan_patches_k4s2: patch matrix of an image [B][C][H][W] (element strides b,c,h,w; C <= 4,
+ * H, W even) on the half-size grid: X[(b, i, j)][4 t + c] = img[b][c][2i-1+kh][2j-1+kw],
+ * t = 4 kh + kw, zero outside the image and for c >= C; X is [B*(H/2)*(W/2)][64] floats,
+ * 16-byte aligned.  Every image-layer GEMM then runs as a 1x1 rgan_conv_* over X.
+ * rgan_patch_weight: W1[o][4 t + c] = w[o*row_stride + c*channel_stride + t] (rows x 64).
+ * rgan_unpatch_grad: dw[o][c][t] = g1[o*row_stride + (4 t + c)*col_stride] (rows x C x 16). */
+int rgan_patches_k4s2(const float* img, int batch, int channels, int height, int width,
+                      const long long* strides, float* patches, void* stream);
+int rgan_patch_weight(const float* w, int rows, int channels, long long row_stride, long long channel_stride,
+                      float* w1, void* stream);
+int rgan_unpatch_grad(const float* g1, int rows, int channels, long long row_stride, long long col_stride,
+                      float* dw, void* stream);
+
 /* ---- image export (GLI:563-565 sample grid, GLI:759-768 extra FID images) ----
  * torchvision.utils.save_image's float -> uint8 step on the device: t = x*scale + shift;
  * optional normalize with range = device float[2] {min, max} of the batch

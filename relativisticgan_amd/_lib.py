@@ -35,6 +35,9 @@ _SIGS = {
     "rgan_conv_dgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "rgan_conv_wgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "rgan_nn_fold_weight": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    "rgan_patches_k4s2": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
+    "rgan_patch_weight": (c_int, [c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp]),
+    "rgan_unpatch_grad": (c_int, [c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp]),
     "rgan_nn_unfold_grad": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
     "rgan_gather_images_u8": (c_int, [c_vp, c_vp, c_int, c_ll, c_vp, c_vp]),
     "rgan_minmax_ws_bytes": (c_sz, [c_ll]),

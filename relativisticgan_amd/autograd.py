@@ -15,6 +15,8 @@ plus torch tensor algebra for the per-channel BN normalisation and the activatio
 and differentiated with ``torch.autograd.grad``; ``gp.backward()`` then runs through
 those pieces.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -25,6 +27,11 @@ from . import kernels as K
 # Test/diagnostic hook: when a list, every fused layer whose activation has a derivative
 # discontinuous at 0 (ReLU, LeakyReLU, SELU) appends the sign mask of its output, in call
 # order, so parity tests can count sign flips against an exact (fp64) forward.
+# Image-layer gradients (k4 s2 p1, <= 4 image channels) as 1x1 GEMMs over a patch matrix
+# (kernels.patches_k4s2); the forwards keep the direct narrow kernels (as fast: both are
+# bound by writing the 128-channel side).  False = narrow kernels / implicit GEMM throughout.
+PATCH_IMAGE_LAYERS = os.environ.get("RGAN_PATCH_IMAGE", "1") != "0"
+
 ACT_TRACE = None
 ACT_TAGS = []      # per ACT_TRACE entry: the net that produced it ("G" / "D", set by nets._Net)
 TRACE_NET = None
@@ -249,16 +256,46 @@ class ConvLayerFn(torch.autograd.Function):
             dy = K.act_backward(da, t5, spec.act, spec.alpha)
         else:
             dy = da
-        dx = K.conv_dgrad(dy, w, spec.geom, tuple(x.shape), wscale=wscale, like=x, cache=True) if nx else None
-        dw = db = None
+        if ConvLayerFn._patch_conv(spec, x):
+            # image-side Conv2d (D's first layer; the forward ran the direct narrow kernel):
+            # the weight gradient is a 1x1 GEMM over the image's patch matrix
+            dx = K.conv_dgrad(dy, w, spec.geom, tuple(x.shape), wscale=wscale, like=x, cache=True) if nx else None
+            dw = db = None
+            if nw or nb:
+                g1, db = K.conv_wgrad(K.patches_k4s2(x), dy, K.G1X1, (w.shape[0], 64, 1, 1),
+                                      with_bias=bias is not None and nb)
+                dw = K.unpatch_grad(g1, w.shape[0], w.shape[1], 64, 1)
+        elif ConvLayerFn._patch_convt(spec, w, bias):
+            # image-side ConvTranspose2d (G's last layer): both gradients are 1x1 GEMMs over
+            # the patch matrix of the image gradient, on x's grid
+            Xg = K.patches_k4s2(dy)
+            dx = K.conv_fwd(Xg, K.PATCHW.get(w, True), K.G1X1, wscale=wscale, cache=True) if nx else None
+            dw = db = None
+            if nw:
+                g1, _ = K.conv_wgrad(Xg, x, K.G1X1, (w.shape[0], 64, 1, 1))
+                dw = K.unpatch_grad(g1, w.shape[0], w.shape[1], 64, 1)
+        else:
+            dx = K.conv_dgrad(dy, w, spec.geom, tuple(x.shape), wscale=wscale, like=x, cache=True) if nx else None
+            dw = db = None
+            if nw or nb:
+                dw, db = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), with_bias=bias is not None and nb)
         if nw or nb:
-            dw, db = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), with_bias=bias is not None and nb)
             if spec.spectral and nw:
                 u, v, inv_sigma = sn
                 dw = K.spectral_backward(w, dw, u, v, inv_sigma, spec.geom.transposed)
             if not nw:
                 dw = None
         return dx, dw, db, dgamma, dbeta, None, None, None, None
+
+    @staticmethod
+    def _patch_conv(spec, x):
+        return (PATCH_IMAGE_LAYERS and not spec.geom.transposed and not spec.bn and K.patchable(spec.geom, x.shape[1])
+                and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0)
+
+    @staticmethod
+    def _patch_convt(spec, w, bias):
+        return (PATCH_IMAGE_LAYERS and spec.geom.transposed and not spec.bn and bias is None
+                and K.patchable(spec.geom, w.shape[1]))
 
     @staticmethod
     def _seg_bn_backward(ctx, da, y, stats, gamma, beta, ng, nbeta):

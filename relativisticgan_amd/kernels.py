@@ -122,18 +122,20 @@ PACKS = _PackCache()
 class _FoldCache:
     """Folded --NN_conv weights (Wt = A W A^T), one per (weight, version): like the packs,
     refolded only after an optimizer step.  A new Wt tensor is made per version so the
-    pack cache (keyed by the Wt object) never sees a stale layout."""
+    pack cache (keyed by the Wt object) never sees a stale layout.  ``fn`` is the fold
+    (nn_fold here; the image-layer patch weights use their own instance)."""
 
-    def __init__(self):
+    def __init__(self, fn=None):
         self.entries = {}
+        self.fn = fn
 
-    def get(self, w):
+    def get(self, w, *args):
         base = w._base if w._base is not None else w
-        key = id(base)
+        key = (id(base),) + args
         ent = self.entries.get(key)
         if ent is not None and ent[0]() is base and ent[1] == w._version and ent[2] == w.data_ptr():
             return ent[3]
-        wt = nn_fold(w)
+        wt = (self.fn or nn_fold)(w, *args)
         self.entries[key] = (weakref.ref(base, self._drop(key)), w._version, w.data_ptr(), wt)
         return wt
 
@@ -149,6 +151,48 @@ class _FoldCache:
 
 
 FOLDS = _FoldCache()
+
+
+# ------------------------------------------------------------------ image layers as 1x1 GEMMs
+G1X1 = ConvGeom(1, 1, 0, False)
+
+
+def patchable(geom, cin_img):
+    """k4 s2 p1 layer whose image side has <= 4 channels (D's first conv, G's last convT)."""
+    return (geom.k, geom.stride, geom.pad, geom.upsample) == (4, 2, 1, 1) and cin_img <= 4
+
+
+def patches_k4s2(img):
+    """Patch matrix of an image [B][C][H][W] (any strides, C <= 4) on the half-size grid,
+    as an NHWC [B, 64, H/2, W/2] tensor (rgan_patches_k4s2)."""
+    L.require_cuda(img)
+    _f32(img)
+    B, C, H, W = img.shape
+    X = empty_nhwc(B, 64, H // 2, W // 2, img.device)
+    st = (L.c_ll * 4)(*img.stride())
+    L.check(L.lib().rgan_patches_k4s2(L.ptr(img), B, C, H, W, st, L.ptr(X), L.stream()), "rgan_patches_k4s2")
+    return X
+
+
+def patch_weight(w, transposed):
+    """Image-layer weight -> the 1x1 GEMM weight [O][64][1][1], W1[o][4t+c] = W[o][c][t]:
+    Conv2d [co][ci][4][4] (o = co, c = ci) or ConvTranspose2d [ci][co][4][4] (o = ci, c = co)."""
+    wc = w.contiguous()
+    O, C = wc.shape[0], wc.shape[1]
+    w1 = torch.empty((O, 64, 1, 1), dtype=torch.float32, device=w.device)
+    L.check(L.lib().rgan_patch_weight(L.ptr(wc), O, C, C * 16, 16, L.ptr(w1), L.stream()), "rgan_patch_weight")
+    return w1
+
+
+PATCHW = _FoldCache(patch_weight)
+
+
+def unpatch_grad(g1, O, C, row_stride, col_stride):
+    """1x1-GEMM weight gradient -> torch layout [O][C][4][4] (dw[o][c][t] = g1[o*rs + (4t+c)*cs])."""
+    dw = torch.empty((O, C, 4, 4), dtype=torch.float32, device=g1.device)
+    L.check(L.lib().rgan_unpatch_grad(L.ptr(g1), O, C, row_stride, col_stride, L.ptr(dw), L.stream()),
+            "rgan_unpatch_grad")
+    return dw
 
 
 def nn_fold(w):

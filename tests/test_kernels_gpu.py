@@ -159,6 +159,47 @@ def test_conv_dense_one_output(K, case):
     assert _rel(db, dy.double().cpu().sum((0, 2, 3))) < 1e-6
 
 
+@pytest.mark.parametrize("C", [1, 3, 4])
+@pytest.mark.parametrize("layout", ["nchw", "nhwc"])
+def test_image_layer_patches(K, C, layout):
+    """Patch matrix X[(b,i,j)][4t+c] of a k4 s2 p1 window vs torch unfold, and the image
+    layers run as 1x1 GEMMs over it (conv fwd / wgrad, convT dgrad / wgrad) vs torch fp64."""
+    torch.manual_seed(C)
+    img = torch.randn(3, C, 10, 12, device=DEV)
+    if layout == "nhwc":
+        img = _nhwc(img)
+    X = K.patches_k4s2(img)
+    assert X.shape == (3, 64, 5, 6) and K.is_nhwc(X)
+    cols = F.unfold(img.double().cpu(), 4, padding=1, stride=2)          # [B, C*16, 30], (c, t)
+    ref = cols.view(3, C, 16, 30).permute(0, 3, 2, 1)                   # [B, p, t, c]
+    got = X.double().cpu().permute(0, 2, 3, 1).reshape(3, 30, 16, 4)    # [B, p, t, 4]
+    assert torch.equal(got[..., :C], ref)
+    assert not got[..., C:].any()
+    # D's first conv as a 1x1 GEMM over X, and its weight gradient
+    g = K.ConvGeom(4, 2, 1, False)
+    w = torch.nn.Parameter(torch.randn(40, C, 4, 4, device=DEV) * 0.1)
+    y = K.conv_fwd(X, K.patch_weight(w, False), K.G1X1)
+    assert _rel(y, _ref_conv(img, w, g)) < 2e-6
+    dy = _nhwc(torch.randn(3, 40, 5, 6, device=DEV))
+    g1, _ = K.conv_wgrad(X, dy, K.G1X1, (40, 64, 1, 1))
+    x64 = img.double().cpu()
+    w64 = w.detach().double().cpu().requires_grad_(True)
+    F.conv2d(x64, w64, stride=2, padding=1).backward(dy.double().cpu())
+    assert _rel(K.unpatch_grad(g1, 40, C, 64, 1), w64.grad) < 2e-6
+    # G's last convT: x [3, 40, 5, 6] -> image [3, C, 10, 12]; gradients over Xg = patches(dimg)
+    gt = K.ConvGeom(4, 2, 1, True)
+    wt = torch.randn(40, C, 4, 4, device=DEV) * 0.1
+    x = _nhwc(torch.randn(3, 40, 5, 6, device=DEV))
+    dimg = torch.randn(3, C, 10, 12, device=DEV)
+    Xg = K.patches_k4s2(dimg)
+    xr = x.double().cpu().requires_grad_(True)
+    wr = wt.double().cpu().requires_grad_(True)
+    F.conv_transpose2d(xr, wr, stride=2, padding=1).backward(dimg.double().cpu())
+    assert _rel(K.conv_fwd(Xg, K.patch_weight(wt, True), K.G1X1), xr.grad) < 2e-6
+    g1, _ = K.conv_wgrad(Xg, x, K.G1X1, (40, 64, 1, 1))
+    assert _rel(K.unpatch_grad(g1, 40, C, 64, 1), wr.grad) < 2e-6
+
+
 @pytest.mark.parametrize("nc", [1, 2, 3, 4])
 def test_conv_narrow_paths(K, nc):
     """Narrow kernels: ConvT k4s2p1 with nc outputs (and the Conv2d dgrad of that shape),

@@ -37,7 +37,8 @@ def wrap(name, fn, shape_of):
         r[0] += 1
         r[1] += pr["ms"]
         r[2] += pr["flops"]
-        r[3] = ",".join(k["name"].split("<")[1].split(">")[0] for k in pr["kernels"])
+        r[3] = ",".join((k["name"].split("<")[1].split(">")[0] if "<" in k["name"] else k["name"].split("(")[0])
+                        for k in pr["kernels"])
         return out
     return f
 
