@@ -70,6 +70,19 @@ int rgan_conv_fwd(const RganConv* d, const float* x, const float* w, const float
                   const float* wscale, const float* bias, float* y, int act, float act_alpha,
                   void* ws, size_t ws_bytes, void* stream);
 
+/* Conv2d/ConvTranspose2d.forward feeding a train-mode BatchNorm2d (GLI:361-366,387-391,
+ * 428-433): y = conv(x, w) * (*wscale) + bias, and -- when the GEMM's vector epilogue
+ * covers the layer -- the BatchNorm batch statistics of y as per-64-row segment moments
+ * bn_part[S][2][C] = (sum y, sum y^2) in double, computed from the finished tile in LDS (no re-read of y).
+ * S = rgan_conv_bn_segments(d, segs) (0: the epilogue cannot, use rgan_bn_stats); `segs`
+ * equal batch segments are kept apart (the batched D(x)/D(G(z)) call: segment k's rows are
+ * segments [k*S/segs, (k+1)*S/segs)).  *fused (host int) = 1 when bn_part was written.
+ * Merge with rgan_bn_segment_stats. */
+long long rgan_conv_bn_segments(const RganConv* d, int segs);
+int rgan_conv_fwd_bn(const RganConv* d, const float* x, const float* w, const float* wpacked,
+                     const float* wscale, const float* bias, float* y, void* ws, size_t ws_bytes,
+                     double* bn_part, long long part_segments, int segs, int* fused, void* stream);
+
 /* dx = d conv / d x applied to dy  (aten convolution_backward, grad_input). */
 int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* w, const float* wpacked,
                     const float* wscale, float* dx, void* ws, size_t ws_bytes, void* stream);
@@ -132,6 +145,12 @@ size_t rgan_bn_partial_bytes(long long P, int C);
 int rgan_bn_stats(const float* y, long long P, int C, long long sp, long long sc,
                   float eps, float momentum, float* running_mean, float* running_var,
                   long long* num_batches_tracked, float* stats, void* partial, void* stream);
+/* rgan_conv_fwd_bn's segment moments [s0, s1) -> stats + running stats (moments == NULL),
+ * or this rank's (count, mean, M2) double[3*C] for SyncBN (moments != NULL, as
+ * rgan_bn_moments).  Chan merges in a fixed order (deterministic). */
+int rgan_bn_segment_stats(const double* part, long long s0, long long s1, int C, int seg_rows,
+                          float eps, float momentum, float* running_mean, float* running_var,
+                          long long* num_batches_tracked, float* stats, double* moments, void* stream);
 /* a = act(gamma * (y - mean) * invstd + beta)  (torch's alpha/beta form) */
 int rgan_bn_apply(const float* y, long long P, int C, long long sp, long long sc,
                   const float* stats, const float* gamma, const float* beta,

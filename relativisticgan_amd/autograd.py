@@ -159,10 +159,16 @@ class _AllReduceSum(torch.autograd.Function):
 
 
 # ---------------------------------------------------------------- fused layer
-def _train_stats(y, spec, rm, rv, nbt):
+def _train_stats(y, spec, rm, rv, nbt, seg=None):
+    """Batch statistics of y; ``seg`` = (part, s0, s1): the conv epilogue's segment moments
+    covering y (rgan_conv_fwd_bn) replace the separate moments pass over y."""
+    C = y.shape[1]
     if dp.sync_bn():
-        mom = dp.all_gather_cat(K.bn_moments(y))
-        return K.bn_finalize(mom, dp.world(), y.shape[1], spec.eps, spec.momentum, rm, rv, nbt)
+        mom = K.bn_segment_moments(seg[0], seg[1], seg[2], C) if seg is not None else K.bn_moments(y)
+        mom = dp.all_gather_cat(mom)
+        return K.bn_finalize(mom, dp.world(), C, spec.eps, spec.momentum, rm, rv, nbt)
+    if seg is not None:
+        return K.bn_segment_stats(seg[0], seg[1], seg[2], C, spec.eps, spec.momentum, rm, rv, nbt)
     return K.bn_stats(y, spec.eps, spec.momentum, rm, rv, nbt)
 
 
@@ -182,8 +188,11 @@ class ConvLayerFn(torch.autograd.Function):
         wscale = sn[2] if spec.spectral else None
         stats_eval = None
         if spec.bn:
-            y = K.conv_fwd(x, w, spec.geom, bias=bias, wscale=wscale, cache=True)
             rm, rv, nbt, training = bufs
+            if training:
+                y, part, S = K.conv_fwd_bn(x, w, spec.geom, bias=bias, wscale=wscale, cache=True, segs=segs)
+            else:
+                y, part, S = K.conv_fwd(x, w, spec.geom, bias=bias, wscale=wscale, cache=True), None, 0
             C = y.shape[1]
             if training and segs > 1:
                 Bs = y.shape[0] // segs
@@ -191,12 +200,13 @@ class ConvLayerFn(torch.autograd.Function):
                 st = []
                 for s_ in range(segs):
                     sl = slice(s_ * Bs, (s_ + 1) * Bs)
-                    st.append(_train_stats(y[sl], spec, rm, rv, nbt))
+                    seg = (part, s_ * S // segs, (s_ + 1) * S // segs) if part is not None else None
+                    st.append(_train_stats(y[sl], spec, rm, rv, nbt, seg))
                     K.bn_apply(y[sl], st[-1], gamma, beta, spec.act, spec.alpha, out=a[sl])
                 stats = torch.stack(st)
             else:
                 if training:
-                    stats = _train_stats(y, spec, rm, rv, nbt)
+                    stats = _train_stats(y, spec, rm, rv, nbt, (part, 0, S) if part is not None else None)
                 else:
                     stats = torch.cat([rm, torch.rsqrt(rv + spec.eps)])
                     stats_eval = (rm, stats[C:])

@@ -199,6 +199,90 @@ __global__ __launch_bounds__(1024) void bn_merge(const double* __restrict__ part
   }
 }
 
+// Segment sums written by the conv GEMM's epilogue (rgan_conv_fwd_bn): [S][2][C] = (sum y,
+// sum y^2) of 64-row segments, in double -> moments of segments [s0, s1).  Block = 4
+// channels x 256 lanes: lane r sums segments s0 + r, s0 + r + 256, ... (loads issued 4
+// ahead), then a fixed-order LDS tree adds the 256 lane sums (deterministic).  Unshifted
+// double sums: var = (S2 - S1^2/n)/n loses ~1e-16 * mean^2/var relative -- far inside fp32
+// (the moments pass over y keeps its shifted sums; it has no segment structure to exploit).
+//   FIN 1: moments [3][C] (count, mean, M2) (SyncBN stage 1)
+//   FIN 2: (mean, invstd) stats + running-stat update, as bn_merge<2>
+constexpr int SEG_CPB = 4, SEG_LANES = 256;
+
+template <int FIN>
+__global__ __launch_bounds__(1024) void bn_seg_merge(const double* __restrict__ part, long long s0, long long s1,
+                                                     int C, double seg_n, double* __restrict__ out, float eps,
+                                                     float momentum, float* running_mean, float* running_var,
+                                                     long long* nbt, float* stats) {
+  __shared__ double sh[2][SEG_LANES][SEG_CPB];
+  const int cl = threadIdx.x % SEG_CPB, r = threadIdx.x / SEG_CPB;
+  const int c = blockIdx.x * SEG_CPB + cl;
+  double a1 = 0.0, a2 = 0.0;
+  if (c < C) {
+    long long k = s0 + r;
+    for (; k + 3 * SEG_LANES < s1; k += 4 * SEG_LANES) {
+      double v[4][2];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u][0] = part[((size_t)(k + u * SEG_LANES) * 2 + 0) * C + c];
+        v[u][1] = part[((size_t)(k + u * SEG_LANES) * 2 + 1) * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { a1 += v[u][0]; a2 += v[u][1]; }
+    }
+    for (; k < s1; k += SEG_LANES) {
+      a1 += part[((size_t)k * 2 + 0) * C + c];
+      a2 += part[((size_t)k * 2 + 1) * C + c];
+    }
+  }
+  sh[0][r][cl] = a1;
+  sh[1][r][cl] = a2;
+  __syncthreads();
+  for (int h = SEG_LANES / 2; h > 0; h >>= 1) {
+    if (r < h) {
+      sh[0][r][cl] += sh[0][r + h][cl];
+      sh[1][r][cl] += sh[1][r + h][cl];
+    }
+    __syncthreads();
+  }
+  if constexpr (FIN == 2) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
+  }
+  if (r != 0 || c >= C) return;
+  const double n = seg_n * (double)(s1 - s0), S1 = sh[0][0][cl], S2 = sh[1][0][cl];
+  const double mean = S1 / n, m2 = fmax(S2 - S1 * mean, 0.0);
+  if constexpr (FIN == 1) {
+    out[c] = n;
+    out[C + c] = mean;
+    out[2 * C + c] = m2;
+  } else {
+    const double var = m2 / n;
+    stats[c] = (float)mean;
+    stats[C + c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    if (running_var) {
+      const float unb = n > 1.0 ? (float)(m2 / (n - 1.0)) : (float)var;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+    }
+  }
+}
+
+extern "C" int rgan_bn_segment_stats(const double* part, long long s0, long long s1, int C, int seg_rows,
+                                     float eps, float momentum, float* running_mean, float* running_var,
+                                     long long* num_batches_tracked, float* stats, double* moments, void* stream) {
+  RGAN_REQUIRE(part && s1 > s0 && s0 >= 0 && C > 0 && seg_rows > 0 && (stats || moments));
+  const hipStream_t s = (hipStream_t)stream;
+  const int blocks = ceil_div(C, SEG_CPB);
+  if (moments)
+    bn_seg_merge<1><<<blocks, 1024, 0, s>>>(part, s0, s1, C, (double)seg_rows, moments, 0.f, 0.f, nullptr,
+                                            nullptr, nullptr, nullptr);
+  else
+    bn_seg_merge<2><<<blocks, 1024, 0, s>>>(part, s0, s1, C, (double)seg_rows, nullptr, eps, momentum,
+                                            running_mean, running_var, num_batches_tracked, stats);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
 // merge `nranks` moment blocks [r][3][C] in rank order -> (mean, invstd) float, running stats
 __global__ void bn_finalize_kernel(const double* __restrict__ mom, int nranks, int C, float eps, float momentum,
                                    float* running_mean, float* running_var, long long* nbt, float* stats) {

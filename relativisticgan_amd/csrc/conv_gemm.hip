@@ -91,6 +91,7 @@ struct GemmArgs {
   int a_bytes, im_bytes, bw_bytes;
   int vec_out;            // output n-quads contiguous and 16-B aligned (host-checked)
   int xgroup, nph;        // XCD-grouped tile order (blocks sharing A rows on one XCD); phases
+  double* bnp;            // nullable: BatchNorm moments of every 64-row output segment (vector epilogue)
 };
 
 __device__ __forceinline__ long long row_offset(const OutMap& o, int m, int phase) {
@@ -748,6 +749,26 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
           }
       }
       __syncthreads();
+      if (!slab_out && g.bnp) {
+        // BatchNorm batch statistics in the epilogue: the wave's 64 finished rows of column
+        // `lane` (one channel; conflict-free LDS row reads) -> (sum y, sum y^2) of the
+        // segment in double (fp32 products are exact in double; the merge is a plain
+        // fixed-order sum).  Host guarantees M % 64 == 0 and n == channel; segment =
+        // (phase, m / 64).
+        const int mrow = m0 + wm, col = n0 + wn + lane;
+        if (mrow < g.M && col < g.N) {
+          double s1 = 0.0, s2 = 0.0;
+#pragma unroll 8
+          for (int rl = 0; rl < 64; ++rl) {
+            const double d = (double)T[rl * EP_LD + lane];
+            s1 += d;
+            s2 += d * d;
+          }
+          const size_t seg = (size_t)phase * (uint32_t)(g.M >> 6) + (uint32_t)(mrow >> 6);
+          g.bnp[(seg * 2) * g.N + col] = s1;
+          g.bnp[(seg * 2 + 1) * g.N + col] = s2;
+        }
+      }
       const int q = lane & 15, n = n0 + wn + 4 * q;
       if (n < g.N) {
         float* slab = slab_out ? g.slab + (size_t)z * g.M * g.N : nullptr;
@@ -1479,6 +1500,11 @@ struct Plan {
   // one-output dense layer (MODE_DENSE1): which = 0 fwd, 1 dgrad, 2 wgrad
   DenseArgs da{};
   int dense_op = 0;
+  // BatchNorm moments in the vector epilogue (rgan_conv_fwd_bn): caller's [S][2][C] buffer,
+  // equal batch segments whose statistics are kept apart, and whether the launch wrote them
+  double* bn_part = nullptr;
+  int bn_segs = 1;
+  bool bn_fused = false;
 };
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
@@ -1996,6 +2022,20 @@ static void run_dense1(const Plan& p, const float* packed, hipStream_t s) {
   }
 }
 
+// The vector epilogue can emit BatchNorm segment moments: 128x128 FAST tiles written whole
+// (no split-K slab, no tap staging), column n = output channel, 64-row segments that never
+// straddle a phase or one of the caller's batch segments.  Call after vec_out is set.
+static bool bn_epilogue_ok(const Plan& p) {
+  const GemmArgs& g = p.g;
+  if (p.mode != MODE_CONV && p.mode != MODE_CONVT2) return false;
+  if (!p.fast || p.cfg != CFG_L || g.splits != 1 || !g.vec_out || p.tap_stage) return false;
+  if (g.out.fnc.d != (uint32_t)g.N || g.M % 64 != 0 || p.bn_segs < 1) return false;
+  if (p.bn_segs > 1 && (p.phases != 1 || g.M % p.bn_segs != 0 || (g.M / p.bn_segs) % 64 != 0)) return false;
+  return true;
+}
+
+static long long bn_epilogue_segments(const Plan& p) { return (long long)p.phases * (p.g.M / 64); }
+
 static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   if (ws_bytes < plan_ws_bytes(p)) return RGAN_EINVAL;
   if (p.mode == MODE_NARROW_T || p.mode == MODE_NARROW_IN || p.mode == MODE_DENSE1) {
@@ -2052,6 +2092,8 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     p.g.vec_out = p.mode != MODE_WGRAD && o.tc == 1 && o.fnc.d % 4 == 0 && p.g.N % 4 == 0 && al4(o.th) &&
                   al4(o.tw) && al4(o.sb) && al4(o.sh) && al4(o.sw) && aligned16(p.g.C);
   }
+  p.bn_fused = p.bn_part && bn_epilogue_ok(p);
+  p.g.bnp = p.bn_fused ? p.bn_part : nullptr;
   int bm, bn;
   tile_dims(p.cfg, bm, bn);
   const int tiles_m = ceil_div(p.g.M, bm);
@@ -2173,6 +2215,40 @@ extern "C" int rgan_conv_fwd(const RganConv* d, const float* x, const float* w, 
   if (!p.pack && !w) return RGAN_EINVAL;  // kernels that read the torch layout
   p.prepacked = wpacked;
   return run_plan(p, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" long long rgan_conv_bn_segments(const RganConv* d, int segs) {
+  Plan p;
+  alignas(16) static const float dummy[4] = {0, 0, 0, 0};
+  if (segs < 1 || plan_fwd(d, dummy, dummy, nullptr, nullptr, (float*)dummy, 0, 0.f, p)) return 0;
+  if (p.mode != MODE_CONV && p.mode != MODE_CONVT2) return 0;
+  const OutMap& o = p.g.out;
+  auto al4 = [](long long v) { return (v & 3) == 0; };
+  p.g.vec_out = o.tc == 1 && o.fnc.d % 4 == 0 && p.g.N % 4 == 0 && al4(o.th) && al4(o.tw) && al4(o.sb) &&
+                al4(o.sh) && al4(o.sw);
+  p.bn_segs = segs;
+  return bn_epilogue_ok(p) ? bn_epilogue_segments(p) : 0;
+}
+
+extern "C" int rgan_conv_fwd_bn(const RganConv* d, const float* x, const float* w, const float* wpacked,
+                                const float* wscale, const float* bias, float* y, void* ws, size_t ws_bytes,
+                                double* bn_part, long long part_segments, int segs, int* fused, void* stream) {
+  if (!x || (!w && !wpacked) || !y || !fused || segs < 1) return RGAN_EINVAL;
+  *fused = 0;
+  g_cur_flops = conv_flops(d);
+  Plan p;
+  int rc = plan_fwd(d, x, w, wscale, bias, y, 0, 0.f, p);
+  if (rc) return rc;
+  if (!p.pack && !w) return RGAN_EINVAL;
+  p.prepacked = wpacked;
+  const bool want = bn_part && p.mode != MODE_NARROW_T && p.mode != MODE_NARROW_IN && p.mode != MODE_DENSE1 &&
+                    bn_epilogue_segments(p) <= part_segments;
+  p.bn_part = want ? bn_part : nullptr;
+  p.bn_segs = segs;
+  rc = run_plan(p, ws, ws_bytes, (hipStream_t)stream);
+  if (rc) return rc;
+  *fused = p.bn_fused ? 1 : 0;
+  return 0;
 }
 
 extern "C" int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* w, const float* wpacked,

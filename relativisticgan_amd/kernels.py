@@ -6,6 +6,7 @@ allocator and launches on the current stream.  Internal activations are NHWC
 wherever the reference hands them over (images into D, out of G).
 """
 import ctypes
+import os
 import weakref
 from dataclasses import dataclass
 
@@ -246,6 +247,61 @@ def conv_fwd(x, w, geom, bias=None, act="none", alpha=0.0, wscale=None, out=None
                               L.ptr(out), L.ACT[act], float(alpha), L.ptr(ws), ws.numel(), L.stream()),
             "rgan_conv_fwd")
     return out
+
+
+# BatchNorm batch statistics from the conv GEMM's epilogue (rgan_conv_fwd_bn); "0" = always
+# the separate moments pass (A/B switch and parity cross-check).
+BN_EPILOGUE = os.environ.get("RGAN_BN_EPILOGUE", "1") != "0"
+
+
+def conv_fwd_bn(x, w, geom, bias=None, wscale=None, cache=False, segs=1):
+    """y = conv(x, w)*wscale + bias (NHWC) for a layer followed by train-mode BatchNorm.
+
+    Returns (y, part, S): when the GEMM's vector epilogue covered the layer, ``part`` is
+    its per-64-row segment sums (sum y, sum y^2) double[S][2][C] (merge with bn_segment_stats; batch
+    segment k = segments [k*S/segs, (k+1)*S/segs)); otherwise (y, None, 0)."""
+    if geom.upsample != 1 or not BN_EPILOGUE:
+        return conv_fwd(x, w, geom, bias=bias, wscale=wscale, cache=cache), None, 0
+    L.require_cuda(x, w, bias, wscale)
+    _f32(x, w, bias)
+    B, cin, H, W = x.shape
+    cout = w.shape[1] if geom.transposed else w.shape[0]
+    Ho, Wo = geom.out_hw(H, W)
+    out = empty_nhwc(B, cout, Ho, Wo, x.device)
+    d = _desc(x.shape, x.stride(), out.shape, out.stride(), geom)
+    lib = L.lib()
+    S = lib.rgan_conv_bn_segments(ctypes.byref(d), int(segs))
+    if S <= 0:
+        return conv_fwd(x, w, geom, bias=bias, wscale=wscale, out=out, cache=cache), None, 0
+    packed = PACKS.get(w, 0, geom, d) if cache else None
+    nbytes = lib.rgan_conv_workspace(ctypes.byref(d), 0, int(packed is not None))
+    if nbytes == 0:
+        raise L.RganError(f"unsupported conv {geom} for input {tuple(x.shape)}")
+    ws = L.workspace(nbytes, x.device)
+    part = torch.empty((S, 2, cout), dtype=torch.float64, device=x.device)
+    fused = L.c_int(0)
+    L.check(lib.rgan_conv_fwd_bn(ctypes.byref(d), L.ptr(x), L.ptr(w), L.ptr(packed), L.ptr(wscale), L.ptr(bias),
+                                 L.ptr(out), L.ptr(ws), ws.numel(), L.ptr(part), S, int(segs), ctypes.byref(fused),
+                                 L.stream()), "rgan_conv_fwd_bn")
+    return (out, part, S) if fused.value else (out, None, 0)
+
+
+def bn_segment_stats(part, s0, s1, C, eps, momentum, running_mean=None, running_var=None,
+                     num_batches_tracked=None):
+    """Segment moments [s0, s1) of conv_fwd_bn -> (mean, invstd) float[2C] + running stats."""
+    stats = torch.empty(2 * C, dtype=torch.float32, device=part.device)
+    L.check(L.lib().rgan_bn_segment_stats(L.ptr(part), int(s0), int(s1), C, 64, float(eps), float(momentum),
+                                          L.ptr(running_mean), L.ptr(running_var), L.ptr(num_batches_tracked),
+                                          L.ptr(stats), None, L.stream()), "rgan_bn_segment_stats")
+    return stats
+
+
+def bn_segment_moments(part, s0, s1, C):
+    """Segment moments [s0, s1) -> this rank's (count, mean, M2) double[3C] (SyncBN stage 1)."""
+    mom = torch.empty(3 * C, dtype=torch.float64, device=part.device)
+    L.check(L.lib().rgan_bn_segment_stats(L.ptr(part), int(s0), int(s1), C, 64, 0.0, 0.0, None, None, None, None,
+                                          L.ptr(mom), L.stream()), "rgan_bn_segment_stats")
+    return mom
 
 
 def conv_dgrad(dy, w, geom, x_shape, wscale=None, out=None, like=None, cache=False):

@@ -325,6 +325,55 @@ def test_batchnorm_train(K, shape, act):
     assert _rel(db, b64.grad) < 2e-5
 
 
+# conv feeding BatchNorm: (B, cin, cout, H, transposed, segs) -- FAST 128x128 layers whose
+# vector epilogue emits the BN segment moments (D conv, G k4s2 ConvT = 4 phases, batched
+# D halves), plus shapes that must fall back (split-K deep layer, ragged M, narrow N)
+BN_EPI = [
+    (16, 32, 128, 128, False, 1),    # >= 512 output tiles: no split-K
+    (32, 32, 128, 128, False, 2),
+    (16, 128, 128, 32, True, 1),
+    (4, 256, 128, 16, False, 1),     # M = 256 rows: split-K -> fallback
+    (3, 64, 128, 10, False, 1),      # M = 75: not a multiple of 64 -> fallback
+    (8, 64, 32, 32, False, 1),       # N = 32: narrow tile -> fallback
+]
+
+
+@pytest.mark.parametrize("case", BN_EPI)
+def test_conv_bn_epilogue_stats(K, case):
+    """rgan_conv_fwd_bn + rgan_bn_segment_stats == rgan_conv_fwd + rgan_bn_stats (fp64 torch)."""
+    from relativisticgan_amd.kernels import ConvGeom
+    B, cin, cout, H, tr, segs = case
+    torch.manual_seed(11)
+    g = ConvGeom(4, 2, 1, tr)
+    x = _nhwc(torch.randn(B, cin, H, H, device=DEV))
+    w = torch.randn((cin, cout, 4, 4) if tr else (cout, cin, 4, 4), device=DEV) * 0.05 + 0.01
+    y, part, S = K.conv_fwd_bn(x, w, g, segs=segs)
+    expect_fused = case[:4] not in {(4, 256, 128, 16), (3, 64, 128, 10), (8, 64, 32, 32)}
+    assert (part is not None) == expect_fused
+    y_ref = K.conv_fwd(x, w, g)
+    assert torch.equal(y, y_ref)  # the epilogue statistics do not touch the stored output
+    Bs = B // segs
+    for k in range(segs):
+        ys = y[k * Bs:(k + 1) * Bs]
+        rm, rv = torch.zeros(cout, device=DEV), torch.ones(cout, device=DEV)
+        nbt = torch.zeros((), dtype=torch.long, device=DEV)
+        if part is not None:
+            stats = K.bn_segment_stats(part, k * S // segs, (k + 1) * S // segs, cout, 1e-5, 0.1, rm, rv, nbt)
+            mom = K.bn_segment_moments(part, k * S // segs, (k + 1) * S // segs, cout).cpu()
+        else:
+            stats = K.bn_stats(ys, 1e-5, 0.1, rm, rv, nbt)
+            mom = K.bn_moments(ys).cpu()
+        y64 = ys.double().cpu()
+        mean, var = y64.mean((0, 2, 3)), y64.var((0, 2, 3), unbiased=False)
+        n = ys.shape[0] * ys.shape[2] * ys.shape[3]
+        assert _rel(stats[:cout], mean) < 1e-6
+        assert _rel(stats[cout:], 1 / torch.sqrt(var + 1e-5)) < 1e-6
+        assert _rel(rv, 0.9 + 0.1 * var * n / (n - 1)) < 1e-6
+        assert int(nbt.item()) == 1
+        assert mom[0].item() == n
+        assert _rel(mom[cout:2 * cout], mean) < 1e-6 and _rel(mom[2 * cout:], var * n) < 1e-6
+
+
 def _torch_head(kind, side, r, f):
     """The reference's expressions (GLI:592-709) in fp64 with torch autograd."""
     ones = torch.ones_like(r if r is not None else f)
