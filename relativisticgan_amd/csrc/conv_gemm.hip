@@ -1561,6 +1561,10 @@ static Img make_img(const float* p, int H, int W, int C, const long long* s /* b
   Img im;
   im.p = p; im.H = H; im.W = W; im.C = C;
   im.sb = s[0]; im.sc = s[1]; im.sh = s[2]; im.sw = s[3];
+  // size-1 spatial dims: only index 0 is ever read, so give them the dense NHWC stride (z as
+  // [B][C][1][1] -- G's first layer -- then qualifies for the vector/FAST loaders)
+  if (W == 1 && im.sc == 1) im.sw = C;
+  if (H == 1 && im.sc == 1) im.sh = (long long)W * im.sw;
   return im;
 }
 

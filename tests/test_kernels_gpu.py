@@ -46,6 +46,7 @@ SMALL = [
     (2, 16, 8, 8, 4, 2, 1, True),       # ConvT k4s2p1
     (2, 8, 3, 8, 4, 2, 1, True),        # last G layer, Cout=3
     (5, 16, 32, 1, 4, 1, 0, True),      # G start 1x1 -> 4x4
+    (4, 64, 32, 1, 4, 1, 0, True),      # G start, Cin % 32 == 0: FAST loaders on a 1x1 image
     (5, 32, 1, 4, 4, 1, 0, False),      # D end 4x4 -> 1x1
     (2, 12, 20, 8, 3, 1, 1, False),     # arch-1 3x3
     (2, 64, 128, 8, 4, 2, 1, False),
