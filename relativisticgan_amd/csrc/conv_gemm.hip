@@ -634,6 +634,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
         for (int t = 0; t < TM; ++t) a4[t] = *reinterpret_cast<const float4*>(Ar + 32 * t * KROW_LD + qo);
 #pragma unroll
         for (int t = 0; t < TN; ++t) b4[t] = *reinterpret_cast<const float4*>(Br + 32 * t * KROW_LD + qo);
+#if RGAN_EXP_SETPRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
@@ -641,6 +644,9 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
             for (int j = 0; j < TN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[i][s4], b4[j][s4], acc[i][j], 0, 0, 0);
+#if RGAN_EXP_SETPRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
       }
     } else {
 #if RGAN_GEMM_FRAGALL
