@@ -1,12 +1,15 @@
 #!/usr/bin/env python3
 """Throughput benchmark: D+G training iterations per second on synthetic images.
 
-Workload (BASELINE.json configs[1]): RaSGAN (--loss_D 6) DCGAN 128x128, h=128, batch 64
-per GPU, fp32 (weak scaling: global batch = 64 * n_gpus).  One "step" = one reference
-iteration (GLI:560-714): D step (D(real), G(z) no-grad, D(fake), head, backward, Adam)
-+ G step (G(z), D(fake), fresh real batch D(x), head, backward, Adam).  Inputs are
-resident in HBM (a 1024-image synthetic set; batches gathered on the device, z drawn
-on the device).
+Workload (BASELINE.json metric "RaLSGAN DCGAN 64^2/256^2", configs[2]'s per-GPU shard):
+RaLSGAN (--loss_D 7) DCGAN 256x256, h=128 (the reference default, GLI:24-25), batch 32
+per GPU, fp32 (weak scaling: global batch = 32 * n_gpus; 8 GPUs = configs[2]'s global
+batch 256).  One "step" = one reference iteration (GLI:560-714): D step (D(real), G(z)
+no-grad, D(fake), head, backward, Adam) + G step (G(z), D(fake), fresh real batch D(x),
+head, backward, Adam).  Inputs are resident in HBM (a 1024-image synthetic set; batches
+gathered on the device, z drawn on the device).  On one GPU the line also carries the
+64^2 half of the metric (C1: RaLSGAN 64^2, B=32, h=128 = configs[0]'s shape) and
+configs[1] (C2: RaSGAN 128^2, B=64) under ``extra_workloads``.
 
 Prints ONE JSON line (rank 0).  Extra fields:
   roofline     -- the dominant kernel (the fp32-MFMA implicit-GEMM conv): algorithmic
@@ -37,11 +40,23 @@ WORKLOADS = {
     "C3": (7, 256, 32, 128),   # configs[2] per-GPU shard: RaLSGAN 256x256, 32 per GPU
     "C3h32": (7, 256, 32, 32),
     "C5": (8, 128, 32, 128),   # spectral RaHinge 128x128 (spectral flag set below)
+    "C4": (3, 32, 32, 128),    # configs[3]: WGAN-GP standard CNN (arch 1, 32x32 only: GLI:246,313)
+    "C4p": (3, 64, 32, 128),   # configs[3] at 64x64 on DCGAN arch 0 (SURVEY C4')
 }
+ARCH = {"C4": 1}
+DEFAULT_WORKLOAD = "C3"
+EXTRA_WORKLOADS = ("C1", "C2")
 
 
 def conv_flops_per_iteration(t):
-    """9 F_D + 4 F_G - 2 d0 - g0; F = forward conv FLOPs (2*MACs)."""
+    """Algorithmic conv FLOPs of one reference iteration, F = forward conv
+    FLOPs (2*MACs) per net, d0/g0 = the image-side first layers (no data gradient needed):
+      relativistic heads 5-8: 9 F_D + 4 F_G - 2 d0 - g0  (D step: D(x), D(fake) fwd+wgrad+
+        dgrad, G fwd; G step: G fwd, D(fake) fwd + dgrad, G wgrad + dgrad, D(x) fwd);
+      heads 1-4: the G step has no D(x): 8 F_D + 4 F_G - 2 d0 - g0;
+      gradient penalty (GLI:646-658): + D(x_hat) fwd, its create-graph dgrad chain, and the
+        double backward (adjoint conv fwd + wgrad per dgrad, then wgrad + dgrad back through
+        the forward): 6 F_D - d0 - 3 F_end."""
     def layer_flops(net, x_shape):
         out, h = [], torch.zeros(x_shape, device="meta")
         for layer in net._plan:
@@ -63,33 +78,73 @@ def conv_flops_per_iteration(t):
         return out
     p = t.p
     fg = layer_flops(t.G, (t.B, p.z_size, 1, 1))
-    fd = layer_flops(t.D, (t.B, p.n_colors, p.image_size, p.image_size))
-    return 9 * sum(fd) + 4 * sum(fg) - 2 * fd[0] - fg[0]
-
-
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "round1_c2_pmc_traffic.json")
+    fd = layer_flops(t.D, (t.B, p.n_colors * getattr(p, "pac", 1), p.image_size, p.image_size))
+    total = 9 * sum(fd) + 4 * sum(fg) - 2 * fd[0] - fg[0]
+    if p.loss_D <= 4:
+        total -= sum(fd)
+    if p.loss_D == 3 or p.grad_penalty:
+        total += 6 * sum(fd) - fd[0] - 3 * fd[-1]
+    return total
 
 
 def pmc_traffic(workload, symbol):
     """HBM-side bytes per launch of `symbol` from the committed rocprofv3 PMC passes
-    (tools/pmc_traffic.sh on this bench command: FETCH_SIZE x2 + WRITE_SIZE), or None."""
-    if workload != "C2" or not os.path.exists(PMC_TRAFFIC):
+    (tools/pmc_traffic.sh on this bench command: FETCH_SIZE x2 + WRITE_SIZE), or None.
+    The newest round's file for the workload wins."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"round*_{workload.lower()}_pmc_traffic.json")),
+                   key=lambda f: int(os.path.basename(f).split("_")[0][5:]))
+    if not files:
         return None, None
-    with open(PMC_TRAFFIC) as f:
+    with open(files[-1]) as f:
         d = json.load(f)
     ent = d.get(symbol)
     if ent is None:
         return None, None
-    return ent["bytes_per_launch"], os.path.relpath(PMC_TRAFFIC, ROOT)
+    return ent["bytes_per_launch"], os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(loss_D, size, batch, h, spectral, seconds_hint):
-    """Oracle (CPU restatement, pinned to the reference) on this host: bounded sample."""
+def host_cpus():
+    """The CPUs this process may use: affinity mask, cgroup CPU quota (the lease's share
+    on the GPU box), and the machine's model / physical cores (lscpu's fields from
+    /proc/cpuinfo)."""
+    aff = sorted(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    model, cores = None, set()
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo").read().splitlines() + [""]:
+            if not line.strip():
+                if cur.get("processor") is not None and int(cur["processor"]) in aff:
+                    cores.add((cur.get("physical id", "0"), cur.get("core id", cur["processor"])))
+                    model = model or cur.get("model name")
+                cur = {}
+                continue
+            k, _, v = line.partition(":")
+            cur[k.strip()] = v.strip()
+    except OSError:
+        pass
+    usable = len(aff) if quota is None else max(1, min(len(aff), int(quota)))
+    return {"threads": usable, "affinity_cpus": len(aff), "cgroup_cpu_quota": quota,
+            "physical_cores_in_affinity": len(cores) or None, "model": model}
+
+
+def cpu_baseline(loss_D, size, batch, h, spectral, seconds_hint, arch=0):
+    """Oracle (CPU restatement, pinned bitwise to the reference) on this host's CPUs:
+    every CPU the process is allowed (affinity, capped by the cgroup quota), 1 warm-up
+    iteration, then timed iterations until ~seconds_hint of CPU work or 5 iterations."""
     from oracle.reference_cpu import Trainer as OracleTrainer, make_param, synthetic_images
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    cpus = host_cpus()
+    threads = cpus["threads"]
     torch.set_num_threads(threads)
     p = make_param(loss_D=loss_D, image_size=size, batch_size=batch, G_h_size=h, D_h_size=h, seed=1, cuda=False,
-                   print_every=10 ** 9, spectral=spectral)
+                   print_every=10 ** 9, spectral=spectral, arch=arch)
     t = OracleTrainer(p, synthetic_images(256, size))
     t.iteration(1)  # warm-up (i=1: skips the i=0 sample-image forward)
     n, t0 = 0, time.perf_counter()
@@ -100,8 +155,81 @@ def cpu_baseline(loss_D, size, batch, h, spectral, seconds_hint):
         if el > seconds_hint or n >= 5:
             break
     return {"value": batch * n / el, "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu": cpus, "s_per_iter": el / n,
             "sample": f"{n} timed + 1 warm-up oracle iterations of the same workload (B={batch}, {size}^2, h={h}), "
-                      f"torch {torch.__version__} CPU fp32, {threads} threads"}
+                      f"torch {torch.__version__} CPU fp32, {threads} threads on {cpus['model']}"}
+
+
+def run_workload(name, steps, warmup, world, args, K):
+    """Train `steps` timed iterations of workload `name` (after `warmup`); returns the
+    measurement (max over ranks)."""
+    from relativisticgan_amd.config import make_param
+    from relativisticgan_amd.train import Trainer, synthetic_images
+    loss_D, size, bpg, h = WORKLOADS[name]
+    spectral = name == "C5"
+    bd = {"auto": None, "on": True, "off": False}[args.batch_d]
+    p = make_param(loss_D=loss_D, image_size=size, batch_size=bpg * world, G_h_size=h, D_h_size=h, seed=1,
+                   print_every=10 ** 9, spectral=spectral, rgan_rng="device", arch=ARCH.get(name, 0),
+                   rgan_batch_D=bd)
+    images = synthetic_images(1024, size, device="cuda")
+    t = Trainer(p, images)
+    flops_iter = conv_flops_per_iteration(t)
+
+    for i in range(warmup):
+        t.iteration(i + 1)
+    t.flush()
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    K.profile_begin(capacity=400 * steps + 64)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        t.iteration(warmup + 1 + i)
+    t.flush()  # the last G step (deferred under DP) is inside the timed region
+    barrier()
+    elapsed = time.perf_counter() - t0
+    prof = K.profile_end()
+    if world > 1:
+        e = torch.tensor([elapsed], device="cuda")
+        torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(e.item())
+    res = {"name": name, "loss_D": loss_D, "size": size, "bpg": bpg, "h": h, "spectral": spectral,
+           "arch": ARCH.get(name, 0), "batch_D": t.batch_D, "elapsed": elapsed, "steps": steps,
+           "value": bpg * world * steps / elapsed, "ms_per_step": 1000.0 * elapsed / steps,
+           "flops_iter": flops_iter, "prof": prof}
+    del t, images
+    torch.cuda.empty_cache()
+    return res
+
+
+def roofline_of(res, workload):
+    """Dominant kernel = the conv kernel symbol with the most time (HIP events around each
+    launch on its stream); the whole conv family is reported beside it."""
+    prof, steps = res["prof"], res["steps"]
+    gemm_ms, gemm_flops = prof["ms"], prof["flops"]
+    top = max(prof["kernels"], key=lambda k: k["ms"])
+    achieved = top["flops"] / (top["ms"] / 1000.0)
+    traffic, traffic_src = pmc_traffic(workload, top["name"])
+    return {"bound": "mfma", "achieved": achieved / 1e12, "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
+            "frac": achieved / FP32_MFMA_PEAK, "traffic": traffic, "traffic_unit": "bytes/launch",
+            "traffic_source": traffic_src, "kernel": top["name"], "launches": top["launches"],
+            "avg_launch_us": 1000.0 * top["ms"] / top["launches"],
+            "flops_per_launch": top["flops"] / top["launches"],
+            "conv_family": {"achieved": gemm_flops / (gemm_ms / 1000.0) / 1e12, "launches": prof["launches"],
+                            "ms_per_step": gemm_ms / steps,
+                            "frac": gemm_flops / (gemm_ms / 1000.0) / FP32_MFMA_PEAK,
+                            "kernels": prof["kernels"]}}
+
+
+def describe(res):
+    arch = "arch1 (standard CNN)" if res["arch"] == 1 else "arch0"
+    return (f"{res['name']}: loss_D {res['loss_D']} DCGAN {arch} {res['size']}x{res['size']}, h={res['h']}, "
+            f"batch {res['bpg']}/GPU{', spectral D' if res['spectral'] else ''}"
+            f"{', gradient penalty' if res['loss_D'] == 3 else ''}")
 
 
 def main():
@@ -109,7 +237,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default=DEFAULT_WORKLOAD, choices=sorted(WORKLOADS))
+    ap.add_argument("--extra", default=",".join(EXTRA_WORKLOADS),
+                    help="comma-separated workloads also measured on one GPU (extra_workloads); '' = none")
+    ap.add_argument("--batch-d", default="auto", choices=("auto", "on", "off"),
+                    help="D(x), D(x_fake) as one batched pass (auto: on for 1 process, off under DP -- "
+                         "'off' at N=1 is the like-for-like baseline of the N>1 runs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--sync-bn", action="store_true",
@@ -125,8 +258,6 @@ def main():
         local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     from relativisticgan_amd import dp, kernels as K
-    from relativisticgan_amd.config import make_param
-    from relativisticgan_amd.train import Trainer, synthetic_images
     if world > 1:
         import torch.distributed as dist
         if backend == "nccl":
@@ -134,72 +265,36 @@ def main():
         else:
             dist.init_process_group(backend)
         dp.setup(sync_bn=args.sync_bn)
-    loss_D, size, bpg, h = WORKLOADS[args.workload]
-    spectral = args.workload == "C5"
-    p = make_param(loss_D=loss_D, image_size=size, batch_size=bpg * world, G_h_size=h, D_h_size=h, seed=1,
-                   print_every=10 ** 9, spectral=spectral, rgan_rng="device")
-    images = synthetic_images(1024, size, device="cuda")
-    t = Trainer(p, images)
-    flops_iter = conv_flops_per_iteration(t)
-
-    for i in range(args.warmup):
-        t.iteration(i + 1)
-    t.flush()
-
-    def barrier():
-        if world > 1:
-            torch.distributed.barrier()
-        torch.cuda.synchronize()
-
-    barrier()
-    K.profile_begin(capacity=200 * args.steps + 64)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        t.iteration(args.warmup + 1 + i)
-    t.flush()  # the last G step (deferred under DP) is inside the timed region
-    barrier()
-    elapsed = time.perf_counter() - t0
-    prof = K.profile_end()
-    if world > 1:
-        e = torch.tensor([elapsed], device="cuda")
-        torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
-        elapsed = float(e.item())
+    res = run_workload(args.workload, args.steps, args.warmup, world, args, K)
+    extras = {}
+    if world == 1:
+        for name in [w for w in args.extra.split(",") if w and w != args.workload]:
+            r = run_workload(name, args.steps, min(args.warmup, 5), world, args, K)
+            extras[name] = {"workload": describe(r), "value": r["value"], "unit": "images/s",
+                            "ms_per_step": r["ms_per_step"], "steps": r["steps"],
+                            "step_mfma_util": r["flops_iter"] / (r["ms_per_step"] / 1000.0) / FP32_MFMA_PEAK,
+                            "roofline": {k: v for k, v in roofline_of(r, name).items() if k != "conv_family"}}
     if rank != 0:
         torch.distributed.destroy_process_group()
         return
-    imgs = bpg * world * args.steps
-    value = imgs / elapsed
-    ms_step = 1000.0 * elapsed / args.steps
-    # dominant kernel = the conv kernel symbol with the most time (HIP events around each
-    # launch on its stream); the whole conv family is reported beside it
-    gemm_ms, gemm_flops = prof["ms"], prof["flops"]
-    top = max(prof["kernels"], key=lambda k: k["ms"])
-    achieved = top["flops"] / (top["ms"] / 1000.0)
-    traffic, traffic_src = pmc_traffic(args.workload, top["name"])
-    roofline = {"bound": "mfma", "achieved": achieved / 1e12, "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
-                "frac": achieved / FP32_MFMA_PEAK, "traffic": traffic, "traffic_unit": "bytes/launch",
-                "traffic_source": traffic_src, "kernel": top["name"], "launches": top["launches"],
-                "avg_launch_us": 1000.0 * top["ms"] / top["launches"],
-                "flops_per_launch": top["flops"] / top["launches"],
-                "conv_family": {"achieved": gemm_flops / (gemm_ms / 1000.0) / 1e12, "launches": prof["launches"],
-                                "ms_per_step": gemm_ms / args.steps,
-                                "frac": gemm_flops / (gemm_ms / 1000.0) / FP32_MFMA_PEAK,
-                                "kernels": prof["kernels"]}}
     out = {
-        "metric": METRIC, "value": value, "unit": "images/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
+        "metric": METRIC, "value": res["value"], "unit": "images/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": res["ms_per_step"], "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
-        "config": {"workload": f"{args.workload}: loss_D {loss_D} DCGAN arch0 {size}x{size}, h={h}, "
-                               f"batch {bpg}/GPU{', spectral D' if spectral else ''}",
-                   "loss_D": loss_D, "image_size": size, "batch_per_gpu": bpg, "global_batch": bpg * world,
-                   "G_h_size": h, "D_h_size": h, "parallelism": f"dp{world}",
+        "config": {"workload": describe(res), "loss_D": res["loss_D"], "image_size": res["size"],
+                   "batch_per_gpu": res["bpg"], "global_batch": res["bpg"] * world, "G_h_size": res["h"],
+                   "D_h_size": res["h"], "arch": res["arch"], "parallelism": f"dp{world}",
+                   "batched_D_step": res["batch_D"],
                    "batchnorm": "SyncBN" if args.sync_bn else "per-shard (reference DataParallel)"},
-        "step_mfma_util": flops_iter * args.steps / elapsed / (world * FP32_MFMA_PEAK),
-        "conv_tflop_per_step": flops_iter / 1e12,
-        "roofline": roofline,
+        "step_mfma_util": res["flops_iter"] * args.steps / res["elapsed"] / (world * FP32_MFMA_PEAK),
+        "conv_tflop_per_step": res["flops_iter"] / 1e12,
+        "roofline": roofline_of(res, args.workload),
     }
+    if extras:
+        out["extra_workloads"] = extras
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(loss_D, size, bpg, h, spectral, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(res["loss_D"], res["size"], res["bpg"], res["h"], res["spectral"],
+                                           args.cpu_seconds, arch=res["arch"])
     print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

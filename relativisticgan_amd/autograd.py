@@ -34,7 +34,9 @@ PATCH_IMAGE_LAYERS = os.environ.get("RGAN_PATCH_IMAGE", "1") != "0"
 
 ACT_TRACE = None
 ACT_TAGS = []      # per ACT_TRACE entry: the net that produced it ("G" / "D", set by nets._Net)
+ACT_LAYERS = []    # per ACT_TRACE entry: the layer's index in the net's plan
 TRACE_NET = None
+TRACE_LAYER = -1
 _KINKED = ("relu", "lrelu", "selu")
 
 
@@ -219,6 +221,7 @@ class ConvLayerFn(torch.autograd.Function):
         if ACT_TRACE is not None and spec.act in _KINKED:
             ACT_TRACE.append((a.detach() > 0).cpu())
             ACT_TAGS.append(TRACE_NET)
+            ACT_LAYERS.append(TRACE_LAYER)
         ctx.spec = spec
         ctx.stats_eval = stats_eval
         ctx.training = bufs[3] if bufs is not None else True
@@ -242,8 +245,7 @@ class ConvLayerFn(torch.autograd.Function):
             y = t5
             P = y.shape[0] * y.shape[2] * y.shape[3]
             if ctx.stats_eval is not None:
-                # eval-mode BN is a per-channel affine map: dy = da * act' * gamma * invstd
-                dy, _, _ = K.bn_backward(da, y, stats, gamma, beta, spec.act, spec.alpha, need_affine=False)
+                # the reference never calls .eval() (GLI:560-714): no training path reaches this
                 raise NotImplementedError("backward through eval-mode BatchNorm is not on the training path")
             if stats.dim() == 2:  # segmented call: BN backward per segment, one dy
                 dy, dgamma, dbeta = ConvLayerFn._seg_bn_backward(ctx, da, y, stats, gamma, beta, ng, nbeta)

@@ -7,10 +7,11 @@ persistent replica and processes ``B_global / world`` samples; the exchanges are
 (SURVEY §8(e)):
 
   * loss heads: the batch sums the relativistic means need (2 floats fwd, 4 bwd);
-  * BatchNorm (SyncBN, default on): per-layer moments [3C] all-gathered and merged in
-    rank order in the forward, [2C] sums all-reduced in the backward, so the math equals
-    the global-batch single-process result (the reference's DP did NOT sync BN:
-    ``sync_bn=False`` reproduces that per-shard behaviour);
+  * BatchNorm: by default (``sync_bn=False``, the reference's DataParallel semantics)
+    every rank normalises its own shard -- no exchange; with ``sync_bn=True`` (SyncBN,
+    ``--rgan_sync_bn True``) per-layer moments [3C] are all-gathered and merged in rank
+    order in the forward and [2C] sums all-reduced in the backward, so the math equals
+    the global-batch single-process result;
   * gradients: one bucketed all-reduce (SUM: the losses already divide by the global
     batch) before each optimizer step.
 Spectral-norm u/v and Adam are replicated and stay identical on every rank.
@@ -28,13 +29,13 @@ class _State:
     grad_group = None  # second communicator for the bucketed gradient all-reduce
     world = 1
     rank = 0
-    sync_bn = True
+    sync_bn = False
 
 
 _S = _State()
 
 
-def setup(group=None, sync_bn=True):
+def setup(group=None, sync_bn=False):
     """Activate data-parallel mode for the current process (after init_process_group)."""
     if not dist.is_available() or not dist.is_initialized():
         _S.group, _S.grad_group, _S.world, _S.rank = None, None, 1, 0
@@ -51,7 +52,7 @@ def setup(group=None, sync_bn=True):
 
 
 def reset():
-    _S.group, _S.grad_group, _S.world, _S.rank, _S.sync_bn = None, None, 1, 0, True
+    _S.group, _S.grad_group, _S.world, _S.rank, _S.sync_bn = None, None, 1, 0, False
 
 
 def world():
@@ -64,6 +65,10 @@ def rank():
 
 def active():
     return _S.world > 1
+
+
+def group():
+    return _S.group
 
 
 def sync_bn():

@@ -198,7 +198,8 @@ class _Net(nn.Module):
     def _run(self, x):
         AG.TRACE_NET = self._tag
         h = x
-        for layer in self._plan:
+        for li, layer in enumerate(self._plan):
+            AG.TRACE_LAYER = li
             h = layer.run(h, self.training)
         return h
 
@@ -221,15 +222,19 @@ class _Net(nn.Module):
         trace0 = len(AG.ACT_TRACE) if AG.ACT_TRACE is not None else 0
         AG.TRACE_NET = self._tag
         h = torch.cat(xs)
-        for layer in self._plan:
+        for li, layer in enumerate(self._plan):
+            AG.TRACE_LAYER = li
             h = layer.run(h, self.training, n)
         if AG.ACT_TRACE is not None:  # activation masks in the separate calls' order
             masks = AG.ACT_TRACE[trace0:]
+            layers = AG.ACT_LAYERS[trace0:]
             del AG.ACT_TRACE[trace0:]
             del AG.ACT_TAGS[trace0:]
+            del AG.ACT_LAYERS[trace0:]
             for s_ in range(n):
                 AG.ACT_TRACE.extend(m[s_ * B:(s_ + 1) * B] for m in masks)
                 AG.ACT_TAGS.extend(self._tag for _ in masks)
+                AG.ACT_LAYERS.extend(layers)
         return list(h.split(B))
 
 

@@ -62,9 +62,13 @@ class Adam(torch.optim.Optimizer):
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 if first is None:
                     first = st
+                for k in ("exp_avg", "exp_avg_sq"):
+                    if st[k].stride() != p.stride():  # e.g. state loaded from a checkpoint
+                        st[k] = torch.empty_like(p).copy_(st[k])
                 g = p.grad
                 if g.stride() != p.stride():
-                    g = g.contiguous(memory_format=torch.preserve_format)
+                    # the kernel walks p, g, m, v with one flat index: g must share p's layout
+                    g = g.contiguous() if p.is_contiguous() else torch.empty_like(p).copy_(g)
                 ps.append(p)
                 gs.append(g)
                 ms.append(st["exp_avg"])
@@ -72,6 +76,12 @@ class Adam(torch.optim.Optimizer):
             if not ps:
                 continue
             hyper, _, step = self._group_dev(gi, group, ps[0].device, first)
+            # one device step counter per group: every stepped parameter must agree with it
+            # (torch keeps one per parameter; a parameter that skipped steps would diverge)
+            steps = {float(self.state[p]["step"]) for p in ps}
+            if len(steps) != 1:
+                raise RuntimeError(f"Adam: parameters of group {gi} are at different steps {sorted(steps)}; "
+                                   "the fused kernel keeps one step count per group")
             K.adam(ps, gs, ms, vs, hyper, step)
             for p in ps:
                 self.state[p]["step"] += 1  # host mirror of state['step'] (torch Adam's state_dict layout)

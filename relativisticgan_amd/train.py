@@ -38,9 +38,25 @@ class Trainer:
     def __init__(self, param, images, device="cuda", seed_all=True):
         p = self.p = param
         self.device = torch.device(device)
+        world = dp.world()
+        n_gpu = getattr(p, "n_gpu", 1) or 1
+        if n_gpu > 1 and n_gpu != world:
+            # GLI:393-394,455-456: --n_gpu N runs torch's data_parallel over N GPUs inside
+            # forward (per-shard BatchNorm).  Here every GPU is its own process: a single
+            # process would silently train with whole-batch BN statistics instead.
+            raise ValueError(f"--n_gpu {n_gpu} with {world} process(es): launch one process per GPU "
+                             f"(torchrun --nproc-per-node {n_gpu}); each rank then normalises its own shard "
+                             "like the reference's data_parallel")
         if seed_all:
             if p.seed is None:
                 p.seed = random.randint(1, 10000)
+            if world > 1:
+                # every replica must start from the same weights / z_test / batch draws:
+                # rank 0's (possibly random) seed is everyone's
+                import torch.distributed as dist
+                box = [p.seed]
+                dist.broadcast_object_list(box, src=0, group=dp.group())
+                p.seed = box[0]
             random.seed(p.seed)
             numpy.random.seed(p.seed)
             torch.manual_seed(p.seed)

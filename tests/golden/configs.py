@@ -51,6 +51,13 @@ CONFIGS = {
     "sgan_pac2_gp": dict(_cfg(loss_D=1, grad_penalty="True"), pac=2, golden=False),
     "rahinge_pac2_arch1": {"args": {"image_size": 32, "batch_size": 8, "z_size": 16, "loss_D": 8, "arch": 1,
                                     "n_iter": 2}, "seed": 1, "n_images": 64, "pac": 2, "golden": False},
+    # the north-star target at FULL size: RaLSGAN DCGAN 64x64, batch 32, h = z = 128 (the
+    # reference defaults, GLI:20-25) = BASELINE configs[0]; 2 iterations
+    "ralsgan_c1": {"args": {"image_size": 64, "batch_size": 32, "z_size": 128, "G_h_size": 128,
+                            "D_h_size": 128, "loss_D": 7, "n_iter": 2}, "seed": 1, "n_images": 64},
+    # WGAN-GP at 64x64 on the DCGAN nets (SURVEY C4'; GLI:646-658), reduced width
+    "wgangp64": {"args": {"image_size": 64, "batch_size": 16, "z_size": 32, "G_h_size": 16, "D_h_size": 16,
+                          "loss_D": 3, "n_iter": 3}, "seed": 1, "n_images": 64},
     "wgangp_arch1": {"args": {"image_size": 32, "batch_size": 8, "z_size": 16, "loss_D": 3,
                               "arch": 1, "n_iter": 2}, "seed": 1, "n_images": 64},
     "rahinge_arch1": {"args": {"image_size": 32, "batch_size": 8, "z_size": 16, "loss_D": 8,

@@ -202,3 +202,67 @@ def test_overlapped_grad_reducer_gloo_world2():
         pr.join(120)
     res = [q.get() for _ in range(world)]
     assert all(msg == "ok" for _, msg in res), res
+
+
+def _seed_worker(rank, world, port, q):
+    try:
+        dp = _init(rank, world, port)
+        from relativisticgan_amd.config import make_param
+        from relativisticgan_amd.train import Trainer, synthetic_images
+        # no --seed: each rank would draw its own random seed; rank 0's must win
+        import random
+        random.seed(1000 + rank)
+        p = make_param(loss_D=7, image_size=32, batch_size=8, z_size=16, G_h_size=8, D_h_size=8, seed=None)
+        t = Trainer(p, synthetic_images(16, 32, device="cpu"), device="cpu")
+        seeds = [None] * world
+        dist.all_gather_object(seeds, p.seed)
+        assert len(set(seeds)) == 1, seeds
+        flat = torch.cat([v.reshape(-1).float() for v in list(t.G.state_dict().values()) +
+                          list(t.D.state_dict().values())])
+        z = t.z_test.reshape(-1)
+        all_flat = [torch.empty_like(flat) for _ in range(world)]
+        dist.all_gather(all_flat, flat)
+        assert all(torch.equal(all_flat[0], f) for f in all_flat), "replicas start from different weights"
+        all_z = [torch.empty_like(z) for _ in range(world)]
+        dist.all_gather(all_z, z.contiguous())
+        assert not torch.equal(all_z[0], all_z[1]), "z_test shards must differ (one global draw, sliced)"
+        # --n_gpu must match the process count (GLI:393-394 data_parallel is per-process here)
+        try:
+            Trainer(make_param(loss_D=7, image_size=32, batch_size=8, z_size=16, G_h_size=8, D_h_size=8, seed=1,
+                               n_gpu=4), synthetic_images(16, 32, device="cpu"), device="cpu")
+            raise AssertionError("--n_gpu 4 with 2 processes was accepted")
+        except ValueError:
+            pass
+        q.put((rank, "ok"))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_dp_unseeded_replicas_agree_gloo_world2():
+    """Without --seed every rank draws random.randint; the Trainer broadcasts rank 0's
+    seed so the replicas start from identical weights."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seed_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(180)
+    res = [q.get() for _ in range(world)]
+    assert all(msg == "ok" for _, msg in res), res
+
+
+def test_n_gpu_without_processes_fails_loudly():
+    """A single process with --n_gpu 2 would silently use whole-batch BN (GLI:455-456 runs
+    data_parallel with per-shard BN): the build refuses instead."""
+    from relativisticgan_amd.config import make_param
+    from relativisticgan_amd.train import Trainer, synthetic_images
+    p = make_param(loss_D=7, image_size=32, batch_size=8, z_size=16, G_h_size=8, D_h_size=8, seed=1, n_gpu=2)
+    with pytest.raises(ValueError, match="n_gpu"):
+        Trainer(p, synthetic_images(16, 32, device="cpu"), device="cpu")

@@ -284,6 +284,47 @@ def test_conv_full_size(K, case):
     assert _rel(K.conv_wgrad(x, dyk, g, w.shape)[0], wr.grad) < 2e-5
 
 
+# the per-GPU layer shapes of BASELINE configs[2] (RaLSGAN 256^2, h=128, 32 images per GPU;
+# SURVEY Appendix A "C3 per GPU"): the deepest D conv (2048 -> 4096 @ 8 -> 4, fwd K = 32768,
+# wgrad N = 32768), G's deepest ConvT (4096 -> 2048 @ 4 -> 8), the M = 524,288-pixel image
+# layers (D 3 -> 128 @ 256 -> 128, G 128 -> 3 @ 128 -> 256), a mid layer, and both ends
+C3_SHAPES = [
+    (32, 2048, 4096, 8, 4, 2, 1, False),
+    (32, 4096, 2048, 4, 4, 2, 1, True),
+    (32, 3, 128, 256, 4, 2, 1, False),
+    (32, 128, 3, 128, 4, 2, 1, True),
+    (32, 256, 512, 64, 4, 2, 1, False),
+    (32, 128, 4096, 1, 4, 1, 0, True),
+    (32, 4096, 1, 4, 4, 1, 0, False),
+]
+
+
+@pytest.mark.parametrize("case", C3_SHAPES)
+def test_conv_c3_full_size(K, case):
+    """fwd / dgrad / wgrad at the 256^2 shard's full layer shapes vs torch fp64 on the
+    device (ATen's GEMM convolution in double, MIOpen off): rel L2 <= 1e-5 (fp32 MFMA
+    accumulation over K <= 32768 terms; observed ~1e-6)."""
+    B, cin, cout, H, k, s, p, tr = case
+    g = K.ConvGeom(k, s, p, tr)
+    torch.manual_seed(3)
+    x = torch.randn(B, cin, H, H, device=DEV)
+    if cin != 3:
+        x = _nhwc(x)
+    w = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k), device=DEV) * 0.02
+    xr = x.detach().double().contiguous().requires_grad_(True)
+    wr = w.detach().double().requires_grad_(True)
+    with torch.backends.cudnn.flags(enabled=False):
+        ref = (F.conv_transpose2d if tr else F.conv2d)(xr, wr, stride=s, padding=p)
+        dy = torch.randn(ref.shape, device=DEV)
+        ref.backward(dy.double())
+    y = K.conv_fwd(x, w, g)
+    assert _rel(y, ref.detach()) < 1e-5
+    del ref, y
+    dyk = dy if cout == 3 else _nhwc(dy)
+    assert _rel(K.conv_dgrad(dyk, w, g, x.shape, like=x), xr.grad) < 1e-5
+    assert _rel(K.conv_wgrad(x, dyk, g, w.shape)[0], wr.grad) < 1e-5
+
+
 def _bn_ref(y, gamma, beta, eps=1e-5):
     y64 = y.double().cpu()
     mean = y64.mean((0, 2, 3))
@@ -292,7 +333,8 @@ def _bn_ref(y, gamma, beta, eps=1e-5):
     return xh * gamma.double().cpu()[None, :, None, None] + beta.double().cpu()[None, :, None, None], mean, var
 
 
-@pytest.mark.parametrize("shape", [(4, 8, 5, 5), (64, 256, 32, 32), (2, 2048, 4, 4), (3, 3, 1, 1)])
+@pytest.mark.parametrize("shape", [(4, 8, 5, 5), (64, 256, 32, 32), (2, 2048, 4, 4), (3, 3, 1, 1),
+                                   (32, 4096, 4, 4), (32, 256, 64, 64)])   # the last two: C3 D layers
 @pytest.mark.parametrize("act", ["relu", "lrelu", "none", "tanh"])
 def test_batchnorm_train(K, shape, act):
     torch.manual_seed(2)
