@@ -88,9 +88,12 @@ int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* w, const fl
                     const float* wscale, float* dx, void* ws, size_t ws_bytes, void* stream);
 
 /* dw = d conv / d w applied to dy (aten convolution_backward, grad_weight), written
- * in torch weight layout; dbias (nullable) = per-output-channel sum of dy. */
+ * in torch weight layout; dbias (nullable) = per-output-channel sum of dy.
+ * accumulate != 0: dw += ..., dbias += ... (autograd's gradient accumulation into an
+ * existing .grad, GLI:605/624/658's repeated backward calls, done in the GEMM's epilogue
+ * instead of a separate add pass). */
 int rgan_conv_wgrad(const RganConv* d, const float* x, const float* dy, float* dw, float* dbias,
-                    void* ws, size_t ws_bytes, void* stream);
+                    int accumulate, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- --NN_conv blocks: Upsample(scale_factor=2, nearest) + Conv2d(k3, s1, p1) ----
  * (GLI:351-356 middle, GLI:377-382 end).  conv3x3(up2(x), W) equals a k4 s2 p1
@@ -115,7 +118,7 @@ int rgan_patches_k4s2(const float* img, int batch, int channels, int height, int
 int rgan_patch_weight(const float* w, int rows, int channels, long long row_stride, long long channel_stride,
                       float* w1, void* stream);
 int rgan_unpatch_grad(const float* g1, int rows, int channels, long long row_stride, long long col_stride,
-                      float* dw, void* stream);
+                      float* dw, int accumulate, void* stream);
 
 /* ---- image export (GLI:563-565 sample grid, GLI:759-768 extra FID images) ----
  * torchvision.utils.save_image's float -> uint8 step on the device: t = x*scale + shift;
@@ -183,13 +186,57 @@ int rgan_bn_backward_apply(const float* da, long long dsp, long long dsc, const 
                            const double* sums, long long P_global, float* dy, long long ysp,
                            long long ysc, float* dgamma, float* dbeta, void* stream);
 
+/* rgan_bn_backward_apply plus: add (nullable, y's strides) is added to dy, and
+ * accumulate_affine != 0 adds dgamma/dbeta into the given buffers (the batched D
+ * step's two BN calls, the WGAN-GP double backward's second-order terms). */
+int rgan_bn_backward_apply_ex(const float* da, long long dsp, long long dsc, const float* y,
+                              long long P, int C, long long sp, long long sc, const float* stats,
+                              const float* gamma, const float* beta, int act, float act_alpha,
+                              const double* sums, long long P_global, const float* add, float* dy,
+                              long long ysp, long long ysc, float* dgamma, float* dbeta,
+                              int accumulate_affine, void* stream);
+
+/* ---- WGAN-GP double backward (GLI:655 create_graph=True, differentiated by GLI:658) ----
+ * Layer act(BN(y)) with batch statistics `stats`, whose create-graph backward took dh
+ * (the upstream gradient) to dy = BNback(dh act'(z)) with first-order sums
+ * first_sums = (sum e, sum e (y - mean)) [2C] (rgan_bn_backward_sums, global).  Given
+ * a = dP/d(dy) (all [P][C] with strides sp, sc):
+ *   rgan_bn_dd_sums stage 1: sums[3][C] = (sum a, sum a xhat, sum a e);
+ *                   stage 2 (only for act'' != 0: tanh, sigmoid, SELU; needs the global
+ *                   stage-1 sums): sums[2][C] = (sum t, sum t xhat);
+ *   rgan_bn_dd_apply: adj_dh = dP/d(dh) (nullable), ydir = the direct dP/dy of the
+ *                   double backward, dgamma2/dbeta2 (nullable, accumulate_affine: +=)
+ *                   its gamma/beta terms (from the *_local sums when given: under
+ *                   SyncBN the gradient all-reduce sums them over ranks).
+ * Cross-rank: the caller all-reduces first_sums and each stage's sums (SyncBN) and
+ * passes the global pixel count P_global.  partial: rgan_bn_dd_partial_bytes. */
+size_t rgan_bn_dd_partial_bytes(long long P, int C);
+int rgan_bn_dd_sums(const float* a, const float* y, const float* dh, long long P, int C,
+                    long long sp, long long sc, const float* stats, const float* gamma,
+                    const float* beta, int act, float act_alpha, int stage, const double* stage1,
+                    long long P_global, double* sums, void* partial, void* stream);
+int rgan_bn_dd_apply(const float* a, const float* y, const float* dh, long long P, int C,
+                     long long sp, long long sc, const float* stats, const float* gamma,
+                     const float* beta, int act, float act_alpha, const double* first_sums,
+                     const double* stage1, const double* stage2, const double* stage1_local,
+                     const double* stage2_local, long long P_global, float* adj_dh, float* ydir,
+                     float* dgamma2, float* dbeta2, int accumulate_affine, void* stream);
+/* Without BatchNorm (dy = dh act'(y), act_out = act(y)): adj_dh = a act'(y),
+ * ydir = a dh act''(y); either output nullable. */
+int rgan_act_dd(const float* a, const float* act_out, const float* dh, long long n, int act,
+                float act_alpha, float* adj_dh, float* ydir, void* stream);
+
 /* ---- elementwise ---- */
 /* dx = da * act'(a) where a = act(x) is the saved activation output. */
 int rgan_act_backward(const float* da, const float* a, long long n, int act, float act_alpha,
                       float* dx, void* stream);
-/* out[n] = sum over pixels of t (per channel; bias gradient), strided like bn. */
+/* dx = da * act'(a) + add (add nullable, same layout) */
+int rgan_act_backward_ex(const float* da, const float* a, const float* add, long long n, int act,
+                         float act_alpha, float* dx, void* stream);
+/* out[n] (+)= sum over pixels of t (per channel; bias gradient), strided like bn;
+ * accumulate != 0 adds into out (gradient accumulation, no separate add pass). */
 int rgan_channel_sum(const float* t, long long P, int C, long long sp, long long sc,
-                     float* out, void* partial, void* stream);
+                     float* out, int accumulate, void* stream);
 
 /* ---- loss heads (GLI:481-484, 592-644, 686-709) ----
  * kind = --loss_D (1..8); side 0 = D-real (heads 1-4) / D (heads 5-8), 1 = D-fake
@@ -233,7 +280,7 @@ int rgan_spectral_power(const float* W, int rows, int cols, long long rs, long l
 /* dW_orig = dW_eff/sigma - (<dW_eff, W_orig>/sigma^2) u v^T (u, v constants); ws >= 1 KiB. */
 int rgan_spectral_backward(const float* W, const float* dWeff, int rows, int cols,
                            long long rs, long long hs, int lo, const float* u, const float* v,
-                           const float* inv_sigma, float* dW, void* ws, void* stream);
+                           const float* inv_sigma, float* dW, int accumulate, void* ws, void* stream);
 
 /* ---- Adam (torch/optim/adam.py:347-547, _single_tensor_adam semantics) ----
  * Updates `ntensors` tensors (any count; launched in chunks).  hyper = device double[8]:

@@ -38,11 +38,11 @@ _SIGS = {
     "rgan_bn_segment_stats": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp]),
     "rgan_conv_dgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
-    "rgan_conv_wgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
+    "rgan_conv_wgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_sz, c_vp]),
     "rgan_nn_fold_weight": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
     "rgan_patches_k4s2": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "rgan_patch_weight": (c_int, [c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp]),
-    "rgan_unpatch_grad": (c_int, [c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp]),
+    "rgan_unpatch_grad": (c_int, [c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_int, c_vp]),
     "rgan_nn_unfold_grad": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
     "rgan_gather_images_u8": (c_int, [c_vp, c_vp, c_int, c_ll, c_vp, c_vp]),
     "rgan_minmax_ws_bytes": (c_sz, [c_ll]),
@@ -61,8 +61,17 @@ _SIGS = {
                               c_vp]),
     "rgan_bn_backward": (c_int, [c_vp, c_ll, c_ll, c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp, c_int, c_f,
                                  c_vp, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp]),
+    "rgan_bn_backward_apply_ex": (c_int, [c_vp, c_ll, c_ll, c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp, c_int,
+                                          c_f, c_vp, c_ll, c_vp, c_vp, c_ll, c_ll, c_vp, c_vp, c_int, c_vp]),
+    "rgan_bn_dd_partial_bytes": (c_sz, [c_ll, c_int]),
+    "rgan_bn_dd_sums": (c_int, [c_vp, c_vp, c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp, c_int, c_f, c_int, c_vp,
+                                c_ll, c_vp, c_vp, c_vp]),
+    "rgan_bn_dd_apply": (c_int, [c_vp, c_vp, c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp, c_int, c_f, c_vp, c_vp,
+                                 c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
+    "rgan_act_dd": (c_int, [c_vp, c_vp, c_vp, c_ll, c_int, c_f, c_vp, c_vp, c_vp]),
     "rgan_act_backward": (c_int, [c_vp, c_vp, c_ll, c_int, c_f, c_vp, c_vp]),
-    "rgan_channel_sum": (c_int, [c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp]),
+    "rgan_act_backward_ex": (c_int, [c_vp, c_vp, c_vp, c_ll, c_int, c_f, c_vp, c_vp]),
+    "rgan_channel_sum": (c_int, [c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_int, c_vp]),
     "rgan_loss_head": (c_int, [c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "rgan_loss_head_dist": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                                     c_vp]),
@@ -73,8 +82,8 @@ _SIGS = {
     "rgan_spectral_ws_bytes": (c_sz, [c_int, c_int]),
     "rgan_spectral_power": (c_int, [c_vp, c_int, c_int, c_ll, c_ll, c_int, c_f, c_vp, c_vp, c_vp, c_int, c_vp,
                                     c_vp]),
-    "rgan_spectral_backward": (c_int, [c_vp, c_vp, c_int, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                       c_vp]),
+    "rgan_spectral_backward": (c_int, [c_vp, c_vp, c_int, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
+                                       c_vp, c_vp]),
     "rgan_adam": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rgan_lr_decay": (c_int, [c_vp, c_d, c_vp]),
     "rgan_gather_images": (c_int, [c_vp, c_vp, c_int, c_ll, c_vp, c_vp]),

@@ -328,11 +328,17 @@ class ConvLayerFn(torch.autograd.Function):
                 dp.all_reduce_sum(sums)
                 K.bn_backward_apply(da_c, y[sl], stats[s_], gamma, beta, spec.act, spec.alpha, sums,
                                     P * dp.world(), need_affine=False, out=dy[sl])
+                dgamma = dg if dgamma is None or dg is None else dgamma + dg
+                dbeta = db if dbeta is None or db is None else dbeta + db
             else:
-                _, dg, db = K.bn_backward(da[sl], y[sl], stats[s_], gamma, beta, spec.act, spec.alpha,
-                                          need_affine=ng or nbeta, out=dy[sl])
-            dgamma = dg if dgamma is None or dg is None else dgamma + dg
-            dbeta = db if dbeta is None or db is None else dbeta + db
+                # the segments' affine gradients are summed in the apply kernel (segment 0
+                # writes, later segments add): no separate add pass
+                if s_ == 0:
+                    dgamma = torch.empty(C, dtype=torch.float32, device=y.device) if ng and gamma is not None else None
+                    dbeta = torch.empty(C, dtype=torch.float32, device=y.device) if nbeta and beta is not None else None
+                sums, da_c = K.bn_backward_sums(da[sl], y[sl], stats[s_], gamma, beta, spec.act, spec.alpha)
+                K.bn_backward_apply_ex(da_c, y[sl], stats[s_], gamma, beta, spec.act, spec.alpha, sums, P,
+                                       out=dy[sl], dgamma=dgamma, dbeta=dbeta, accumulate_affine=s_ > 0)
         return dy, dgamma, dbeta
 
     @staticmethod

@@ -67,6 +67,10 @@ static int max_chunks(long long P, int C) {
   return std::max(bn_geo(P, C, C, 1).chunks, bn_geo(P, C, 1, 2).chunks);
 }
 
+extern "C" size_t rgan_bn_dd_partial_bytes(long long P, int C) {
+  return (size_t)max_chunks(P, C) * 3 * C * sizeof(double) + 256;
+}
+
 extern "C" size_t rgan_bn_partial_bytes(long long P, int C) {
   // [chunks][2][C] partial sums + [2][C] merged sums + [3][C] moments, doubles
   return ((size_t)max_chunks(P, C) * 2 + 5) * C * sizeof(double) + 256;
@@ -507,7 +511,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ da
                                                     const float* __restrict__ beta, int act, float alpha,
                                                     const double* __restrict__ sums, double inv_pg,
                                                     float* __restrict__ dy, long long ysp, long long ysc,
-                                                    float* dgamma, float* dbeta, int tpr) {
+                                                    float* dgamma, float* dbeta, int tpr,
+                                                    const float* __restrict__ add, int accum_affine) {
   const int tid = threadIdx.x, lc = tid % tpr, rl = tid / tpr, rp = blockDim.x / tpr;
   const int c0 = (blockIdx.x * tpr + lc) * Q;
   if (c0 >= C) return;
@@ -522,8 +527,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ da
     k1[q] = (float)(sums[c] * inv_pg);
     k2[q] = (float)(sums[C + c] * (double)inv * (double)inv * inv_pg);
     if (blockIdx.y == 0 && rl == 0 && c0 + q < C) {
-      if (dbeta) dbeta[c] = (float)sums[c];
-      if (dgamma) dgamma[c] = (float)(sums[C + c] * (double)inv);
+      const float db = (float)sums[c], dg = (float)(sums[C + c] * (double)inv);
+      if (dbeta) dbeta[c] = accum_affine ? dbeta[c] + db : db;
+      if (dgamma) dgamma[c] = accum_affine ? dgamma[c] + dg : dg;
     }
   }
   const long long step = (long long)gridDim.y * rp;
@@ -532,6 +538,12 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ da
     for (int q = 0; q < Q; ++q) {
       const float gz = g[q] * act_grad_from_in(v[q] * al[q] + be[q], act, alpha);
       v[q] = al[q] * (gz - k1[q] - (v[q] - mean[q]) * k2[q]);
+    }
+    if (add) {
+      float w[Q];
+      load_q<Q>(add, p * ysp + (long long)c0 * ysc, w);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) v[q] += w[q];
     }
     if constexpr (Q == 4) {
       *reinterpret_cast<float4*>(dy + p * ysp + c0) = make_float4(v[0], v[1], v[2], v[3]);
@@ -586,25 +598,38 @@ extern "C" int rgan_bn_backward_sums(const float* da, long long dsp, long long d
   return 0;
 }
 
+extern "C" int rgan_bn_backward_apply_ex(const float* da, long long dsp, long long dsc, const float* y,
+                                         long long P, int C, long long sp, long long sc, const float* stats,
+                                         const float* gamma, const float* beta, int act, float act_alpha,
+                                         const double* sums, long long P_global, const float* add, float* dy,
+                                         long long ysp, long long ysc, float* dgamma, float* dbeta,
+                                         int accumulate_affine, void* stream) {
+  RGAN_REQUIRE(da && y && stats && sums && dy && P > 0 && C > 0 && P_global >= P);
+  hipStream_t s = (hipStream_t)stream;
+  BnGeo g = bn_geo(P, C, sp, sc);
+  const bool vec = g.vec && dense_nhwc(sp, sc, C, y) && dense_nhwc(dsp, dsc, C, da) &&
+                   dense_nhwc(ysp, ysc, C, dy) && (!add || ((uintptr_t)add & 15) == 0);
+  if (!vec && g.vec) g = bn_geo(P, C, 1, 2);
+  const double inv_pg = 1.0 / (double)P_global;
+  if (vec)
+    bn_bwd_apply<4><<<apply_grid(g, P), 256, 0, s>>>(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act,
+                                                    act_alpha, sums, inv_pg, dy, ysp, ysc, dgamma, dbeta, g.tpr,
+                                                    add, accumulate_affine);
+  else
+    bn_bwd_apply<1><<<apply_grid(g, P), 256, 0, s>>>(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act,
+                                                    act_alpha, sums, inv_pg, dy, ysp, ysc, dgamma, dbeta, g.tpr,
+                                                    add, accumulate_affine);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int rgan_bn_backward_apply(const float* da, long long dsp, long long dsc, const float* y, long long P,
                                       int C, long long sp, long long sc, const float* stats, const float* gamma,
                                       const float* beta, int act, float act_alpha, const double* sums,
                                       long long P_global, float* dy, long long ysp, long long ysc, float* dgamma,
                                       float* dbeta, void* stream) {
-  RGAN_REQUIRE(da && y && stats && sums && dy && P > 0 && C > 0 && P_global >= P);
-  hipStream_t s = (hipStream_t)stream;
-  BnGeo g = bn_geo(P, C, sp, sc);
-  const bool vec = g.vec && dense_nhwc(sp, sc, C, y) && dense_nhwc(dsp, dsc, C, da) && dense_nhwc(ysp, ysc, C, dy);
-  if (!vec && g.vec) g = bn_geo(P, C, 1, 2);
-  const double inv_pg = 1.0 / (double)P_global;
-  if (vec)
-    bn_bwd_apply<4><<<apply_grid(g, P), 256, 0, s>>>(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act,
-                                                    act_alpha, sums, inv_pg, dy, ysp, ysc, dgamma, dbeta, g.tpr);
-  else
-    bn_bwd_apply<1><<<apply_grid(g, P), 256, 0, s>>>(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act,
-                                                    act_alpha, sums, inv_pg, dy, ysp, ysc, dgamma, dbeta, g.tpr);
-  RGAN_CHECK_LAUNCH();
-  return 0;
+  return rgan_bn_backward_apply_ex(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, sums,
+                                   P_global, nullptr, dy, ysp, ysc, dgamma, dbeta, 0, stream);
 }
 
 extern "C" int rgan_bn_backward(const float* da, long long dsp, long long dsc, const float* y, long long P,
@@ -620,37 +645,315 @@ extern "C" int rgan_bn_backward(const float* da, long long dsp, long long dsc, c
                                 dy, ysp, ysc, dgamma, dbeta, stream);
 }
 
+// ------------------------------------------------------------------ WGAN-GP double backward
+// The penalty (GLI:646-658) differentiates the create-graph backward of every D layer.
+// Through train-mode BatchNorm2d + activation that backward is (per channel, N pixels):
+//   xhat = (y - mean) invstd,  z = gamma xhat + beta,  e = dh act'(z),
+//   dy = s (e - mean(e) - xhat mean(e xhat)),  s = gamma invstd.
+// Given a = dP/d(dy) (the adjoint conv of the layer's dgrad), the adjoints are
+//   dP/de   = pe = s (a - A - xhat Ax),         A = mean(a), Ax = mean(a xhat)
+//   dP/d(dh) = pe act'(z)                        (feeds the next layer's adjoint conv)
+//   t       = pe dh act''(z)                     (0 for ReLU / LeakyReLU)
+//   gx      = -s (a c + e Ax) + gamma t          (dP/dxhat, c = mean(e xhat))
+//   dP/dy   = invstd (gx - mean(gx) - xhat mean(gx xhat)) - dPds gamma invstd^2 xhat / N
+//   dPds    = sum a e - mean(e) sum a - c sum a xhat     (s = gamma invstd depends on y)
+//   dgamma += dPds invstd + sum t xhat,  dbeta += sum t.
+// mean(gx) and mean(gx xhat) follow from the stage sums, so one elementwise pass writes
+// both outputs: stage 1 sums (a, a xhat, a e); stage 2 (only when act'' != 0) sums (t, t xhat).
+template <int Q, int STAGE>
+__global__ __launch_bounds__(256) void bn_dd_partial(const float* __restrict__ a, const float* __restrict__ y,
+                                                     const float* __restrict__ dh, long long P, int C, long long sp,
+                                                     long long sc, const float* __restrict__ stats,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     int act, float alpha, const double* __restrict__ s1,
+                                                     double inv_pg, int tpr, long long rows,
+                                                     double* __restrict__ part) {
+  constexpr int NS = STAGE == 1 ? 3 : 2;
+  __shared__ double sh[NS][256][Q];
+  const int tid = threadIdx.x, lc = tid % tpr, rl = tid / tpr, rp = blockDim.x / tpr;
+  const int c0 = (blockIdx.y * tpr + lc) * Q;
+  const long long p0 = blockIdx.x * rows, p1 = min(P, p0 + rows);
+  double acc[NS][Q];
+  float mean[Q], inv[Q], gam[Q], bet[Q], sg[Q], A[Q], Ax[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+#pragma unroll
+    for (int k = 0; k < NS; ++k) acc[k][q] = 0.0;
+    const int c = min(c0 + q, C - 1);
+    mean[q] = stats[c];
+    inv[q] = stats[C + c];
+    gam[q] = gamma ? gamma[c] : 1.f;
+    bet[q] = beta ? beta[c] : 0.f;
+    sg[q] = gam[q] * inv[q];
+    A[q] = STAGE == 2 ? (float)(s1[c] * inv_pg) : 0.f;
+    Ax[q] = STAGE == 2 ? (float)(s1[C + c] * inv_pg) : 0.f;
+  }
+  if (c0 < C) {
+    for (long long p = p0 + rl; p < p1; p += rp) {
+      float va[Q], vy[Q], vd[Q];
+      const long long off = p * sp + (long long)c0 * sc;
+      load_q<Q>(a, off, va);
+      load_q<Q>(y, off, vy);
+      load_q<Q>(dh, off, vd);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const float xh = (vy[q] - mean[q]) * inv[q], z = gam[q] * xh + bet[q];
+        if constexpr (STAGE == 1) {
+          const float e = vd[q] * act_grad_from_in(z, act, alpha);
+          acc[0][q] += (double)va[q];
+          acc[1][q] += (double)(va[q] * xh);
+          acc[2][q] += (double)(va[q] * e);
+        } else {
+          const float pe = sg[q] * (va[q] - A[q] - xh * Ax[q]);
+          const float t = pe * vd[q] * act_grad2_from_in(z, act, alpha);
+          acc[0][q] += (double)t;
+          acc[1][q] += (double)(t * xh);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NS; ++k)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) sh[k][tid][q] = acc[k][q];
+  __syncthreads();
+  if (rl == 0 && c0 < C) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      if (c0 + q >= C) continue;
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        double t = 0.0;
+        for (int r = 0; r < rp; ++r) t += sh[k][r * tpr + lc][q];
+        part[((size_t)blockIdx.x * NS + k) * C + c0 + q] = t;
+      }
+    }
+  }
+}
+
+// [chunks][NS][C] partials -> [NS][C] totals, fixed order (bn_merge's layout, NS rows)
+template <int NS>
+__global__ __launch_bounds__(1024) void bn_merge_n(const double* __restrict__ part, int chunks, int C,
+                                                   double* __restrict__ out) {
+  __shared__ double sh[NS][MERGE_ROWS][MERGE_CPB];
+  const int cl = threadIdx.x % MERGE_CPB, r = threadIdx.x / MERGE_CPB;
+  const int c = blockIdx.x * MERGE_CPB + cl;
+  double acc[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) acc[k] = 0.0;
+  if (c < C)
+    for (int j = r; j < chunks; j += MERGE_ROWS)
+#pragma unroll
+      for (int k = 0; k < NS; ++k) acc[k] += part[((size_t)j * NS + k) * C + c];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) sh[k][r][cl] = acc[k];
+  __syncthreads();
+  if (r != 0 || c >= C) return;
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    double t = 0.0;
+    for (int q = 0; q < MERGE_ROWS; ++q) t += sh[k][q][cl];
+    out[(size_t)k * C + c] = t;
+  }
+}
+
+template <int Q>
+__global__ __launch_bounds__(256) void bn_dd_apply(const float* __restrict__ a, const float* __restrict__ y,
+                                                   const float* __restrict__ dh, long long P, int C, long long sp,
+                                                   long long sc, const float* __restrict__ stats,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   int act, float alpha, const double* __restrict__ fs,
+                                                   const double* __restrict__ s1, const double* __restrict__ s2,
+                                                   const double* __restrict__ s1l, const double* __restrict__ s2l,
+                                                   double inv_pg, float* __restrict__ adj_dh,
+                                                   float* __restrict__ ydir, float* dgamma2, float* dbeta2,
+                                                   int accum_affine, int tpr) {
+  const int tid = threadIdx.x, lc = tid % tpr, rl = tid / tpr, rp = blockDim.x / tpr;
+  const int c0 = (blockIdx.x * tpr + lc) * Q;
+  if (c0 >= C) return;
+  const bool two = act_has_grad2(act);
+  float mean[Q], inv[Q], gam[Q], bet[Q], sg[Q], A[Q], Ax[Q], c1[Q], mgx[Q], mgxx[Q], kk[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int c = min(c0 + q, C - 1);
+    const double dinv = stats[C + c], dgam = gamma ? gamma[c] : 1.0, ds = dgam * dinv;
+    mean[q] = stats[c];
+    inv[q] = (float)dinv;
+    gam[q] = (float)dgam;
+    bet[q] = beta ? beta[c] : 0.f;
+    sg[q] = (float)ds;
+    const double em = fs[c] * inv_pg, dc1 = dinv * fs[C + c] * inv_pg;
+    const double dA = s1[c] * inv_pg, dAx = s1[C + c] * inv_pg;
+    const double dPds = s1[2 * C + c] - em * s1[c] - dc1 * s1[C + c];
+    const double T0 = s2 ? s2[c] : 0.0, T1 = s2 ? s2[C + c] : 0.0;
+    A[q] = (float)dA;
+    Ax[q] = (float)dAx;
+    c1[q] = (float)dc1;
+    mgx[q] = (float)(-ds * (dc1 * dA + dAx * em) + dgam * T0 * inv_pg);
+    mgxx[q] = (float)(-2.0 * ds * dc1 * dAx + dgam * T1 * inv_pg);
+    kk[q] = (float)(dPds * dgam * dinv * dinv * inv_pg);
+    if (blockIdx.y == 0 && rl == 0 && c0 + q < C) {
+      const double dPl = s1l[2 * C + c] - em * s1l[c] - dc1 * s1l[C + c];
+      const float dg = (float)(dPl * dinv + (s2l ? s2l[C + c] : 0.0));
+      const float db = (float)(s2l ? s2l[c] : 0.0);
+      if (dgamma2) dgamma2[c] = accum_affine ? dgamma2[c] + dg : dg;
+      if (dbeta2) dbeta2[c] = accum_affine ? dbeta2[c] + db : db;
+    }
+  }
+  const long long step = (long long)gridDim.y * rp;
+  for (long long p = (long long)blockIdx.y * rp + rl; p < P; p += step) {
+    float va[Q], vy[Q], vd[Q], oh[Q], oy[Q];
+    const long long off = p * sp + (long long)c0 * sc;
+    load_q<Q>(a, off, va);
+    load_q<Q>(y, off, vy);
+    load_q<Q>(dh, off, vd);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const float xh = (vy[q] - mean[q]) * inv[q], z = gam[q] * xh + bet[q];
+      const float d1 = act_grad_from_in(z, act, alpha), e = vd[q] * d1;
+      const float pe = sg[q] * (va[q] - A[q] - xh * Ax[q]);
+      oh[q] = pe * d1;
+      const float t = two ? pe * vd[q] * act_grad2_from_in(z, act, alpha) : 0.f;
+      const float gx = -sg[q] * (va[q] * c1[q] + e * Ax[q]) + gam[q] * t;
+      oy[q] = inv[q] * (gx - mgx[q] - xh * mgxx[q]) - kk[q] * xh;
+    }
+    if constexpr (Q == 4) {
+      if (adj_dh) *reinterpret_cast<float4*>(adj_dh + off) = make_float4(oh[0], oh[1], oh[2], oh[3]);
+      *reinterpret_cast<float4*>(ydir + off) = make_float4(oy[0], oy[1], oy[2], oy[3]);
+    } else {
+      if (adj_dh) adj_dh[off] = oh[0];
+      ydir[off] = oy[0];
+    }
+  }
+}
+
+extern "C" int rgan_bn_dd_sums(const float* a, const float* y, const float* dh, long long P, int C, long long sp,
+                               long long sc, const float* stats, const float* gamma, const float* beta, int act,
+                               float act_alpha, int stage, const double* stage1, long long P_global, double* sums,
+                               void* partial, void* stream) {
+  RGAN_REQUIRE(a && y && dh && stats && sums && partial && P > 0 && C > 0 && (stage == 1 || stage == 2));
+  RGAN_REQUIRE(stage == 1 || (stage1 && P_global >= P));
+  hipStream_t s = (hipStream_t)stream;
+  BnGeo g = bn_geo(P, C, sp, sc);
+  const bool vec = g.vec && dense_nhwc(sp, sc, C, a) && dense_nhwc(sp, sc, C, y) && dense_nhwc(sp, sc, C, dh);
+  if (!vec && g.vec) g = bn_geo(P, C, 1, 2);
+  double* part = (double*)partial;
+  const dim3 grid(g.chunks, g.cgroups);
+  const double inv_pg = stage == 2 ? 1.0 / (double)P_global : 0.0;
+#define RGAN_DD(QQ, ST) \
+  bn_dd_partial<QQ, ST><<<grid, 256, 0, s>>>(a, y, dh, P, C, sp, sc, stats, gamma, beta, act, act_alpha, stage1, \
+                                             inv_pg, g.tpr, g.rows, part)
+  if (stage == 1) {
+    if (vec) RGAN_DD(4, 1); else RGAN_DD(1, 1);
+  } else {
+    if (vec) RGAN_DD(4, 2); else RGAN_DD(1, 2);
+  }
+#undef RGAN_DD
+  RGAN_CHECK_LAUNCH();
+  if (stage == 1)
+    bn_merge_n<3><<<ceil_div(C, MERGE_CPB), 1024, 0, s>>>(part, g.chunks, C, sums);
+  else
+    bn_merge_n<2><<<ceil_div(C, MERGE_CPB), 1024, 0, s>>>(part, g.chunks, C, sums);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int rgan_bn_dd_apply(const float* a, const float* y, const float* dh, long long P, int C, long long sp,
+                                long long sc, const float* stats, const float* gamma, const float* beta, int act,
+                                float act_alpha, const double* first_sums, const double* stage1,
+                                const double* stage2, const double* stage1_local, const double* stage2_local,
+                                long long P_global, float* adj_dh, float* ydir, float* dgamma2, float* dbeta2,
+                                int accumulate_affine, void* stream) {
+  RGAN_REQUIRE(a && y && dh && stats && first_sums && stage1 && ydir && P > 0 && C > 0 && P_global >= P);
+  RGAN_REQUIRE(!act_has_grad2(act) || stage2);
+  hipStream_t s = (hipStream_t)stream;
+  BnGeo g = bn_geo(P, C, sp, sc);
+  const bool vec = g.vec && dense_nhwc(sp, sc, C, a) && dense_nhwc(sp, sc, C, y) && dense_nhwc(sp, sc, C, dh) &&
+                   dense_nhwc(sp, sc, C, ydir) && (!adj_dh || dense_nhwc(sp, sc, C, adj_dh));
+  if (!vec && g.vec) g = bn_geo(P, C, 1, 2);
+  const double inv_pg = 1.0 / (double)P_global;
+  const double* s1l = stage1_local ? stage1_local : stage1;
+  const double* s2l = stage2_local ? stage2_local : stage2;
+  if (vec)
+    bn_dd_apply<4><<<apply_grid(g, P), 256, 0, s>>>(a, y, dh, P, C, sp, sc, stats, gamma, beta, act, act_alpha,
+                                                   first_sums, stage1, stage2, s1l, s2l, inv_pg, adj_dh, ydir,
+                                                   dgamma2, dbeta2, accumulate_affine, g.tpr);
+  else
+    bn_dd_apply<1><<<apply_grid(g, P), 256, 0, s>>>(a, y, dh, P, C, sp, sc, stats, gamma, beta, act, act_alpha,
+                                                   first_sums, stage1, stage2, s1l, s2l, inv_pg, adj_dh, ydir,
+                                                   dgamma2, dbeta2, accumulate_affine, g.tpr);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+// The same without BatchNorm: dy = dh act'(y) (act from its output o = act(y)):
+//   dP/d(dh) = a act'(y),  dP/dy = a dh act''(y)  (ydir nullable: only when act'' != 0)
+__global__ void act_dd_kernel(const float* __restrict__ a, const float* __restrict__ o,
+                              const float* __restrict__ dh, long long n, int act, float alpha,
+                              float* __restrict__ adj_dh, float* __restrict__ ydir) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float v = a[i], out = o[i];
+    if (adj_dh) adj_dh[i] = v * act_grad_from_out(out, act, alpha);
+    if (ydir) ydir[i] = v * dh[i] * act_grad2_from_out(out, act, alpha);
+  }
+}
+
+extern "C" int rgan_act_dd(const float* a, const float* act_out, const float* dh, long long n, int act,
+                           float act_alpha, float* adj_dh, float* ydir, void* stream) {
+  RGAN_REQUIRE(a && act_out && n >= 0 && (adj_dh || ydir) && (!ydir || dh));
+  if (n == 0) return 0;
+  const int blocks = (int)std::max<long long>(1, std::min<long long>((n + 255) / 256, 8192));
+  act_dd_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(a, act_out, dh, n, act, act_alpha, adj_dh, ydir);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
 // ------------------------------------------------------------------ activations
 __global__ void act_bwd_kernel(const float* __restrict__ da, const float* __restrict__ a, long long n, int act,
-                               float alpha, float* __restrict__ dx, int vec) {
+                               float alpha, float* __restrict__ dx, int vec, const float* __restrict__ add) {
   const long long n4 = vec ? n >> 2 : 0;
   const float4* da4 = reinterpret_cast<const float4*>(da);
   const float4* a4 = reinterpret_cast<const float4*>(a);
+  const float4* add4 = reinterpret_cast<const float4*>(add);
   float4* dx4 = reinterpret_cast<float4*>(dx);
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride) {
     const float4 g = da4[i], v = a4[i];
-    dx4[i] = make_float4(g.x * act_grad_from_out(v.x, act, alpha), g.y * act_grad_from_out(v.y, act, alpha),
-                         g.z * act_grad_from_out(v.z, act, alpha), g.w * act_grad_from_out(v.w, act, alpha));
+    float4 o = make_float4(g.x * act_grad_from_out(v.x, act, alpha), g.y * act_grad_from_out(v.y, act, alpha),
+                           g.z * act_grad_from_out(v.z, act, alpha), g.w * act_grad_from_out(v.w, act, alpha));
+    if (add) {
+      const float4 w = add4[i];
+      o.x += w.x; o.y += w.y; o.z += w.z; o.w += w.w;
+    }
+    dx4[i] = o;
   }
   for (long long i = (n4 << 2) + blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += stride)
-    dx[i] = da[i] * act_grad_from_out(a[i], act, alpha);
+    dx[i] = da[i] * act_grad_from_out(a[i], act, alpha) + (add ? add[i] : 0.f);
 }
 
 extern "C" int rgan_act_backward(const float* da, const float* a, long long n, int act, float act_alpha,
                                  float* dx, void* stream) {
   RGAN_REQUIRE(da && a && dx && n >= 0);
   if (n == 0) return 0;
-  const int vec = ((((uintptr_t)da | (uintptr_t)a | (uintptr_t)dx) & 15) == 0) ? 1 : 0;
+  return rgan_act_backward_ex(da, a, nullptr, n, act, act_alpha, dx, stream);
+}
+
+extern "C" int rgan_act_backward_ex(const float* da, const float* a, const float* add, long long n, int act,
+                                    float act_alpha, float* dx, void* stream) {
+  RGAN_REQUIRE(da && a && dx && n >= 0);
+  if (n == 0) return 0;
+  const int vec = ((((uintptr_t)da | (uintptr_t)a | (uintptr_t)dx | (uintptr_t)add) & 15) == 0) ? 1 : 0;
   const int blocks = (int)std::max<long long>(1, std::min<long long>((n / 4 + 255) / 256, 4096));
-  act_bwd_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(da, a, n, act, act_alpha, dx, vec);
+  act_bwd_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(da, a, n, act, act_alpha, dx, vec, add);
   RGAN_CHECK_LAUNCH();
   return 0;
 }
 
 // per-channel sum over pixels (bias gradients); one block per 64 channels, fixed order, double
 __global__ __launch_bounds__(256) void channel_sum_kernel(const float* __restrict__ t, long long P, int C,
-                                                          long long sp, long long sc, float* __restrict__ out) {
+                                                          long long sp, long long sc, float* __restrict__ out,
+                                                          int accum) {
   __shared__ double sh[4][64];
   const int lane = threadIdx.x & 63, row = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
@@ -659,14 +962,16 @@ __global__ __launch_bounds__(256) void channel_sum_kernel(const float* __restric
     for (long long p = row; p < P; p += 4) s += t[p * sp + c * sc];
   sh[row][lane] = s;
   __syncthreads();
-  if (row == 0 && c < C) out[c] = (float)(sh[0][lane] + sh[1][lane] + sh[2][lane] + sh[3][lane]);
+  if (row == 0 && c < C) {
+    const float v = (float)(sh[0][lane] + sh[1][lane] + sh[2][lane] + sh[3][lane]);
+    out[c] = accum ? out[c] + v : v;
+  }
 }
 
 extern "C" int rgan_channel_sum(const float* t, long long P, int C, long long sp, long long sc, float* out,
-                                void* partial, void* stream) {
-  (void)partial;
+                                int accumulate, void* stream) {
   RGAN_REQUIRE(t && out && P > 0 && C > 0);
-  channel_sum_kernel<<<ceil_div(C, 64), 256, 0, (hipStream_t)stream>>>(t, P, C, sp, sc, out);
+  channel_sum_kernel<<<ceil_div(C, 64), 256, 0, (hipStream_t)stream>>>(t, P, C, sp, sc, out, accumulate);
   RGAN_CHECK_LAUNCH();
   return 0;
 }

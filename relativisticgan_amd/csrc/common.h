@@ -66,6 +66,39 @@ __device__ __forceinline__ float act_grad_from_in(float x, int act, float alpha)
   }
 }
 
+// second derivative of act through its INPUT x (0 for the piecewise-linear ReLU/LeakyReLU):
+// the WGAN-GP double backward differentiates act' itself
+__device__ __forceinline__ float act_grad2_from_in(float x, int act, float alpha) {
+  (void)alpha;
+  switch (act) {
+    case RGAN_ACT_TANH: { float t = tanhf(x); return -2.f * t * (1.f - t * t); }
+    case RGAN_ACT_SIGMOID: { float s = 1.f / (1.f + expf(-x)); return s * (1.f - s) * (1.f - 2.f * s); }
+    case RGAN_ACT_SELU: {
+      const float sa = 1.7580993408473768599402175208123f;
+      return x > 0.f ? 0.f : sa * expf(x);
+    }
+    default: return 0.f;
+  }
+}
+
+// the same through the OUTPUT a = act(x)
+__device__ __forceinline__ float act_grad2_from_out(float a, int act, float alpha) {
+  (void)alpha;
+  switch (act) {
+    case RGAN_ACT_TANH: return -2.f * a * (1.f - a * a);
+    case RGAN_ACT_SIGMOID: return a * (1.f - a) * (1.f - 2.f * a);
+    case RGAN_ACT_SELU: {
+      const float sa = 1.7580993408473768599402175208123f;
+      return a > 0.f ? 0.f : a + sa;
+    }
+    default: return 0.f;
+  }
+}
+
+__host__ __device__ inline bool act_has_grad2(int act) {
+  return act == RGAN_ACT_TANH || act == RGAN_ACT_SIGMOID || act == RGAN_ACT_SELU;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

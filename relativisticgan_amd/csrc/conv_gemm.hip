@@ -92,6 +92,7 @@ struct GemmArgs {
   int vec_out;            // output n-quads contiguous and 16-B aligned (host-checked)
   int xgroup, nph;        // XCD-grouped tile order (blocks sharing A rows on one XCD); phases
   double* bnp;            // nullable: BatchNorm moments of every 64-row output segment (vector epilogue)
+  int accum;              // WGRAD: add into C (gradient accumulation) instead of overwriting it
 };
 
 __device__ __forceinline__ long long row_offset(const OutMap& o, int m, int phase) {
@@ -837,7 +838,11 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
 #if RGAN_EXP_NOSTORE  // timing-only experiment: drop the output stores
           if (v == 1234.5f)
 #endif
-          g.C[moff[rl] + noff[cl]] = act_fwd(v, g.act, g.alpha);
+          {
+            float* dst = g.C + moff[rl] + noff[cl];
+            v = act_fwd(v, g.act, g.alpha);
+            *dst = (MODE == MODE_WGRAD && g.accum) ? *dst + v : v;
+          }
         }
       }
     }
@@ -903,8 +908,14 @@ __global__ __launch_bounds__(256) void splitk_reduce(GemmArgs g, FastDiv fdiv, u
       red_sum<4>(base + (size_t)m * g.N + n, MN, g.splits, v);
       const float4 o = make_float4(red_epi(g, v[0], wsc, n), red_epi(g, v[1], wsc, n + 1),
                                    red_epi(g, v[2], wsc, n + 2), red_epi(g, v[3], wsc, n + 3));
-      *reinterpret_cast<float4*>(g.C + row_offset(g.out, (int)m, MODE == MODE_CONVT2 ? phase : 0) +
-                                 col_offset(g.out, n)) = o;
+      float4* dst = reinterpret_cast<float4*>(g.C + row_offset(g.out, (int)m, MODE == MODE_CONVT2 ? phase : 0) +
+                                              col_offset(g.out, n));
+      if (g.accum) {
+        const float4 q = *dst;
+        *dst = make_float4(q.x + o.x, q.y + o.y, q.z + o.z, q.w + o.w);
+      } else {
+        *dst = o;
+      }
     } else if constexpr (KIND == RED_TAPS) {
       const uint32_t mc = idx >> 2;                   // fdiv = channels c
       const int q = (int)(idx & 3);                   // taps 4q .. 4q+3 (kh = q)
@@ -919,15 +930,20 @@ __global__ __launch_bounds__(256) void splitk_reduce(GemmArgs g, FastDiv fdiv, u
         red_sum<1>(s + (size_t)(4 * q + i) * nc, MN, g.splits, w);
         v[i] = red_epi(g, w[0], wsc, (4 * q + i) * nc + c);
       }
-      *reinterpret_cast<float4*>(g.C + (long long)m * g.out.sb + (long long)c * 16 + 4 * q) =
-          make_float4(v[0], v[1], v[2], v[3]);
+      float4* dst = reinterpret_cast<float4*>(g.C + (long long)m * g.out.sb + (long long)c * 16 + 4 * q);
+      if (g.accum) {
+        const float4 o = *dst;
+        v[0] += o.x; v[1] += o.y; v[2] += o.z; v[3] += o.w;
+      }
+      *dst = make_float4(v[0], v[1], v[2], v[3]);
     } else {
       const uint32_t m = fdiv.div(idx);               // fdiv = N
       const int n = (int)(idx - m * fdiv.d);
       float v[1];
       red_sum<1>(base + (size_t)m * g.N + n, MN, g.splits, v);
-      g.C[row_offset(g.out, (int)m, MODE == MODE_CONVT2 ? phase : 0) + col_offset(g.out, n)] =
-          red_epi(g, v[0], wsc, n);
+      float* dst = g.C + row_offset(g.out, (int)m, MODE == MODE_CONVT2 ? phase : 0) + col_offset(g.out, n);
+      const float o = red_epi(g, v[0], wsc, n);
+      *dst = g.accum ? *dst + o : o;
     }
   }
 }
@@ -956,6 +972,7 @@ struct DenseArgs {
   int act;
   float alpha;
   int vec;
+  int accum;                  // wgrad: add into out
 };
 
 __device__ __forceinline__ long long dense_x_off(const DenseArgs& a, int e, int& widx) {
@@ -1034,7 +1051,7 @@ __global__ __launch_bounds__(256) void dense1_wgrad(DenseArgs a) {
   float acc = 0.f;
 #pragma unroll 16
   for (int b = 0; b < a.B; ++b) acc = fmaf(a.y[(long long)b * a.ysb], a.x[(long long)b * a.xsb + xo], acc);
-  a.out[wi] = acc;
+  a.out[wi] = a.accum ? a.out[wi] + acc : acc;
 }
 
 // WGRAD with 4x4 taps: the GEMM writes C[co][(tap, ci)] with whole-row float4 stores
@@ -1044,7 +1061,7 @@ __global__ __launch_bounds__(256) void dense1_wgrad(DenseArgs a) {
 // 16 taps x 64 channels per block through LDS; reads 256-B rows, writes 4 KiB runs.
 constexpr int TT_LD = 68;  // (16 t + ci) distinct mod 64 on the read side
 __global__ __launch_bounds__(256) void taps_transpose(const float* __restrict__ T, float* __restrict__ O, int Cin,
-                                                      long long osb) {
+                                                      long long osb, int accum) {
   __shared__ float sh[16 * TT_LD];
   const int co = blockIdx.y, c0 = blockIdx.x * 64;
   const float* src = T + (size_t)co * 16 * Cin;
@@ -1057,10 +1074,16 @@ __global__ __launch_bounds__(256) void taps_transpose(const float* __restrict__ 
   }
   __syncthreads();
   const int ci = threadIdx.x >> 2, tq = threadIdx.x & 3;
-  if (c0 + ci < Cin)
-    *reinterpret_cast<float4*>(O + (long long)co * osb + (long long)(c0 + ci) * 16 + 4 * tq) =
-        make_float4(sh[(4 * tq) * TT_LD + ci], sh[(4 * tq + 1) * TT_LD + ci], sh[(4 * tq + 2) * TT_LD + ci],
-                    sh[(4 * tq + 3) * TT_LD + ci]);
+  if (c0 + ci < Cin) {
+    float4* dst = reinterpret_cast<float4*>(O + (long long)co * osb + (long long)(c0 + ci) * 16 + 4 * tq);
+    float4 v = make_float4(sh[(4 * tq) * TT_LD + ci], sh[(4 * tq + 1) * TT_LD + ci], sh[(4 * tq + 2) * TT_LD + ci],
+                           sh[(4 * tq + 3) * TT_LD + ci]);
+    if (accum) {
+      const float4 o = *dst;
+      v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+    }
+    *dst = v;
+  }
 }
 
 // ---------------------------------------------------------------- weight packing
@@ -2090,9 +2113,11 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   float* tap_dst = nullptr;
   long long tap_osb = 0;
   if (p.tap_stage && !aligned16(p.g.C)) p.tap_stage = false;  // workspace stays sized for it
+  const int accum = p.g.accum;
   if (p.tap_stage) {
     tap_dst = p.g.C;
     tap_osb = p.g.out.sb;
+    p.g.accum = 0;  // the staging buffer is written fresh; taps_transpose accumulates
     p.g.C = (float*)(w + align_up(p.slab_floats * 4, 256));
     p.g.out = make_out(1, 1, 1, p.g.N, 0, 0, 1, 1, p.g.N, 0, 0, 1);  // [M][N], n contiguous
   }
@@ -2130,9 +2155,10 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     hipEventRecord(rec.b, s);
     g_recs.push_back(rec);
   }
+  p.g.accum = accum;
   if (p.tap_stage) {
     const int cin = p.g.N / 16;
-    taps_transpose<<<dim3(ceil_div(cin, 64), p.g.M), 256, 0, s>>>(p.g.C, tap_dst, cin, tap_osb);
+    taps_transpose<<<dim3(ceil_div(cin, 64), p.g.M), 256, 0, s>>>(p.g.C, tap_dst, cin, tap_osb, p.g.accum);
     RGAN_CHECK_LAUNCH();
   }
   if (p.g.splits > 1) {
@@ -2274,12 +2300,14 @@ extern "C" int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* 
 }
 
 extern "C" int rgan_conv_wgrad(const RganConv* d, const float* x, const float* dy, float* dw,
-                               float* dbias, void* ws, size_t ws_bytes, void* stream) {
+                               float* dbias, int accumulate, void* ws, size_t ws_bytes, void* stream) {
   if (!x || !dy || !dw) return RGAN_EINVAL;
   g_cur_flops = conv_flops(d);
   Plan p;
   int rc = plan_wgrad(d, x, dy, dw, p);
   if (rc) return rc;
+  p.g.accum = accumulate ? 1 : 0;
+  p.da.accum = p.g.accum;
   rc = run_plan(p, ws, ws_bytes, (hipStream_t)stream);
   if (rc) return rc;
   if (dbias) {
@@ -2294,7 +2322,7 @@ extern "C" int rgan_conv_wgrad(const RganConv* d, const float* x, const float* d
         return RGAN_EINVAL;
       sp = d->cout;
     }
-    return rgan_channel_sum(dy, P, d->cout, sp, d->ys[1], dbias, nullptr, stream);
+    return rgan_channel_sum(dy, P, d->cout, sp, d->ys[1], dbias, accumulate, stream);
   }
   return 0;
 }

@@ -407,7 +407,8 @@ __global__ __launch_bounds__(256) void sn_dot_kernel(SnView w, const float* __re
 __global__ __launch_bounds__(256) void sn_bwd_kernel(SnView w, const float* __restrict__ dWe,
                                                      const float* __restrict__ part, int nparts,
                                                      const float* __restrict__ u, const float* __restrict__ v,
-                                                     const float* __restrict__ inv_sigma, float* __restrict__ dW) {
+                                                     const float* __restrict__ inv_sigma, float* __restrict__ dW,
+                                                     int accum) {
   __shared__ float kk;
   if (threadIdx.x == 0) {
     float d = 0.f;
@@ -422,13 +423,14 @@ __global__ __launch_bounds__(256) void sn_bwd_kernel(SnView w, const float* __re
        i += (long long)gridDim.x * blockDim.x) {
     const int r = (int)(i / w.cols), c = (int)(i - (long long)r * w.cols);
     const long long o = w.off(r, c);
-    dW[o] = dWe[o] * is - k * u[r] * v[c];
+    const float g = dWe[o] * is - k * u[r] * v[c];
+    dW[o] = accum ? dW[o] + g : g;
   }
 }
 
 extern "C" int rgan_spectral_backward(const float* W, const float* dWeff, int rows, int cols, long long rs,
                                       long long hs, int lo, const float* u, const float* v,
-                                      const float* inv_sigma, float* dW, void* ws, void* stream) {
+                                      const float* inv_sigma, float* dW, int accumulate, void* ws, void* stream) {
   RGAN_REQUIRE(W && dWeff && u && v && inv_sigma && dW && ws && rows > 0 && cols > 0 && lo > 0);
   hipStream_t s = (hipStream_t)stream;
   SnView w{W, rows, cols, lo, rs, hs};
@@ -437,7 +439,7 @@ extern "C" int rgan_spectral_backward(const float* W, const float* dWeff, int ro
   float* part = (float*)ws;
   sn_dot_kernel<<<nparts, 256, 0, s>>>(w, dWeff, part);
   RGAN_CHECK_LAUNCH();
-  sn_bwd_kernel<<<grid1(total), 256, 0, s>>>(w, dWeff, part, nparts, u, v, inv_sigma, dW);
+  sn_bwd_kernel<<<grid1(total), 256, 0, s>>>(w, dWeff, part, nparts, u, v, inv_sigma, dW, accumulate);
   RGAN_CHECK_LAUNCH();
   return 0;
 }

@@ -55,11 +55,12 @@ __global__ void patch_weight_kernel(const float* __restrict__ Wt, int O, int C, 
 
 // dW[o][c][t] = G1[o * so + (t * 4 + c) * sn]  (c < C): back to torch weight layout
 __global__ void unpatch_grad_kernel(const float* __restrict__ G1, int O, int C, long long so, long long sn,
-                                    float* __restrict__ dW) {
+                                    float* __restrict__ dW, int accum) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= O * C * 16) return;
   const int t = e & 15, oc = e >> 4, c = oc % C, o = oc / C;
-  dW[e] = G1[(long long)o * so + (long long)(t * 4 + c) * sn];
+  const float v = G1[(long long)o * so + (long long)(t * 4 + c) * sn];
+  dW[e] = accum ? dW[e] + v : v;
 }
 
 }  // namespace rgan
@@ -88,10 +89,10 @@ extern "C" int rgan_patch_weight(const float* w, int rows, int channels, long lo
 }
 
 extern "C" int rgan_unpatch_grad(const float* g1, int rows, int channels, long long row_stride,
-                                 long long col_stride, float* dw, void* stream) {
+                                 long long col_stride, float* dw, int accumulate, void* stream) {
   RGAN_REQUIRE(g1 && dw && rows > 0 && channels > 0 && channels <= 4);
   unpatch_grad_kernel<<<ceil_div((long long)rows * channels * 16, 256), 256, 0, (hipStream_t)stream>>>(
-      g1, rows, channels, row_stride, col_stride, dw);
+      g1, rows, channels, row_stride, col_stride, dw, accumulate);
   RGAN_CHECK_LAUNCH();
   return 0;
 }

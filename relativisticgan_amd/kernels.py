@@ -43,6 +43,10 @@ class ConvGeom:
 NN_T = ConvGeom(4, 2, 1, True)
 
 
+# activations with a nonzero second derivative (the WGAN-GP double backward needs act'')
+ACT_HAS_GRAD2 = {"none": False, "relu": False, "lrelu": False, "tanh": True, "sigmoid": True, "selu": True}
+
+
 def _nn_check(geom):
     if geom.upsample != 2 or geom.transposed or (geom.k, geom.stride, geom.pad) != (3, 1, 1):
         raise L.RganError(f"unsupported upsampling conv {geom}: only Upsample(x2)+Conv2d(k3,s1,p1) (--NN_conv)")
@@ -188,10 +192,12 @@ def patch_weight(w, transposed):
 PATCHW = _FoldCache(patch_weight)
 
 
-def unpatch_grad(g1, O, C, row_stride, col_stride):
-    """1x1-GEMM weight gradient -> torch layout [O][C][4][4] (dw[o][c][t] = g1[o*rs + (4t+c)*cs])."""
-    dw = torch.empty((O, C, 4, 4), dtype=torch.float32, device=g1.device)
-    L.check(L.lib().rgan_unpatch_grad(L.ptr(g1), O, C, row_stride, col_stride, L.ptr(dw), L.stream()),
+def unpatch_grad(g1, O, C, row_stride, col_stride, out=None):
+    """1x1-GEMM weight gradient -> torch layout [O][C][4][4] (dw[o][c][t] = g1[o*rs + (4t+c)*cs]);
+    ``out`` given: added into it (gradient accumulation)."""
+    acc = out is not None
+    dw = out if acc else torch.empty((O, C, 4, 4), dtype=torch.float32, device=g1.device)
+    L.check(L.lib().rgan_unpatch_grad(L.ptr(g1), O, C, row_stride, col_stride, L.ptr(dw), int(acc), L.stream()),
             "rgan_unpatch_grad")
     return dw
 
@@ -330,19 +336,27 @@ def conv_dgrad(dy, w, geom, x_shape, wscale=None, out=None, like=None, cache=Fal
     return out
 
 
-def conv_wgrad(x, dy, geom, w_shape, with_bias=False):
-    """(dw in torch layout, dbias or None)."""
+def conv_wgrad(x, dy, geom, w_shape, with_bias=False, out=None, out_bias=None):
+    """(dw in torch layout, dbias or None).  ``out`` / ``out_bias`` given: the gradients are
+    ADDED into them in the GEMM epilogue (autograd accumulation without an add pass)."""
     L.require_cuda(x, dy)
     _f32(x, dy)
     if geom.upsample != 1:
         _nn_check(geom)
+        if out is not None:
+            raise L.RganError("accumulating NN_conv weight gradients is not supported")
         cout, cin = w_shape[0], w_shape[1]
         dwt, db = conv_wgrad(x, dy, NN_T, (cin, cout, 4, 4), with_bias=with_bias)
         return nn_unfold_grad(dwt, tuple(w_shape)), db
-    dw = torch.empty(w_shape, dtype=torch.float32, device=x.device)
+    acc = out is not None
+    if acc and (tuple(out.shape) != tuple(w_shape) or not out.is_contiguous()):
+        raise L.RganError("conv_wgrad: out must be a contiguous tensor of the weight's shape")
+    dw = out if acc else torch.empty(w_shape, dtype=torch.float32, device=x.device)
     db = None
     if with_bias:
-        db = torch.empty(dy.shape[1], dtype=torch.float32, device=x.device)
+        if acc != (out_bias is not None):
+            raise L.RganError("conv_wgrad: accumulate weight and bias gradients together")
+        db = out_bias if acc else torch.empty(dy.shape[1], dtype=torch.float32, device=x.device)
         if not is_nhwc(dy):
             dy = dy.contiguous(memory_format=torch.channels_last)
     d = _desc(x.shape, x.stride(), dy.shape, dy.stride(), geom)
@@ -351,7 +365,7 @@ def conv_wgrad(x, dy, geom, w_shape, with_bias=False):
     if nbytes == 0:
         raise L.RganError(f"unsupported conv wgrad {geom} for {tuple(x.shape)}")
     ws = L.workspace(nbytes, x.device)
-    L.check(lib.rgan_conv_wgrad(ctypes.byref(d), L.ptr(x), L.ptr(dy), L.ptr(dw), L.ptr(db), L.ptr(ws),
+    L.check(lib.rgan_conv_wgrad(ctypes.byref(d), L.ptr(x), L.ptr(dy), L.ptr(dw), L.ptr(db), int(acc), L.ptr(ws),
                                 ws.numel(), L.stream()), "rgan_conv_wgrad")
     return dw, db
 
@@ -454,6 +468,86 @@ def bn_backward(da, y, stats, gamma, beta, act="none", alpha=0.0, need_affine=Tr
     return dy, dgamma, dbeta
 
 
+def bn_backward_apply_ex(da, y, stats, gamma, beta, act, alpha, sums, P_global, add=None, out=None,
+                         dgamma=None, dbeta=None, accumulate_affine=False):
+    """dy = BN-backward(da * act') + add; dgamma/dbeta (given buffers) written or, with
+    accumulate_affine, added into."""
+    if not is_nhwc(da):
+        da = da.contiguous(memory_format=torch.channels_last)
+    P, C, sp, sc = _pc(y)
+    _, _, dsp, dsc = _pc(da)
+    dy = torch.empty_like(y) if out is None else out
+    if dy.stride() != y.stride() or (add is not None and add.stride() != y.stride()):
+        raise L.RganError("bn_backward_apply_ex: out / add must have y's strides")
+    L.check(L.lib().rgan_bn_backward_apply_ex(L.ptr(da), dsp, dsc, L.ptr(y), P, C, sp, sc, L.ptr(stats),
+                                              L.ptr(gamma), L.ptr(beta), L.ACT[act], float(alpha), L.ptr(sums),
+                                              int(P_global), L.ptr(add), L.ptr(dy), sp, sc, L.ptr(dgamma),
+                                              L.ptr(dbeta), int(bool(accumulate_affine)), L.stream()),
+            "rgan_bn_backward_apply_ex")
+    return dy
+
+
+def bn_dd_sums(a, y, dh, stats, gamma, beta, act, alpha, stage, stage1=None, P_global=0):
+    """WGAN-GP double backward through BN+act: stage 1 -> double[3C], stage 2 -> double[2C]."""
+    P, C, sp, sc = _pc(y)
+    for t in (a, dh):
+        if t.stride() != y.stride():
+            raise L.RganError("bn_dd_sums: a, dh must have y's strides")
+    lib = L.lib()
+    out = torch.empty((3 if stage == 1 else 2) * C, dtype=torch.float64, device=y.device)
+    part = L.workspace(lib.rgan_bn_dd_partial_bytes(P, C), y.device)
+    L.check(lib.rgan_bn_dd_sums(L.ptr(a), L.ptr(y), L.ptr(dh), P, C, sp, sc, L.ptr(stats), L.ptr(gamma),
+                                L.ptr(beta), L.ACT[act], float(alpha), int(stage), L.ptr(stage1), int(P_global),
+                                L.ptr(out), L.ptr(part), L.stream()), "rgan_bn_dd_sums")
+    return out
+
+
+def bn_dd_apply(a, y, dh, stats, gamma, beta, act, alpha, first_sums, s1, s2, P_global, s1_local=None,
+                s2_local=None, adj_dh=None, ydir=None, need_adj=True, dgamma2=None, dbeta2=None,
+                accumulate_affine=False):
+    """-> (adj_dh or None, ydir); dgamma2 / dbeta2 buffers written (or added into)."""
+    P, C, sp, sc = _pc(y)
+    if adj_dh is None and need_adj:
+        adj_dh = torch.empty_like(y)
+    if ydir is None:
+        ydir = torch.empty_like(y)
+    for t in (a, dh, ydir) + ((adj_dh,) if adj_dh is not None else ()):
+        if t.stride() != y.stride():
+            raise L.RganError("bn_dd_apply: tensors must share y's strides")
+    L.check(L.lib().rgan_bn_dd_apply(L.ptr(a), L.ptr(y), L.ptr(dh), P, C, sp, sc, L.ptr(stats), L.ptr(gamma),
+                                     L.ptr(beta), L.ACT[act], float(alpha), L.ptr(first_sums), L.ptr(s1),
+                                     L.ptr(s2), L.ptr(s1_local), L.ptr(s2_local), int(P_global),
+                                     L.ptr(adj_dh if need_adj else None), L.ptr(ydir), L.ptr(dgamma2),
+                                     L.ptr(dbeta2), int(bool(accumulate_affine)), L.stream()), "rgan_bn_dd_apply")
+    return (adj_dh if need_adj else None), ydir
+
+
+def act_dd(a, act_out, dh, act, alpha, need_adj=True, need_ydir=False, adj_dh=None, ydir=None):
+    """No-BN layer: (adj_dh = a act'(y) or None, ydir = a dh act''(y) or None)."""
+    for t in (a, dh, adj_dh, ydir):
+        if t is not None and t.stride() != act_out.stride():
+            raise L.RganError("act_dd: a, act_out, dh and the outputs must share strides")
+    if need_adj and adj_dh is None:
+        adj_dh = torch.empty_like(act_out)
+    if need_ydir and ydir is None:
+        ydir = torch.empty_like(act_out)
+    if not need_ydir:
+        ydir = None
+    L.check(L.lib().rgan_act_dd(L.ptr(a), L.ptr(act_out), L.ptr(dh), act_out.numel(), L.ACT[act], float(alpha),
+                                L.ptr(adj_dh if need_adj else None), L.ptr(ydir), L.stream()), "rgan_act_dd")
+    return (adj_dh if need_adj else None), ydir
+
+
+def act_backward_ex(da, a, act, alpha=0.0, add=None, out=None):
+    """dx = da * act'(a) + add."""
+    if da.stride() != a.stride() or (add is not None and add.stride() != a.stride()):
+        raise L.RganError("act_backward_ex: da, a, add must share strides")
+    dx = torch.empty_like(a) if out is None else out
+    L.check(L.lib().rgan_act_backward_ex(L.ptr(da), L.ptr(a), L.ptr(add), a.numel(), L.ACT[act], float(alpha),
+                                         L.ptr(dx), L.stream()), "rgan_act_backward_ex")
+    return dx
+
+
 def act_backward(da, a, act, alpha=0.0):
     """dx = da * act'(x) from the activation output a (same strides required)."""
     if da.stride() != a.stride():
@@ -462,6 +556,18 @@ def act_backward(da, a, act, alpha=0.0):
     L.check(L.lib().rgan_act_backward(L.ptr(da), L.ptr(a), a.numel(), L.ACT[act], float(alpha), L.ptr(dx),
                                       L.stream()), "rgan_act_backward")
     return dx
+
+
+def channel_sum(t, out, accumulate=False):
+    """out[c] (+)= sum over (b, h, w) of t[:, c] (bias gradients), NHWC or [B, C, 1, 1]."""
+    B, C, H, W = t.shape
+    if is_nhwc(t):
+        sp, sc = (t.stride()[0] if H * W == 1 else C), 1
+    else:
+        raise L.RganError("channel_sum expects NHWC (channels_last) input")
+    L.check(L.lib().rgan_channel_sum(L.ptr(t), B * H * W, C, sp, sc, L.ptr(out), int(bool(accumulate)),
+                                     L.stream()), "rgan_channel_sum")
+    return out
 
 
 # ------------------------------------------------------------------ loss heads / GP
@@ -495,11 +601,14 @@ def scale(t, s):
     return out
 
 
-def gp_interp(x, xf, u):
+def gp_interp(x, xf, u, out=None):
     B = x.shape[0]
     x = x.contiguous()
     xf = xf.contiguous()
-    out = torch.empty_like(x)
+    if out is None:
+        out = torch.empty_like(x)
+    elif not out.is_contiguous() or out.shape != x.shape:
+        raise L.RganError("gp_interp: out must be contiguous and shaped like x")
     L.check(L.lib().rgan_gp_interp(L.ptr(x), L.ptr(xf), L.ptr(u.contiguous()), B, x[0].numel(), L.ptr(out),
                                    L.stream()), "rgan_gp_interp")
     return out
@@ -515,9 +624,13 @@ def gp_penalty(g, lam, n_global):
     return loss, norms, g
 
 
-def gp_penalty_backward(g, norms, lam, n_global, gscale):
+def gp_penalty_backward(g, norms, lam, n_global, gscale, out=None):
     B = g.shape[0]
-    dg = torch.empty_like(g)
+    if not g.is_contiguous():
+        raise L.RganError("gp_penalty_backward: g must be contiguous")
+    dg = torch.empty_like(g) if out is None else out
+    if not dg.is_contiguous() or dg.shape != g.shape:
+        raise L.RganError("gp_penalty_backward: out must be contiguous and shaped like g")
     L.check(L.lib().rgan_gp_penalty_backward(L.ptr(g), L.ptr(norms), B, g[0].numel(), float(lam), int(n_global),
                                              L.ptr(gscale), L.ptr(dg), L.stream()), "rgan_gp_penalty_backward")
     return dg
@@ -546,12 +659,14 @@ def spectral_power(w, u, v, transposed, eps=1e-12, do_iter=True):
     return inv_sigma
 
 
-def spectral_backward(w, dw_eff, u, v, inv_sigma, transposed):
+def spectral_backward(w, dw_eff, u, v, inv_sigma, transposed, out=None):
+    """dW_orig of W_eff = W / sigma(W) (u, v constant); ``out`` given: added into it."""
     rows, cols, rs, hs, lo = sn_view(w, transposed)
-    dw = torch.empty_like(w)
+    acc = out is not None
+    dw = out if acc else torch.empty_like(w)
     ws = L.workspace(4096, w.device)
     L.check(L.lib().rgan_spectral_backward(L.ptr(w), L.ptr(dw_eff), rows, cols, rs, hs, lo, L.ptr(u), L.ptr(v),
-                                           L.ptr(inv_sigma), L.ptr(dw), L.ptr(ws), L.stream()),
+                                           L.ptr(inv_sigma), L.ptr(dw), int(acc), L.ptr(ws), L.stream()),
             "rgan_spectral_backward")
     return dw
 

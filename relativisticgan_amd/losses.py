@@ -98,8 +98,18 @@ class _GPPenalty(torch.autograd.Function):
 def gradient_penalty(D, x, x_fake, u, penalty):
     """penalty * mean((||dD(x_hat)/dx_hat||_2 - 1)^2), x_hat = x*u + x_fake*(1-u) (GLI:648-657).
 
-    The double backward runs through the create-graph path of ConvLayerFn (conv
-    dgrad/wgrad GEMMs differentiated on the MFMA kernels)."""
+    Native engine (gp.py): forward, create-graph backward and double backward as explicit
+    kernel sweeps.  Under SyncBN the double backward runs through the create-graph path of
+    ConvLayerFn (conv dgrad/wgrad GEMMs differentiated on the MFMA kernels, BN algebra as
+    autograd tensor ops)."""
+    from . import gp as _gp
+    if _gp.supported(D):
+        return _gp.gradient_penalty(D, x, x_fake, u, penalty)
+    return gradient_penalty_composite(D, x, x_fake, u, penalty)
+
+
+def gradient_penalty_composite(D, x, x_fake, u, penalty):
+    """The autograd form of the penalty (create_graph through ConvLayerFn)."""
     x_both = K.gp_interp(x.detach(), x_fake.detach(), u.detach()).requires_grad_(True)
     out = D(x_both)
     grad = torch.autograd.grad(outputs=out, inputs=x_both, grad_outputs=torch.ones_like(out),

@@ -363,7 +363,14 @@ def test_batchnorm_train(K, shape, act):
     out.backward(da.double().cpu())
     dy, dg, db = K.bn_backward(da, y, stats, gamma, beta, act, 0.2)
     tol = 1e-4 if n == 1 else 2e-5
-    assert _rel(dy, y64.grad) < tol
+    keep = torch.ones_like(y64, dtype=torch.bool)
+    if act in ("relu", "lrelu"):
+        # act' jumps at 0: elements whose pre-activation is within fp32 rounding of 0 may
+        # take the other branch (a flip moves that element by (1-alpha)*da*gamma*invstd)
+        zn = (y64.detach() - mean[None, :, None, None]) / torch.sqrt(var + 1e-5)[None, :, None, None]
+        zn = zn * gamma.double().cpu()[None, :, None, None] + beta.double().cpu()[None, :, None, None]
+        keep = zn.abs() > 1e-5
+    assert _rel(dy.cpu()[keep], y64.grad[keep]) < tol
     assert _rel(dg, g64.grad) < 2e-5
     assert _rel(db, b64.grad) < 2e-5
 

@@ -2,7 +2,8 @@
 
 For every fixture config the oracle (CPU, fp32) replays the reference loop and exposes,
 per iteration, the pre-step state, the drawn inputs and the results.  The GPU trainer is
-teacher-forced from the same pre-step state and inputs.  Each compared tensor T must
+teacher-forced from the same pre-step state and inputs, and again between its D step and
+its G step (the G step starts from the oracle's post-D-step D, as does the fp64 run).  Each compared tensor T must
 satisfy (tolerances stated here):
 
   direct:    rel_L2(T_gpu, T_oracle32) <= TOL[kind]                      OR
@@ -105,8 +106,11 @@ def oracle_exact_step(name, st):
     """The same teacher-forced step in float64 (the 'exact' reference for the envelope)."""
     from oracle.reference_cpu import Trainer
     cur, holder = {}, {}
-    t = Trainer(param_for(name), dataset_for(name), hooks=lambda tag, r: _cap(cur, holder["t"], tag, r),
-                dtype=torch.float64)
+    def hook(tag, r):
+        _cap(cur, holder["t"], tag, r)
+        if tag == "D.post":  # the G step starts from the oracle's post-D-step D (see gpu_step)
+            holder["t"].D.load_state_dict(st["postD"])
+    t = Trainer(param_for(name), dataset_for(name), hooks=hook, dtype=torch.float64)
     holder["t"] = t
     t.G.load_state_dict(st["pre"]["G"])
     t.D.load_state_dict(st["pre"]["D"])
@@ -142,6 +146,12 @@ def gpu_step(t, st):
             if tag == "D":  # everything traced so far belongs to the D step
                 split["D"] = len(autograd.ACT_TRACE)
             _cap(got, t, tag, r)
+            if tag == "D.post":
+                # teacher-force the G step too: it starts from the oracle's post-D-step D.
+                # Adam's first steps are sign steps, so D after a fp32 step differs from
+                # fp64 by +-lr on near-zero-gradient elements; the G step would otherwise
+                # inherit that (and every activation flip it causes in D(fake)).
+                t.D.load_state_dict(st["postD"])
         t.iteration(st["i"], feed={k: v.to(DEV) for k, v in _feed(st).items()}, hooks=hook)
         masks = list(zip(autograd.ACT_TAGS, autograd.ACT_TRACE))
         got["trace_info"] = [(tag, li, "D" if k < split["D"] else "G")
