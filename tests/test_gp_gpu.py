@@ -63,7 +63,8 @@ def test_native_gp_matches_composite(case):
     names = [n for n, _ in D.named_parameters()]
     for n, a, b, g0 in zip(names, g_n, g_c, grads0):
         # compare the GP's own contribution (the accumulated base cancels exactly)
-        assert _rel(a - g0, b - g0) < 2e-5 or (b - g0).abs().max() < 1e-9, (case, n, _rel(a - g0, b - g0))
+        # (a conv bias feeding BatchNorm has an exact GP gradient of 0: both are roundoff)
+        assert _rel(a - g0, b - g0) < 2e-5 or (a - b).abs().max() < 1e-7, (case, n, _rel(a - g0, b - g0))
     for k in st_c:  # BN running stats and spectral u/v move exactly as in one D(x_hat) call
         if st_c[k].is_floating_point():
             assert _rel(st_n[k], st_c[k]) < 1e-6, (case, k)
