@@ -16,22 +16,22 @@ stop() { case $1 in 124|134|137|139) echo "STOP: rc=$1 at $2"; exit "$1" ;; esac
 for s in $steps; do
   w=${s#*=}; [ "$w" = "$s" ] && w=""
   sfx=${w:+_$w}
-  wl=${w:+--workload $w --extra ''}
+  wl=${w:+--workload $w --extra=}
   case $s in
     tests)
       RGAN_PARITY_AUDIT=$out/parity timeout -k 10 1100 python -u -m pytest tests -m gpu -v --timeout 300 \
         --timeout-method thread -p no:cacheprovider > "$out/pytest.log" 2>&1
       rc=$?; echo "tests rc=$rc"; tail -3 "$out/pytest.log"; stop $rc tests ;;
     bench*)
-      eval timeout -k 10 500 python -u bench.py $wl > "$out/bench$sfx.json" 2> "$out/bench$sfx.err"
+      timeout -k 10 500 python -u bench.py $wl > "$out/bench$sfx.json" 2> "$out/bench$sfx.err"
       rc=$?; echo "bench$sfx rc=$rc"; stop $rc bench ;;
     prof*)
-      eval timeout -k 10 450 tools/profile_bench.sh "$out/prof$sfx" --steps 10 --warmup 3 --no-cpu-baseline \
-        --extra "''" $wl
+      timeout -k 10 450 tools/profile_bench.sh "$out/prof$sfx" --steps 10 --warmup 3 --no-cpu-baseline \
+        --extra= $wl
       rc=$?; echo "prof$sfx rc=$rc"; head -25 "$out/prof$sfx/summary.txt"; stop $rc prof ;;
     pmc*)
-      eval timeout -k 10 850 tools/pmc_traffic.sh "$out/pmc$sfx" --steps 5 --warmup 2 --no-cpu-baseline \
-        --extra "''" $wl
+      timeout -k 10 850 tools/pmc_traffic.sh "$out/pmc$sfx" --steps 5 --warmup 2 --no-cpu-baseline \
+        --extra= $wl
       rc=$?; echo "pmc$sfx rc=$rc"; stop $rc pmc ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
