@@ -46,7 +46,8 @@ typedef struct RganConv {
   long long ys[4];         /* y strides (b, c, h, w) in elements */
 } RganConv;
 
-/* Workspace bytes needed by rgan_conv_{fwd,dgrad,wgrad}; `which` = 0 fwd, 1 dgrad, 2 wgrad;
+/* Workspace bytes needed by rgan_conv_{fwd,dgrad,wgrad}; `which` = 0 fwd, 1 dgrad, 2 wgrad
+ * (wgrad's includes the bias-gradient reduction scratch);
  * `prepacked` != 0: the caller passes packed weights (no packing scratch).  0 = unsupported. */
 size_t rgan_conv_workspace(const RganConv* d, int which, int prepacked);
 
@@ -234,9 +235,10 @@ int rgan_act_backward(const float* da, const float* a, long long n, int act, flo
 int rgan_act_backward_ex(const float* da, const float* a, const float* add, long long n, int act,
                          float act_alpha, float* dx, void* stream);
 /* out[n] (+)= sum over pixels of t (per channel; bias gradient), strided like bn;
- * accumulate != 0 adds into out (gradient accumulation, no separate add pass). */
+ * accumulate != 0 adds into out (gradient accumulation, no separate add pass).
+ * partial: rgan_bn_partial_bytes(P, C) of scratch (fixed-order two-level sum). */
 int rgan_channel_sum(const float* t, long long P, int C, long long sp, long long sc,
-                     float* out, int accumulate, void* stream);
+                     float* out, int accumulate, void* partial, void* stream);
 
 /* ---- loss heads (GLI:481-484, 592-644, 686-709) ----
  * kind = --loss_D (1..8); side 0 = D-real (heads 1-4) / D (heads 5-8), 1 = D-fake
@@ -244,6 +246,10 @@ int rgan_channel_sum(const float* t, long long P, int C, long long sp, long long
  * dr, df: [n] gradients of loss w.r.t. r and f (nullable).  n <= 65536. */
 int rgan_loss_head(int kind, int side, const float* r, const float* f, int n,
                    float* loss, float* dr, float* df, void* stream);
+/* Heads 1-4, D side as ONE launch: loss3 = {errD_real, errD_fake, errD_real + errD_fake}
+ * and both gradients (nullable) -- the batched D step's pair of losses. */
+int rgan_loss_head_pair(int kind, const float* r, const float* f, int n, float* loss3, float* dr,
+                        float* df, void* stream);
 /* Distributed form: the three phases of the same head with the cross-rank sums done by
  * the caller between them.  phase 0: sums[0..1] = (sum r, sum f) local;
  * phase 1: given global means in gsum[0..1] (sum r, sum f over n_global), sums[0..3] =

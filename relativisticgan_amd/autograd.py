@@ -161,17 +161,17 @@ class _AllReduceSum(torch.autograd.Function):
 
 
 # ---------------------------------------------------------------- fused layer
-def _train_stats(y, spec, rm, rv, nbt, seg=None):
+def _train_stats(y, spec, rm, rv, nbt, seg=None, out=None):
     """Batch statistics of y; ``seg`` = (part, s0, s1): the conv epilogue's segment moments
     covering y (rgan_conv_fwd_bn) replace the separate moments pass over y."""
     C = y.shape[1]
     if dp.sync_bn():
         mom = K.bn_segment_moments(seg[0], seg[1], seg[2], C) if seg is not None else K.bn_moments(y)
         mom = dp.all_gather_cat(mom)
-        return K.bn_finalize(mom, dp.world(), C, spec.eps, spec.momentum, rm, rv, nbt)
+        return K.bn_finalize(mom, dp.world(), C, spec.eps, spec.momentum, rm, rv, nbt, out=out)
     if seg is not None:
-        return K.bn_segment_stats(seg[0], seg[1], seg[2], C, spec.eps, spec.momentum, rm, rv, nbt)
-    return K.bn_stats(y, spec.eps, spec.momentum, rm, rv, nbt)
+        return K.bn_segment_stats(seg[0], seg[1], seg[2], C, spec.eps, spec.momentum, rm, rv, nbt, out=out)
+    return K.bn_stats(y, spec.eps, spec.momentum, rm, rv, nbt, out=out)
 
 
 class ConvLayerFn(torch.autograd.Function):
@@ -184,7 +184,7 @@ class ConvLayerFn(torch.autograd.Function):
     calls in a single K-doubled GEMM instead of two GEMMs and a gradient add)."""
 
     @staticmethod
-    def forward(ctx, x, w, bias, gamma, beta, spec, bufs, sn, segs=1):
+    def forward(ctx, x, w, bias, gamma, beta, spec, bufs, sn, segs=1, out=None):
         # bufs = (running_mean, running_var, num_batches_tracked, training)
         # sn   = (u, v, inv_sigma) clones for spectral layers, else None
         wscale = sn[2] if spec.spectral else None
@@ -198,25 +198,24 @@ class ConvLayerFn(torch.autograd.Function):
             C = y.shape[1]
             if training and segs > 1:
                 Bs = y.shape[0] // segs
-                a = torch.empty_like(y)
-                st = []
+                a = torch.empty_like(y) if out is None else out
+                stats = torch.empty((segs, 2 * C), dtype=torch.float32, device=y.device)
                 for s_ in range(segs):
                     sl = slice(s_ * Bs, (s_ + 1) * Bs)
                     seg = (part, s_ * S // segs, (s_ + 1) * S // segs) if part is not None else None
-                    st.append(_train_stats(y[sl], spec, rm, rv, nbt, seg))
-                    K.bn_apply(y[sl], st[-1], gamma, beta, spec.act, spec.alpha, out=a[sl])
-                stats = torch.stack(st)
+                    _train_stats(y[sl], spec, rm, rv, nbt, seg, out=stats[s_])
+                    K.bn_apply(y[sl], stats[s_], gamma, beta, spec.act, spec.alpha, out=a[sl])
             else:
                 if training:
                     stats = _train_stats(y, spec, rm, rv, nbt, (part, 0, S) if part is not None else None)
                 else:
                     stats = torch.cat([rm, torch.rsqrt(rv + spec.eps)])
                     stats_eval = (rm, stats[C:])
-                a = K.bn_apply(y, stats, gamma, beta, spec.act, spec.alpha)
+                a = K.bn_apply(y, stats, gamma, beta, spec.act, spec.alpha, out=out)
             ctx.save_for_backward(x, w, bias, gamma, beta, y, stats, *(sn if spec.spectral else ()))
         else:
             a = K.conv_fwd(x, w, spec.geom, bias=bias, act=spec.act, alpha=spec.alpha, wscale=wscale,
-                           nchw_out=spec.nchw_out, cache=True)
+                           nchw_out=spec.nchw_out, cache=True, out=out)
             ctx.save_for_backward(x, w, bias, gamma, beta, a, None, *(sn if spec.spectral else ()))
         if ACT_TRACE is not None and spec.act in _KINKED:
             ACT_TRACE.append((a.detach() > 0).cpu())
@@ -297,7 +296,7 @@ class ConvLayerFn(torch.autograd.Function):
                 dw = K.spectral_backward(w, dw, u, v, inv_sigma, spec.geom.transposed)
             if not nw:
                 dw = None
-        return dx, dw, db, dgamma, dbeta, None, None, None, None
+        return dx, dw, db, dgamma, dbeta, None, None, None, None, None
 
     @staticmethod
     def _patch_conv(spec, x):
@@ -349,7 +348,7 @@ class ConvLayerFn(torch.autograd.Function):
         spec = ctx.spec
         slots = [i for i, t in enumerate((x, w, bias, gamma, beta))
                  if t is not None and ctx.needs_input_grad[i]]
-        out = [None] * 9
+        out = [None] * 10
         if not slots:
             return tuple(out)
         src = (x, w, bias, gamma, beta)

@@ -950,28 +950,81 @@ extern "C" int rgan_act_backward_ex(const float* da, const float* a, const float
   return 0;
 }
 
-// per-channel sum over pixels (bias gradients); one block per 64 channels, fixed order, double
-__global__ __launch_bounds__(256) void channel_sum_kernel(const float* __restrict__ t, long long P, int C,
-                                                          long long sp, long long sc, float* __restrict__ out,
-                                                          int accum) {
-  __shared__ double sh[4][64];
-  const int lane = threadIdx.x & 63, row = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
-  double s = 0.0;
-  if (c < C)
-    for (long long p = row; p < P; p += 4) s += t[p * sp + c * sc];
-  sh[row][lane] = s;
+// per-channel sum over pixels (bias gradients, GLI:202-223 / 260-302 arch-1 convs with bias):
+// the BN grid (pixel chunks x channel groups, double partials [chunk][C]) and a fixed-order
+// merge that writes (or adds into) the float result -- deterministic, and parallel over
+// pixels (one block per 64 channels walking every pixel took 0.75 ms at 32x64x32x32).
+template <int Q>
+__global__ __launch_bounds__(256) void chsum_partial(const float* __restrict__ t, long long P, int C, long long sp,
+                                                     long long sc, int tpr, long long rows,
+                                                     double* __restrict__ part) {
+  __shared__ double sh[256][Q];
+  const int tid = threadIdx.x, lc = tid % tpr, rl = tid / tpr, rp = blockDim.x / tpr;
+  const int c0 = (blockIdx.y * tpr + lc) * Q;
+  const long long p0 = blockIdx.x * rows, p1 = min(P, p0 + rows);
+  double s[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) s[q] = 0.0;
+  if (c0 < C) {
+    long long p = p0 + rl;
+    for (; p + (BN_UNR - 1) * rp < p1; p += BN_UNR * rp) {
+      float v[BN_UNR][Q];
+#pragma unroll
+      for (int u = 0; u < BN_UNR; ++u) load_q<Q>(t, (p + u * rp) * sp + (long long)c0 * sc, v[u]);
+#pragma unroll
+      for (int u = 0; u < BN_UNR; ++u)
+#pragma unroll
+        for (int q = 0; q < Q; ++q) s[q] += (double)v[u][q];
+    }
+    for (; p < p1; p += rp) {
+      float v[Q];
+      load_q<Q>(t, p * sp + (long long)c0 * sc, v);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) s[q] += (double)v[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) sh[tid][q] = s[q];
   __syncthreads();
-  if (row == 0 && c < C) {
-    const float v = (float)(sh[0][lane] + sh[1][lane] + sh[2][lane] + sh[3][lane]);
-    out[c] = accum ? out[c] + v : v;
+  if (rl == 0 && c0 < C) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      if (c0 + q >= C) continue;
+      double a = 0.0;
+      for (int r = 0; r < rp; ++r) a += sh[r * tpr + lc][q];
+      part[(size_t)blockIdx.x * C + c0 + q] = a;
+    }
   }
 }
 
+__global__ __launch_bounds__(1024) void chsum_merge(const double* __restrict__ part, int chunks, int C,
+                                                    float* __restrict__ out, int accum) {
+  __shared__ double sh[MERGE_ROWS][MERGE_CPB];
+  const int cl = threadIdx.x % MERGE_CPB, r = threadIdx.x / MERGE_CPB;
+  const int c = blockIdx.x * MERGE_CPB + cl;
+  double a = 0.0;
+  if (c < C)
+    for (int j = r; j < chunks; j += MERGE_ROWS) a += part[(size_t)j * C + c];
+  sh[r][cl] = a;
+  __syncthreads();
+  if (r != 0 || c >= C) return;
+  double t = 0.0;
+  for (int q = 0; q < MERGE_ROWS; ++q) t += sh[q][cl];
+  out[c] = accum ? out[c] + (float)t : (float)t;
+}
+
 extern "C" int rgan_channel_sum(const float* t, long long P, int C, long long sp, long long sc, float* out,
-                                int accumulate, void* stream) {
-  RGAN_REQUIRE(t && out && P > 0 && C > 0);
-  channel_sum_kernel<<<ceil_div(C, 64), 256, 0, (hipStream_t)stream>>>(t, P, C, sp, sc, out, accumulate);
+                                int accumulate, void* partial, void* stream) {
+  RGAN_REQUIRE(t && out && partial && P > 0 && C > 0);
+  hipStream_t s = (hipStream_t)stream;
+  BnGeo g = bn_geo(P, C, sp, sc);
+  if (g.vec && ((uintptr_t)t & 15)) g = bn_geo(P, C, 1, 2);
+  double* part = (double*)partial;
+  const dim3 grid(g.chunks, g.cgroups);
+  if (g.vec) chsum_partial<4><<<grid, 256, 0, s>>>(t, P, C, sp, sc, g.tpr, g.rows, part);
+  else chsum_partial<1><<<grid, 256, 0, s>>>(t, P, C, sp, sc, g.tpr, g.rows, part);
+  RGAN_CHECK_LAUNCH();
+  chsum_merge<<<ceil_div(C, MERGE_CPB), 1024, 0, s>>>(part, g.chunks, C, out, accumulate);
   RGAN_CHECK_LAUNCH();
   return 0;
 }

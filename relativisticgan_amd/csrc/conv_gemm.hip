@@ -2210,7 +2210,10 @@ extern "C" size_t rgan_conv_workspace(const RganConv* d, int which, int prepacke
   else rc = plan_wgrad(d, dummy, dummy, (float*)dummy, p);
   if (rc) return 0;
   if (prepacked && which != 2) p.prepacked = dummy;
-  return plan_ws_bytes(p) + 256;  // never 0 for a valid descriptor (0 signals "unsupported")
+  size_t extra = 0;
+  if (which == 2)  // bias-gradient reduction scratch (rgan_channel_sum), after the plan's
+    extra = align_up(rgan_bn_partial_bytes((long long)d->batch * d->hout * d->wout, d->cout), 256);
+  return align_up(plan_ws_bytes(p), 256) + extra + 256;  // never 0 for a valid descriptor
 }
 
 extern "C" size_t rgan_conv_pack_floats(const RganConv* d, int which) {
@@ -2308,6 +2311,7 @@ extern "C" int rgan_conv_wgrad(const RganConv* d, const float* x, const float* d
   if (rc) return rc;
   p.g.accum = accumulate ? 1 : 0;
   p.da.accum = p.g.accum;
+  const size_t plan_bytes = align_up(plan_ws_bytes(p), 256);
   rc = run_plan(p, ws, ws_bytes, (hipStream_t)stream);
   if (rc) return rc;
   if (dbias) {
@@ -2322,7 +2326,9 @@ extern "C" int rgan_conv_wgrad(const RganConv* d, const float* x, const float* d
         return RGAN_EINVAL;
       sp = d->cout;
     }
-    return rgan_channel_sum(dy, P, d->cout, sp, d->ys[1], dbias, accumulate, stream);
+    const size_t need = plan_bytes + rgan_bn_partial_bytes(P, d->cout);
+    if (!ws || ws_bytes < need) return RGAN_EINVAL;
+    return rgan_channel_sum(dy, P, d->cout, sp, d->ys[1], dbias, accumulate, (char*)ws + plan_bytes, stream);
   }
   return 0;
 }

@@ -163,6 +163,41 @@ __global__ __launch_bounds__(1024) void loss_head_kernel(int kind, int side, int
   }
 }
 
+// heads 1-4, D side: errD_real (on r) and errD_fake (on f) and their sum in one launch --
+// the reference's two losses and two backward calls (GLI:595-624); loss3 = {real, fake, sum}
+__global__ __launch_bounds__(1024) void loss_head_pair_kernel(int kind, const float* __restrict__ r,
+                                                              const float* __restrict__ f, int n,
+                                                              float* __restrict__ loss3, float* __restrict__ dr,
+                                                              float* __restrict__ df) {
+  __shared__ float red[16];
+  const int tid = threadIdx.x;
+  const float ng = (float)n;
+  float sr = 0.f, sf = 0.f;
+  for (int i = tid; i < n; i += blockDim.x) {
+    float der;
+    sr += single_term(kind, 0, r[i], der);
+    if (dr) dr[i] = der / ng;
+    sf += single_term(kind, 1, f[i], der);
+    if (df) df[i] = der / ng;
+  }
+  sr = block_sum(sr, red);
+  sf = block_sum(sf, red);
+  if (tid == 0) {
+    const float lr = sr / ng, lf = sf / ng;
+    loss3[0] = lr;
+    loss3[1] = lf;
+    loss3[2] = lr + lf;
+  }
+}
+
+extern "C" int rgan_loss_head_pair(int kind, const float* r, const float* f, int n, float* loss3, float* dr,
+                                   float* df, void* stream) {
+  RGAN_REQUIRE(kind >= 1 && kind <= 4 && r && f && loss3 && n > 0 && n <= 65536);
+  loss_head_pair_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(kind, r, f, n, loss3, dr, df);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
 static bool head_args_ok(int kind, int side, const float* r, const float* f, int n) {
   if (kind < 1 || kind > 8 || n <= 0 || n > 65536) return false;
   if (kind <= 4) return side >= 0 && side <= 2 && (side == 0 ? r != nullptr : f != nullptr);

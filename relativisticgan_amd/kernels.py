@@ -293,9 +293,9 @@ def conv_fwd_bn(x, w, geom, bias=None, wscale=None, cache=False, segs=1):
 
 
 def bn_segment_stats(part, s0, s1, C, eps, momentum, running_mean=None, running_var=None,
-                     num_batches_tracked=None):
+                     num_batches_tracked=None, out=None):
     """Segment moments [s0, s1) of conv_fwd_bn -> (mean, invstd) float[2C] + running stats."""
-    stats = torch.empty(2 * C, dtype=torch.float32, device=part.device)
+    stats = torch.empty(2 * C, dtype=torch.float32, device=part.device) if out is None else out
     L.check(L.lib().rgan_bn_segment_stats(L.ptr(part), int(s0), int(s1), C, 64, float(eps), float(momentum),
                                           L.ptr(running_mean), L.ptr(running_var), L.ptr(num_batches_tracked),
                                           L.ptr(stats), None, L.stream()), "rgan_bn_segment_stats")
@@ -379,11 +379,11 @@ def _pc(t):
     return B * H * W, C, C, 1
 
 
-def bn_stats(y, eps, momentum, running_mean=None, running_var=None, num_batches_tracked=None):
+def bn_stats(y, eps, momentum, running_mean=None, running_var=None, num_batches_tracked=None, out=None):
     """Batch (mean, invstd) as float[2C]; updates running buffers when given."""
     P, C, sp, sc = _pc(y)
     lib = L.lib()
-    stats = torch.empty(2 * C, dtype=torch.float32, device=y.device)
+    stats = torch.empty(2 * C, dtype=torch.float32, device=y.device) if out is None else out
     part = L.workspace(lib.rgan_bn_partial_bytes(P, C), y.device)
     L.check(lib.rgan_bn_stats(L.ptr(y), P, C, sp, sc, float(eps), float(momentum), L.ptr(running_mean),
                               L.ptr(running_var), L.ptr(num_batches_tracked), L.ptr(stats), L.ptr(part),
@@ -402,9 +402,9 @@ def bn_moments(y):
 
 
 def bn_finalize(moments, nranks, C, eps, momentum, running_mean=None, running_var=None,
-                num_batches_tracked=None):
+                num_batches_tracked=None, out=None):
     """Merge [nranks][3][C] moments in rank order -> stats float[2C] (SyncBN stage 2)."""
-    stats = torch.empty(2 * C, dtype=torch.float32, device=moments.device)
+    stats = torch.empty(2 * C, dtype=torch.float32, device=moments.device) if out is None else out
     L.check(L.lib().rgan_bn_finalize(L.ptr(moments), int(nranks), C, float(eps), float(momentum),
                                      L.ptr(running_mean), L.ptr(running_var), L.ptr(num_batches_tracked),
                                      L.ptr(stats), L.stream()), "rgan_bn_finalize")
@@ -565,8 +565,9 @@ def channel_sum(t, out, accumulate=False):
         sp, sc = (t.stride()[0] if H * W == 1 else C), 1
     else:
         raise L.RganError("channel_sum expects NHWC (channels_last) input")
+    part = L.workspace(L.lib().rgan_bn_partial_bytes(B * H * W, C), t.device)
     L.check(L.lib().rgan_channel_sum(L.ptr(t), B * H * W, C, sp, sc, L.ptr(out), int(bool(accumulate)),
-                                     L.stream()), "rgan_channel_sum")
+                                     L.ptr(part), L.stream()), "rgan_channel_sum")
     return out
 
 
@@ -580,6 +581,16 @@ def loss_head(kind, side, r, f, need_dr=True, need_df=True):
     L.check(L.lib().rgan_loss_head(int(kind), int(side), L.ptr(r), L.ptr(f), n, L.ptr(loss), L.ptr(dr),
                                    L.ptr(df), L.stream()), "rgan_loss_head")
     return loss, dr, df
+
+
+def loss_head_pair(kind, r, f, need_dr=True, need_df=True):
+    """Heads 1-4 D side: (loss3 = [real, fake, sum], dr, df) in one launch."""
+    loss3 = torch.empty(3, dtype=torch.float32, device=r.device)
+    dr = torch.empty_like(r) if need_dr else None
+    df = torch.empty_like(f) if need_df else None
+    L.check(L.lib().rgan_loss_head_pair(int(kind), L.ptr(r), L.ptr(f), r.numel(), L.ptr(loss3), L.ptr(dr),
+                                        L.ptr(df), L.stream()), "rgan_loss_head_pair")
+    return loss3, dr, df
 
 
 def loss_head_dist(kind, side, phase, r, f, n_global, gsum=None, need_dr=True, need_df=True):

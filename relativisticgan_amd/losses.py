@@ -67,6 +67,37 @@ def loss_D_fake(kind, y_pred_fake):
     return _Head.apply(None, _flat(y_pred_fake), kind, 1)
 
 
+class _HeadPair(torch.autograd.Function):
+    """errD_real + errD_fake of heads 1-4 (GLI:595-624) as one kernel launch; returns
+    (errD, errD_real, errD_fake) with errD carrying the graph."""
+
+    @staticmethod
+    def forward(ctx, r, f, kind):
+        loss3, dr, df = K.loss_head_pair(kind, r, f, need_dr=ctx.needs_input_grad[0],
+                                         need_df=ctx.needs_input_grad[1])
+        ctx.save_for_backward(dr, df)
+        ctx.mark_non_differentiable(loss3)
+        return loss3[2], loss3
+
+    @staticmethod
+    def backward(ctx, g, _g3):
+        dr, df = ctx.saved_tensors
+        g = g.contiguous()
+        return (K.scale(dr, g) if dr is not None else None,
+                K.scale(df, g) if df is not None else None, None)
+
+
+def loss_D_pair(kind, y_pred, y_pred_fake):
+    """(errD, errD_real, errD_fake) for heads 1-4: errD.backward() is the reference's
+    errD_real.backward(); errD_fake.backward() (GLI:605, 624) accumulated."""
+    assert 1 <= kind <= 4
+    if dp.active():
+        er, ef = loss_D_real(kind, y_pred), loss_D_fake(kind, y_pred_fake)
+        return er + ef, er.detach(), ef.detach()
+    err, loss3 = _HeadPair.apply(_flat(y_pred), _flat(y_pred_fake), kind)
+    return err, loss3[0], loss3[1]
+
+
 def loss_D(kind, y_pred, y_pred_fake):
     """errD for heads 5-8 (GLI:634-641)."""
     assert 5 <= kind <= 8

@@ -164,7 +164,7 @@ class _Layer:
                                nchw_out=nchw_out) if geom is not None else None)
         self.w_view, self.in_view, self.out_view = w_view, in_view, out_view
 
-    def run(self, h, training, segs=1):
+    def run(self, h, training, segs=1, out=None):
         conv, bn = self.conv, self.bn
         w = conv.w if isinstance(conv, _ConvBase) else conv.weight
         if self.w_view is not None:
@@ -178,11 +178,13 @@ class _Layer:
                                            do_iter=training)
             sn = (conv.weight_u.clone(), conv.weight_v.clone(), inv_sigma)
         bufs = (bn.running_mean, bn.running_var, bn.num_batches_tracked, training) if bn is not None else None
-        out = ConvLayerFn.apply(h, w, conv.bias, bn.weight if bn is not None else None,
-                                bn.bias if bn is not None else None, self.spec, bufs, sn, segs)
+        if out is not None and self.out_view is not None:
+            raise ValueError("an output buffer for a reshaped layer")
+        res = ConvLayerFn.apply(h, w, conv.bias, bn.weight if bn is not None else None,
+                                bn.bias if bn is not None else None, self.spec, bufs, sn, segs, out)
         if self.out_view is not None:
-            out = out.reshape(out.shape[0], *self.out_view)
-        return out
+            res = res.reshape(res.shape[0], *self.out_view)
+        return res
 
 
 def _lin_spec(layer, geom, act, alpha=0.0, nchw_out=False):
@@ -195,12 +197,14 @@ class _Net(nn.Module):
     def _tag(self):
         return type(self).__name__[1]  # "G" / "D": activation-trace tag (parity tests)
 
-    def _run(self, x):
+    def _run(self, x, out=None):
+        """``out``: a buffer for the last layer's output (e.g. half of a batched D input)."""
         AG.TRACE_NET = self._tag
         h = x
+        last = len(self._plan) - 1
         for li, layer in enumerate(self._plan):
             AG.TRACE_LAYER = li
-            h = layer.run(h, self.training)
+            h = layer.run(h, self.training, out=out if li == last else None)
         return h
 
     @property
@@ -209,10 +213,11 @@ class _Net(nn.Module):
         reference runs one power iteration per call, so each call has its own sigma)."""
         return not any(layer.spec is not None and layer.spec.spectral for layer in self._plan)
 
-    def forward_segments(self, xs):
+    def forward_segments(self, xs, cat=None):
         """``[self(x) for x in xs]`` as ONE pass over the concatenated batch: every layer's
         GEMMs run once over all segments, BatchNorm normalises (and updates its running
-        statistics) per segment in list order, exactly as the separate calls would."""
+        statistics) per segment in list order, exactly as the separate calls would.
+        ``cat``: the segments already laid out back to back in one tensor (no copy)."""
         if not self.segmentable:
             raise ValueError("forward_segments: a spectral-norm layer needs one call per forward")
         n = len(xs)
@@ -221,7 +226,7 @@ class _Net(nn.Module):
             raise ValueError("forward_segments: segments must have equal shapes")
         trace0 = len(AG.ACT_TRACE) if AG.ACT_TRACE is not None else 0
         AG.TRACE_NET = self._tag
-        h = torch.cat(xs)
+        h = cat if cat is not None else torch.cat(xs)
         for li, layer in enumerate(self._plan):
             AG.TRACE_LAYER = li
             h = layer.run(h, self.training, n)
@@ -295,8 +300,8 @@ class _G0(_Net):
         self.main = main
         self._plan = plan
 
-    def forward(self, z):
-        return self._run(z)
+    def forward(self, z, out=None):
+        return self._run(z, out)
 
 
 class _D0(_Net):
@@ -355,9 +360,9 @@ class _D0(_Net):
     def forward(self, x):
         return self._run(x).view(-1)
 
-    def forward_pair(self, x, x_fake):
+    def forward_pair(self, x, x_fake, cat=None):
         """(D(x), D(x_fake)) in one batched pass (see ``forward_segments``)."""
-        a, b = self.forward_segments([x, x_fake])
+        a, b = self.forward_segments([x, x_fake], cat)
         return a.reshape(-1), b.reshape(-1)
 
 
@@ -397,8 +402,8 @@ class _G1(_Net):
         self.model = nn.Sequential(*layers)
         self._plan = plan
 
-    def forward(self, z):
-        return self._run(z)
+    def forward(self, z, out=None):
+        return self._run(z, out)
 
 
 class _D1(_Net):
@@ -439,8 +444,8 @@ class _D1(_Net):
     def forward(self, x):
         return self._run(x).view(-1)
 
-    def forward_pair(self, x, x_fake):
-        a, b = self.forward_segments([x, x_fake])
+    def forward_pair(self, x, x_fake, cat=None):
+        a, b = self.forward_segments([x, x_fake], cat)
         return a.reshape(-1), b.reshape(-1)
 
 

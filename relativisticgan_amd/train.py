@@ -20,7 +20,7 @@ import torch
 
 from . import dp
 from .config import TITLES, parse
-from .losses import gradient_penalty, loss_D, loss_D_fake, loss_D_real, loss_G
+from .losses import gradient_penalty, loss_D, loss_D_fake, loss_D_pair, loss_D_real, loss_G
 from .nets import DCGAN_D, DCGAN_G, weights_init
 from .optim import Adam
 
@@ -113,7 +113,7 @@ class Trainer:
         b = t.shape[0] // self.pac
         return torch.cat([t[k * b:(k + 1) * b] for k in range(self.pac)], 1)
 
-    def _real(self, feed, key):
+    def _real(self, feed, key, out=None):
         if feed is not None and key in feed:
             return feed[key]
         from .kernels import gather_images
@@ -123,7 +123,7 @@ class Trainer:
             idx = self._shard_pac(torch.from_numpy(idx.astype(numpy.int64))).to(self.device, non_blocking=True)
         else:
             idx = self._shard_pac(torch.randperm(self.images.shape[0], device=self.device)[:n])
-        return self._pack(gather_images(self.images, idx))
+        return self._pack(gather_images(self.images, idx, out=out if self.pac == 1 else None))
 
     def _normal(self, feed, key, shape):
         if feed is not None and key in feed:
@@ -141,12 +141,13 @@ class Trainer:
             return self._shard(torch.empty(shape).uniform_(0, 1)).to(self.device, non_blocking=True)
         return self._shard(torch.rand(shape, device=self.device))
 
-    def _generate_D(self, z):
+    def _generate_D(self, z, out=None):
         """The D step's fake batch.  Single samples: G(z) without a graph (GLI copies it into
-        x_fake's .data).  PacGAN: keep G's graph for the G step (PAC:674) and pack."""
+        x_fake's .data), written into ``out`` when given.  PacGAN: keep G's graph for the G
+        step (PAC:674) and pack."""
         if self.pac == 1:
             with torch.no_grad():
-                return self.G(z)
+                return self.G(z, out=out)
         self._zbuf = z.clone()  # the reference's persistent z buffer (GLI:490)
         self._fake_D = self.G(self._zbuf)
         return self._pack(self._fake_D).detach()
@@ -173,22 +174,29 @@ class Trainer:
         self._set_D_grad(True)
         for _ in range(p.Diters):
             D.zero_grad()
-            x = self._real(feed, "x_D")
+            pair = None
+            if self.batch_D and self.pac == 1:
+                # the real batch and G's fake batch are written back to back into one buffer:
+                # the batched D pass reads it as is (no concatenation)
+                pair = torch.empty((2 * self.B, p.n_colors, p.image_size, p.image_size), dtype=torch.float32,
+                                   device=self.device)
+            x = self._real(feed, "x_D", out=pair[:self.B] if pair is not None else None)
             if self.batch_D:
                 # D(x) and D(x_fake) as one batched pass (per-call BN statistics kept):
                 # the draws keep the reference's order (x, then z); D(x) does not read G
                 z = self._normal(feed, "z_D", zshape)
                 self.flush()
-                x_fake = self._generate_D(z)
-                y_pred, y_pred_fake = D.forward_pair(x, x_fake)
+                x_fake = self._generate_D(z, out=pair[self.B:] if pair is not None else None)
+                laid_out = (pair is not None and x.data_ptr() == pair.data_ptr()
+                            and x_fake.data_ptr() == pair[self.B:].data_ptr())
+                y_pred, y_pred_fake = D.forward_pair(x, x_fake, cat=pair if laid_out else None)
                 if kind <= 4:
                     # err_real.backward(); err_fake.backward() accumulate = one backward of the sum
-                    err_real = loss_D_real(kind, y_pred)
-                    err_fake = loss_D_fake(kind, y_pred_fake)
+                    errD_g, _, _ = loss_D_pair(kind, y_pred, y_pred_fake)
                     if not gp_on:
                         self._arm(self.redD)
-                    (err_real + err_fake).backward()
-                    errD = err_real.detach() + err_fake.detach()
+                    errD_g.backward()
+                    errD = errD_g.detach()
                 else:
                     errD = loss_D(kind, y_pred, y_pred_fake)
                     if not gp_on:
