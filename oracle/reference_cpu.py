@@ -583,3 +583,23 @@ def optimizer_state(opt, module):
         if st:
             out[n] = (st["exp_avg"], st["exp_avg_sq"], float(st["step"]))
     return out
+
+
+def checkpoint(t, i, current_set_images):
+    """The reference's checkpoint dict (GLI:737-747; saved with torch.save at GLI:737)."""
+    return {"i": i, "current_set_images": current_set_images, "G_state": t.G.state_dict(),
+            "D_state": t.D.state_dict(), "G_optimizer": t.optG.state_dict(), "D_optimizer": t.optD.state_dict(),
+            "G_scheduler": t.decayG.state_dict(), "D_scheduler": t.decayD.state_dict(), "z_test": t.z_test}
+
+
+def load_checkpoint(t, ck):
+    """GLI:537-549: restore modules, optimizers, schedulers and z_test into a freshly built
+    (and seeded) trainer; returns (iter_offset, current_set_images)."""
+    t.G.load_state_dict(ck["G_state"])
+    t.D.load_state_dict(ck["D_state"])
+    t.optG.load_state_dict(ck["G_optimizer"])
+    t.optD.load_state_dict(ck["D_optimizer"])
+    t.decayG.load_state_dict(ck["G_scheduler"])
+    t.decayD.load_state_dict(ck["D_scheduler"])
+    t.z_test.copy_(ck["z_test"])
+    return ck["i"], ck["current_set_images"]

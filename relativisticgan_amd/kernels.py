@@ -572,22 +572,26 @@ def channel_sum(t, out, accumulate=False):
 
 
 # ------------------------------------------------------------------ loss heads / GP
-def loss_head(kind, side, r, f, need_dr=True, need_df=True):
+def loss_head(kind, side, r, f, need_dr=True, need_df=True, dr=None, df=None):
     t = r if r is not None else f
     n = t.numel()
     loss = torch.empty((), dtype=torch.float32, device=t.device)
-    dr = torch.empty_like(r) if (r is not None and need_dr) else None
-    df = torch.empty_like(f) if (f is not None and need_df) else None
+    if dr is None:
+        dr = torch.empty_like(r) if (r is not None and need_dr) else None
+    if df is None:
+        df = torch.empty_like(f) if (f is not None and need_df) else None
     L.check(L.lib().rgan_loss_head(int(kind), int(side), L.ptr(r), L.ptr(f), n, L.ptr(loss), L.ptr(dr),
                                    L.ptr(df), L.stream()), "rgan_loss_head")
     return loss, dr, df
 
 
-def loss_head_pair(kind, r, f, need_dr=True, need_df=True):
+def loss_head_pair(kind, r, f, need_dr=True, need_df=True, dr=None, df=None):
     """Heads 1-4 D side: (loss3 = [real, fake, sum], dr, df) in one launch."""
     loss3 = torch.empty(3, dtype=torch.float32, device=r.device)
-    dr = torch.empty_like(r) if need_dr else None
-    df = torch.empty_like(f) if need_df else None
+    if dr is None and need_dr:
+        dr = torch.empty_like(r)
+    if df is None and need_df:
+        df = torch.empty_like(f)
     L.check(L.lib().rgan_loss_head_pair(int(kind), L.ptr(r), L.ptr(f), r.numel(), L.ptr(loss3), L.ptr(dr),
                                         L.ptr(df), L.stream()), "rgan_loss_head_pair")
     return loss3, dr, df

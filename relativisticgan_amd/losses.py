@@ -73,6 +73,7 @@ class _HeadPair(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, r, f, kind):
+        ctx.set_materialize_grads(False)
         loss3, dr, df = K.loss_head_pair(kind, r, f, need_dr=ctx.needs_input_grad[0],
                                          need_df=ctx.needs_input_grad[1])
         ctx.save_for_backward(dr, df)
@@ -96,6 +97,38 @@ def loss_D_pair(kind, y_pred, y_pred_fake):
         return er + ef, er.detach(), ef.detach()
     err, loss3 = _HeadPair.apply(_flat(y_pred), _flat(y_pred_fake), kind)
     return err, loss3[0], loss3[1]
+
+
+class _HeadCat(torch.autograd.Function):
+    """The D-step loss on the batched pass's joint output y = [D(x); D(x_fake)] (one
+    autograd input: the gradient is written into one [2B] buffer, no concatenation).
+    Heads 1-4: errD_real + errD_fake (GLI:595-624); heads 5-8: errD (GLI:634-641)."""
+
+    @staticmethod
+    def forward(ctx, y, kind):
+        ctx.set_materialize_grads(False)
+        B = y.numel() // 2
+        dy = torch.empty_like(y)
+        if kind <= 4:
+            loss3, _, _ = K.loss_head_pair(kind, y[:B], y[B:], dr=dy[:B], df=dy[B:])
+            loss = loss3[2]
+        else:
+            loss, _, _ = K.loss_head(kind, 0, y[:B], y[B:], dr=dy[:B], df=dy[B:])
+        ctx.save_for_backward(dy)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        dy, = ctx.saved_tensors
+        return K.scale(dy, g.contiguous()), None
+
+
+def loss_D_cat(kind, y):
+    """errD of the D step from the joint [D(x); D(x_fake)] output (single process)."""
+    if dp.active():
+        B = y.numel() // 2
+        return (loss_D_pair(kind, y[:B], y[B:])[0] if kind <= 4 else loss_D(kind, y[:B], y[B:]))
+    return _HeadCat.apply(y, kind)
 
 
 def loss_D(kind, y_pred, y_pred_fake):

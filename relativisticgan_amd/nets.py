@@ -213,11 +213,12 @@ class _Net(nn.Module):
         reference runs one power iteration per call, so each call has its own sigma)."""
         return not any(layer.spec is not None and layer.spec.spectral for layer in self._plan)
 
-    def forward_segments(self, xs, cat=None):
+    def forward_segments(self, xs, cat=None, flat=False):
         """``[self(x) for x in xs]`` as ONE pass over the concatenated batch: every layer's
         GEMMs run once over all segments, BatchNorm normalises (and updates its running
         statistics) per segment in list order, exactly as the separate calls would.
-        ``cat``: the segments already laid out back to back in one tensor (no copy)."""
+        ``cat``: the segments already laid out back to back in one tensor (no copy);
+        ``flat``: return the joint output (segments back to back) instead of a list."""
         if not self.segmentable:
             raise ValueError("forward_segments: a spectral-norm layer needs one call per forward")
         n = len(xs)
@@ -240,7 +241,7 @@ class _Net(nn.Module):
                 AG.ACT_TRACE.extend(m[s_ * B:(s_ + 1) * B] for m in masks)
                 AG.ACT_TAGS.extend(self._tag for _ in masks)
                 AG.ACT_LAYERS.extend(layers)
-        return list(h.split(B))
+        return h if flat else list(h.split(B))
 
 
 # ---------------------------------------------------------------- arch 0 (DCGAN)
@@ -361,9 +362,10 @@ class _D0(_Net):
         return self._run(x).view(-1)
 
     def forward_pair(self, x, x_fake, cat=None):
-        """(D(x), D(x_fake)) in one batched pass (see ``forward_segments``)."""
-        a, b = self.forward_segments([x, x_fake], cat)
-        return a.reshape(-1), b.reshape(-1)
+        """[D(x); D(x_fake)] as one [2B] vector from one batched pass (``forward_segments``):
+        the loss heads read both halves of it (losses.loss_D_cat), so autograd sees one
+        output and the backward needs no concatenation of two gradients."""
+        return self.forward_segments([x, x_fake], cat, flat=True).reshape(-1)
 
 
 # ---------------------------------------------------------------- arch 1 ("standard CNN", 32x32)
@@ -445,8 +447,7 @@ class _D1(_Net):
         return self._run(x).view(-1)
 
     def forward_pair(self, x, x_fake, cat=None):
-        a, b = self.forward_segments([x, x_fake], cat)
-        return a.reshape(-1), b.reshape(-1)
+        return self.forward_segments([x, x_fake], cat, flat=True).reshape(-1)
 
 
 def DCGAN_G(param):

@@ -20,7 +20,7 @@ import torch
 
 from . import dp
 from .config import TITLES, parse
-from .losses import gradient_penalty, loss_D, loss_D_fake, loss_D_pair, loss_D_real, loss_G
+from .losses import gradient_penalty, loss_D, loss_D_cat, loss_D_fake, loss_D_real, loss_G
 from .nets import DCGAN_D, DCGAN_G, weights_init
 from .optim import Adam
 
@@ -91,6 +91,7 @@ class Trainer:
         bd = (self.world == 1) if bd is None else bool(bd)
         self.batch_D = bd and self.pac == 1 and self.D.segmentable
         self._fake_D = None
+        self._one = None
         self.errD = self.errG = None
         self.last = {}
 
@@ -157,6 +158,14 @@ class Trainer:
         if red is not None:
             red.arm()
 
+    def _backward(self, loss):
+        """loss.backward() (GLI:605/624/644/658/710) with a cached device 1.0 as the seed
+        gradient (autograd would fill a fresh ones tensor on every call)."""
+        one = self._one
+        if one is None or one.device != loss.device:
+            one = self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
+        loss.backward(one)
+
     def _set_D_grad(self, flag):
         for q in self.D.parameters():
             q.requires_grad = flag
@@ -189,23 +198,19 @@ class Trainer:
                 x_fake = self._generate_D(z, out=pair[self.B:] if pair is not None else None)
                 laid_out = (pair is not None and x.data_ptr() == pair.data_ptr()
                             and x_fake.data_ptr() == pair[self.B:].data_ptr())
-                y_pred, y_pred_fake = D.forward_pair(x, x_fake, cat=pair if laid_out else None)
-                if kind <= 4:
-                    # err_real.backward(); err_fake.backward() accumulate = one backward of the sum
-                    errD_g, _, _ = loss_D_pair(kind, y_pred, y_pred_fake)
-                    if not gp_on:
-                        self._arm(self.redD)
-                    errD_g.backward()
-                    errD = errD_g.detach()
-                else:
-                    errD = loss_D(kind, y_pred, y_pred_fake)
-                    if not gp_on:
-                        self._arm(self.redD)
-                    errD.backward()
+                y_all = D.forward_pair(x, x_fake, cat=pair if laid_out else None)
+                y_pred, y_pred_fake = y_all[:self.B], y_all[self.B:]
+                # heads 1-4: err_real.backward(); err_fake.backward() accumulate = one backward
+                # of the sum (GLI:605, 624); heads 5-8: errD.backward() (GLI:644)
+                errD = loss_D_cat(kind, y_all)
+                if not gp_on:
+                    self._arm(self.redD)
+                self._backward(errD)
+                errD = errD.detach()
             elif kind <= 4:
                 y_pred = D(x)
                 err_real = loss_D_real(kind, y_pred)
-                err_real.backward()
+                self._backward(err_real)
                 z = self._normal(feed, "z_D", zshape)
                 self.flush()
                 x_fake = self._generate_D(z)
@@ -213,7 +218,7 @@ class Trainer:
                 err_fake = loss_D_fake(kind, y_pred_fake)
                 if not gp_on:
                     self._arm(self.redD)
-                err_fake.backward()
+                self._backward(err_fake)
                 errD = err_real.detach() + err_fake.detach()
             else:
                 y_pred = D(x)
@@ -224,14 +229,14 @@ class Trainer:
                 errD = loss_D(kind, y_pred, y_pred_fake)
                 if not gp_on:
                     self._arm(self.redD)
-                errD.backward()
+                self._backward(errD)
             rec = {"x": x, "z": z, "y_pred": y_pred.detach(), "y_pred_fake": y_pred_fake.detach(),
                    "errD": errD.detach()}
             if gp_on:
                 u = self._uniform(feed, "u", (p.batch_size, 1, 1, 1))
                 gp = gradient_penalty(D, x, x_fake, u, p.penalty)
                 self._arm(self.redD)
-                gp.backward()
+                self._backward(gp)
                 rec.update(u=u, gp=gp.detach())
             if self.redD is not None:
                 self.redD.finish()
@@ -266,7 +271,7 @@ class Trainer:
                 recG.update(x=x, y_pred=y_pred)
             errG = loss_G(kind, y_pred_fake, y_pred)
             self._arm(self.redG)
-            errG.backward()
+            self._backward(errG)
             recG.update(y_pred_fake=y_pred_fake.detach(), errG=errG.detach())
             self._pending_G = (hooks, recG)
             if self.redG is None:
