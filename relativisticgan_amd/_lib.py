@@ -25,6 +25,11 @@ class RganConv(ctypes.Structure):
                 ("transposed", c_int), ("xs", c_ll * 4), ("ys", c_ll * 4)]
 
 
+class RganSnLayer(ctypes.Structure):
+    _fields_ = [("W", c_vp), ("rows", c_int), ("cols", c_int), ("lo", c_int), ("rs", c_ll), ("hs", c_ll),
+                ("u", c_vp), ("v", c_vp), ("u_copy", c_vp), ("v_copy", c_vp), ("inv_sigma", c_vp)]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "rgan_conv_workspace": (c_sz, [ctypes.POINTER(RganConv), c_int, c_int]),
@@ -83,6 +88,8 @@ _SIGS = {
     "rgan_spectral_ws_bytes": (c_sz, [c_int, c_int]),
     "rgan_spectral_power": (c_int, [c_vp, c_int, c_int, c_ll, c_ll, c_int, c_f, c_vp, c_vp, c_vp, c_int, c_vp,
                                     c_vp]),
+    "rgan_spectral_batch_ws_bytes": (c_sz, [c_int, c_vp]),
+    "rgan_spectral_power_batch": (c_int, [c_int, c_vp, c_f, c_vp, c_vp, c_vp]),
     "rgan_spectral_backward": (c_int, [c_vp, c_vp, c_int, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
                                        c_vp, c_vp]),
     "rgan_adam": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

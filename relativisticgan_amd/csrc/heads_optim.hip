@@ -423,6 +423,182 @@ extern "C" int rgan_spectral_power(const float* W, int rows, int cols, long long
   return 0;
 }
 
+// ---- all of a net's spectral layers in two launches (one power iteration each) ----
+// Phase V: blocks over (layer, 64-column chunk); 4 waves split the rows, lanes take
+// consecutive columns (coalesced rows of W), t[c] = sum_r W(r,c) u[r] complete per block;
+// the layer's last block (a counter, reset by that block) sums the per-block squares in
+// block order and writes v = t / max(||t||, eps).
+// Phase U: blocks over (layer, 4-row chunk), a wave per row: w[r] = sum_c W(r,c) v[c];
+// the layer's last block: u = w / max(||w||, eps), sigma = u . w, inv_sigma = 1/sigma.
+// Both phases are deterministic (fixed-order sums; only the completion counter is atomic).
+constexpr int SNB_MAX = 16;
+struct SnBatch {
+  SnView w[SNB_MAX];
+  float* u[SNB_MAX];
+  float* v[SNB_MAX];
+  float* u2[SNB_MAX];       // nullable second copies (the autograd-saved u, v of this call)
+  float* v2[SNB_MAX];
+  float* inv_sigma[SNB_MAX];
+  float* t[SNB_MAX];        // workspace: [cols] (phase V) / [rows] (phase U)
+  float* part[SNB_MAX];     // workspace: per-block squares
+  int first[SNB_MAX + 1];   // block prefix per layer
+  unsigned* counter;        // [SNB_MAX] zero-initialised, reset by each layer's last block
+  int n;
+  float eps;
+};
+
+__device__ __forceinline__ int snb_layer(const SnBatch& b, int blk) {
+  int l = 0;
+  while (l + 1 < b.n && blk >= b.first[l + 1]) ++l;
+  return l;
+}
+
+// The layer's last block to finish, with every other block's plain global writes visible
+// to it (the in-launch split-K hand-off of cdna_hip_programming.md: per-wave vmcnt drain,
+// barrier, ONE agent-scope release by lane 0, ticket via a relaxed agent-scope vector
+// atomic; the last arriver resets the ticket and takes ONE agent-scope acquire).  Blocks may
+// sit on different XCDs (private L2s): plain stores + a fence-free counter would be stale.
+__device__ __forceinline__ bool snb_last(unsigned* counter, int nblocks) {
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned done = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = done == (unsigned)(nblocks - 1) ? 1 : 0;
+    if (last) {
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  return last != 0;
+}
+
+// fixed-order sum of n per-block partials by wave 0 with lane-indexed (vector) loads; the
+// result is valid in thread 0
+__device__ __forceinline__ float snb_sum_parts(const float* part, int n) {
+  float a = 0.f;
+  if (threadIdx.x < 64) {
+    for (int i = threadIdx.x; i < n; i += 64) a += part[i];
+    a = wave_sum(a);
+  }
+  return a;
+}
+
+__global__ __launch_bounds__(256) void sn_batch_v(SnBatch b) {
+  __shared__ float red[4][64];
+  const int l = snb_layer(b, blockIdx.x), blk = blockIdx.x - b.first[l];
+  const SnView& w = b.w[l];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = blk * 64 + lane;
+  float s = 0.f;
+  if (c < w.cols) {
+    const float* u = b.u[l];
+    for (int r = wid; r < w.rows; r += 4) s += w.W[w.off(r, c)] * u[r];
+  }
+  red[wid][lane] = s;
+  __syncthreads();
+  if (wid == 0) {
+    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    if (c < w.cols) b.t[l][c] = t;
+    const float sq = wave_sum(c < w.cols ? t * t : 0.f);
+    if (lane == 0) b.part[l][blk] = sq;
+  }
+  const int nblk = b.first[l + 1] - b.first[l];
+  if (!snb_last(b.counter + l, nblk)) return;
+  __shared__ float den;
+  const float a = snb_sum_parts(b.part[l], nblk);
+  if (threadIdx.x == 0) den = fmaxf(sqrtf(a), b.eps);
+  __syncthreads();
+  float* v2 = b.v2[l];
+  for (int i = threadIdx.x; i < w.cols; i += blockDim.x) {
+    const float x = b.t[l][i] / den;
+    b.v[l][i] = x;
+    if (v2) v2[i] = x;
+  }
+}
+
+__global__ __launch_bounds__(256) void sn_batch_u(SnBatch b) {
+  __shared__ float red[16];
+  const int l = snb_layer(b, blockIdx.x), blk = blockIdx.x - b.first[l];
+  const SnView& w = b.w[l];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int row = blk * 4 + wid;
+  float s = 0.f;
+  if (row < w.rows) {
+    const float* v = b.v[l];
+    for (int c = lane; c < w.cols; c += 64) s += w.W[w.off(row, c)] * v[c];
+  }
+  s = wave_sum(s);
+  if (lane == 0) red[wid] = row < w.rows ? s : 0.f;
+  __syncthreads();
+  if (threadIdx.x < 4) {  // lane-indexed stores
+    const int i = threadIdx.x;
+    if (blk * 4 + i < w.rows) b.t[l][blk * 4 + i] = red[i];
+    if (i == 0) b.part[l][blk] = red[0] * red[0] + red[1] * red[1] + red[2] * red[2] + red[3] * red[3];
+  }
+  const int nblk = b.first[l + 1] - b.first[l];
+  if (!snb_last(b.counter + l, nblk)) return;
+  __shared__ float den;
+  const float a = snb_sum_parts(b.part[l], nblk);
+  if (threadIdx.x == 0) den = fmaxf(sqrtf(a), b.eps);
+  __syncthreads();
+  float d = 0.f;
+  float* u2 = b.u2[l];
+  for (int r = threadIdx.x; r < w.rows; r += blockDim.x) {
+    const float wr = b.t[l][r], ur = wr / den;
+    b.u[l][r] = ur;
+    if (u2) u2[r] = ur;
+    d += ur * wr;
+  }
+  d = block_sum(d, red);
+  if (threadIdx.x == 0) b.inv_sigma[l][0] = 1.f / d;
+}
+
+extern "C" size_t rgan_spectral_batch_ws_bytes(int n, const RganSnLayer* layers) {
+  if (n <= 0 || n > SNB_MAX || !layers) return 0;
+  size_t f = 0;
+  for (int i = 0; i < n; ++i) {
+    const int cols = layers[i].cols, rows = layers[i].rows;
+    f += (size_t)std::max(cols, rows) + (size_t)std::max(ceil_div(cols, 64), ceil_div(rows, 4)) + 64;
+  }
+  return f * sizeof(float) + 256;
+}
+
+extern "C" int rgan_spectral_power_batch(int n, const RganSnLayer* layers, float eps, void* ws, unsigned* counters,
+                                         void* stream) {
+  RGAN_REQUIRE(n > 0 && n <= SNB_MAX && layers && ws && counters);
+  SnBatch bv{}, bu{};
+  float* p = (float*)ws;
+  int nv = 0, nu = 0;
+  for (int i = 0; i < n; ++i) {
+    const RganSnLayer& L = layers[i];
+    RGAN_REQUIRE(L.W && L.u && L.v && L.inv_sigma && L.rows > 0 && L.cols > 0 && L.lo > 0);
+    const SnView w{L.W, L.rows, L.cols, L.lo, L.rs, L.hs};
+    const int cv = ceil_div(L.cols, 64), cu = ceil_div(L.rows, 4);
+    float* t = p;
+    float* part = t + std::max(L.cols, L.rows);
+    p = part + std::max(cv, cu) + 64;
+    for (SnBatch* b : {&bv, &bu}) {
+      b->w[i] = w; b->u[i] = L.u; b->v[i] = L.v; b->inv_sigma[i] = L.inv_sigma; b->t[i] = t; b->part[i] = part;
+      b->u2[i] = L.u_copy; b->v2[i] = L.v_copy;
+    }
+    bv.first[i] = nv; nv += cv;
+    bu.first[i] = nu; nu += cu;
+  }
+  bv.first[n] = nv; bu.first[n] = nu;
+  bv.n = bu.n = n; bv.eps = bu.eps = eps; bv.counter = bu.counter = counters;
+  hipStream_t s = (hipStream_t)stream;
+  sn_batch_v<<<nv, 256, 0, s>>>(bv);
+  RGAN_CHECK_LAUNCH();
+  sn_batch_u<<<nu, 256, 0, s>>>(bu);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
 // <dWeff, W> over the view, per-block partials then one block reduces
 __global__ __launch_bounds__(256) void sn_dot_kernel(SnView w, const float* __restrict__ dWe,
                                                      float* __restrict__ part) {

@@ -94,6 +94,7 @@ class GPEngine:
         h, xc = self.x_hat, self.img
         AG.TRACE_NET = "D"
         plan = D._plan
+        sns = D._spectral()  # one power iteration per spectral layer, as the reference's D(x_both)
         for li, layer in enumerate(plan):
             AG.TRACE_LAYER = li
             r = _Rec()
@@ -106,12 +107,8 @@ class GPEngine:
             r.beta = bn.bias if bn is not None else None
             if layer.in_view is not None:
                 raise NotImplementedError("GP engine: reshaping D layers")
-            r.sn, r.wscale = None, None
-            if spec.spectral:  # one power iteration per train-mode call (torch spectral_norm pre-hook)
-                inv_sigma = K.spectral_power(r.w.detach(), conv.weight_u, conv.weight_v, spec.geom.transposed,
-                                             do_iter=True)
-                r.sn = (conv.weight_u.clone(), conv.weight_v.clone(), inv_sigma)
-                r.wscale = inv_sigma
+            r.sn = sns.get(li)
+            r.wscale = r.sn[2] if r.sn is not None else None
             r.xc, r.h_in = xc, h
             last = li == len(plan) - 1
             cout = r.w.shape[1] if spec.geom.transposed else r.w.shape[0]

@@ -674,6 +674,38 @@ def spectral_power(w, u, v, transposed, eps=1e-12, do_iter=True):
     return inv_sigma
 
 
+_SN_COUNTERS = {}
+
+
+def spectral_power_batch(layers, eps=1e-12):
+    """One power iteration for every (w, u, v, transposed) of a net call, in two launches
+    (rgan_spectral_power_batch): u, v updated in place; returns [(u_copy, v_copy, inv_sigma)]
+    per layer (the copies autograd saves, as torch spectral_norm's clones)."""
+    n = len(layers)
+    if n == 0:
+        return []
+    if n > 16:
+        raise L.RganError("spectral_power_batch: at most 16 layers per call")
+    dev = layers[0][0].device
+    arr = (L.RganSnLayer * n)()
+    outs = []
+    for i, (w, u, v, tr) in enumerate(layers):
+        rows, cols, rs, hs, lo = sn_view(w, tr)
+        uc, vc = torch.empty_like(u), torch.empty_like(v)
+        inv = torch.empty(1, dtype=torch.float32, device=dev)
+        arr[i] = L.RganSnLayer(w.data_ptr(), rows, cols, lo, rs, hs, u.data_ptr(), v.data_ptr(), uc.data_ptr(),
+                               vc.data_ptr(), inv.data_ptr())
+        outs.append((uc, vc, inv))
+    lib = L.lib()
+    ws = L.workspace(lib.rgan_spectral_batch_ws_bytes(n, ctypes.cast(arr, ctypes.c_void_p)), dev)
+    cnt = _SN_COUNTERS.get(dev)
+    if cnt is None:  # zeroed once; every call leaves them zero (the last block of a layer resets its own)
+        cnt = _SN_COUNTERS[dev] = torch.zeros(16, dtype=torch.int32, device=dev)
+    L.check(lib.rgan_spectral_power_batch(n, ctypes.cast(arr, ctypes.c_void_p), float(eps), L.ptr(ws), L.ptr(cnt),
+                                          L.stream()), "rgan_spectral_power_batch")
+    return outs
+
+
 def spectral_backward(w, dw_eff, u, v, inv_sigma, transposed, out=None):
     """dW_orig of W_eff = W / sigma(W) (u, v constant); ``out`` given: added into it."""
     rows, cols, rs, hs, lo = sn_view(w, transposed)

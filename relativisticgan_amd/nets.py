@@ -24,7 +24,7 @@ import torch.nn as nn
 
 from . import autograd as AG
 from .autograd import ConvLayerFn, LayerSpec
-from .kernels import ConvGeom, spectral_power
+from .kernels import ConvGeom, spectral_power, spectral_power_batch
 
 
 # ---------------------------------------------------------------- parameter holders
@@ -164,15 +164,19 @@ class _Layer:
                                nchw_out=nchw_out) if geom is not None else None)
         self.w_view, self.in_view, self.out_view = w_view, in_view, out_view
 
-    def run(self, h, training, segs=1, out=None):
-        conv, bn = self.conv, self.bn
+    def weight(self):
+        conv = self.conv
         w = conv.w if isinstance(conv, _ConvBase) else conv.weight
-        if self.w_view is not None:
-            w = w.view(*self.w_view)
+        return w.view(*self.w_view) if self.w_view is not None else w
+
+    def run(self, h, training, segs=1, out=None, sn=None):
+        """``sn``: this call's (u, v, inv_sigma) when the net already ran the power
+        iteration of all its spectral layers (_Net._spectral)."""
+        conv, bn = self.conv, self.bn
+        w = self.weight()
         if self.in_view is not None:
             h = h.reshape(h.shape[0], *self.in_view)
-        sn = None
-        if self.spec.spectral:
+        if self.spec.spectral and sn is None:
             with torch.no_grad():
                 inv_sigma = spectral_power(w.detach(), conv.weight_u, conv.weight_v, conv.geom.transposed,
                                            do_iter=training)
@@ -197,14 +201,28 @@ class _Net(nn.Module):
     def _tag(self):
         return type(self).__name__[1]  # "G" / "D": activation-trace tag (parity tests)
 
+    def _spectral(self):
+        """One power iteration for every spectral layer of this call, all in two launches
+        (torch's spectral_norm pre-hook runs one per layer per train-mode call,
+        spectral_norm.py:97-116; u and v of different layers are independent)."""
+        idx = [li for li, l in enumerate(self._plan) if l.spec is not None and l.spec.spectral]
+        if not idx or not self.training:
+            return {}
+        with torch.no_grad():
+            outs = spectral_power_batch([(self._plan[li].weight().detach(), self._plan[li].conv.weight_u,
+                                          self._plan[li].conv.weight_v, self._plan[li].conv.geom.transposed)
+                                         for li in idx])
+        return dict(zip(idx, outs))
+
     def _run(self, x, out=None):
         """``out``: a buffer for the last layer's output (e.g. half of a batched D input)."""
         AG.TRACE_NET = self._tag
         h = x
         last = len(self._plan) - 1
+        sns = self._spectral()
         for li, layer in enumerate(self._plan):
             AG.TRACE_LAYER = li
-            h = layer.run(h, self.training, out=out if li == last else None)
+            h = layer.run(h, self.training, out=out if li == last else None, sn=sns.get(li))
         return h
 
     @property
