@@ -556,3 +556,35 @@ def test_gather(K):
     imgs = torch.randn(10, 3, 4, 4, device=DEV)
     idx = torch.tensor([3, 0, 9], dtype=torch.long, device=DEV)
     assert torch.equal(K.gather_images(imgs, idx), imgs[idx])
+
+
+def test_spectral_power_batch(K):
+    """All spectral layers of a call in two launches == one power iteration per layer
+    (torch spectral_norm, fp64 reference), incl. ConvT (dim 1) and the rows = 1 end layer;
+    the completion counters are left at zero for the next call."""
+    torch.manual_seed(9)
+    specs = [(torch.nn.Conv2d(3, 16, 4, 2, 1, bias=False), False), (torch.nn.Conv2d(16, 300, 4, 2, 1, bias=False), False),
+             (torch.nn.ConvTranspose2d(64, 24, 4, 2, 1, bias=False), True), (torch.nn.Conv2d(300, 1, 4, 1, 0, bias=False), False)]
+    layers, refs = [], []
+    for conv, tr in specs:
+        sn = torch.nn.utils.spectral_norm(conv)
+        w = sn.weight_orig.detach().to(DEV)
+        u, v = sn.weight_u.detach().clone().to(DEV), sn.weight_v.detach().clone().to(DEV)
+        layers.append((w, u, v, tr))
+        W = sn.weight_orig.detach().double()
+        if tr:
+            W = W.permute(1, 0, 2, 3)
+        Wm = W.reshape(W.shape[0], -1)
+        v1 = F.normalize(Wm.t() @ sn.weight_u.double(), dim=0, eps=1e-12)
+        u1 = F.normalize(Wm @ v1, dim=0, eps=1e-12)
+        refs.append((u1, v1, torch.dot(u1, Wm @ v1)))
+    for rep in range(2):  # twice: a second call must find the counters reset
+        outs = K.spectral_power_batch(layers)
+        torch.cuda.synchronize()
+        if rep == 0:
+            for (w, u, v, tr), (uc, vc, inv), (u1, v1, sig) in zip(layers, outs, refs):
+                assert _rel(u, u1) < 1e-5 and _rel(v, v1) < 1e-5
+                assert torch.equal(uc, u) and torch.equal(vc, v)
+                assert abs(1 / inv.item() - sig.item()) < 1e-5 * sig.item()
+    cnt = next(iter(K._SN_COUNTERS.values()))
+    assert int(cnt.abs().sum()) == 0

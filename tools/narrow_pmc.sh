@@ -1,0 +1,36 @@
+#!/bin/bash
+# PMC passes over tools/narrow_micro.py (GPU box).  usage: tools/narrow_pmc.sh OUTDIR
+set -u
+out=$(realpath -m "$1")
+root=$(pwd)
+mkdir -p "$out"
+cd /tmp && export TMPDIR=/tmp
+passes=(
+  "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA"
+  "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAIT_INST_LDS"
+  "FETCH_SIZE"
+  "WRITE_SIZE"
+)
+i=0
+for p in "${passes[@]}"; do
+  i=$((i + 1))
+  timeout -k 10 120 rocprofv3 --pmc $p --kernel-trace -d "$out/p$i" -o run --output-format csv -- \
+    python3 "$root/tools/narrow_micro.py" 10 > "$out/p$i.log" 2>&1
+  rc=$?
+  echo "pass $i rc=$rc"
+  case $rc in 124|137|134|139) exit $rc ;; esac
+done
+python3 - "$out" <<'PY'
+import csv, glob, sys, collections
+out = sys.argv[1]
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(out + "/p*/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        agg[r["Kernel_Name"][:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, d in agg.items():
+    if "narrow" not in k and "gemm" not in k:
+        continue
+    print(k)
+    for c, v in sorted(d.items()):
+        print(f"   {c:28s} {sum(v) / len(v):14.1f}")
+PY
