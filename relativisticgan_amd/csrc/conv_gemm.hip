@@ -1291,6 +1291,109 @@ __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
   }
 }
 
+// Conv2d k4 s2 p1 over an image with CI <= 4 channels producing Cout % 128 == 0 channels
+// NHWC (D's image layer GLI:410, and G's image-layer data gradient): an MFMA-bound layer
+// (K = 16 CI) that also streams its 128-channel output.  One block per 128 output pixels
+// (WT = 128-wide row segments, or 128 / WT whole rows) x 128 channels:
+//   * the tile's input window (2R+2 rows x 2WT+2 columns x CI, zero padded) is loaded once
+//     into LDS with row-contiguous loads (no per-element im2col gather from global);
+//   * the product is formed transposed (rows = channels from the weights, held in 48
+//     VGPRs for the whole tile; columns = pixels): every MFMA's im2col operand is ONE
+//     ds_read_b32 at a compile-time offset from a per-lane pixel base (64 distinct banks);
+//   * the epilogue stages 32 pixels x 64 channels per wave in LDS and writes whole 256-B
+//     channel runs per pixel (16 lanes x float4), instead of 32-B pieces per pixel.
+template <int CI, int WT>
+__global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a) {
+  constexpr int K = CI * 16, NS = K / 2;          // MFMA steps (32x32x2)
+  constexpr int R = WT >= 128 ? 1 : 128 / WT;     // output rows per tile
+  constexpr int RL = 2 * WT + 2, RR = 2 * R + 2;  // window row length, rows
+  constexpr int RS = RR * RL;                     // window floats per channel
+  constexpr int ST_LD = 68;                       // staging row (pixel) stride, floats
+  __shared__ __attribute__((aligned(16))) float win[CI * RS];
+  __shared__ __attribute__((aligned(16))) float stg[4][32 * ST_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, lk = lane >> 5;
+  const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;   // channel rows, pixel columns of this wave
+  const int n0 = blockIdx.y * 128;
+  // tile -> (b, oi0, oj0)
+  const int HWo = a.Ho * a.Wo, m0 = blockIdx.x * 128;
+  const int b = m0 / HWo, rem = m0 - b * HWo, oi0 = rem / a.Wo, oj0 = rem - oi0 * a.Wo;
+  // weights: wa[i][s] = W[n0 + wm + 32 i + l32][2 s + lk]  (torch [Cout][CI][4][4] = [n][k])
+  float wa[2][NS];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) wa[i][s] = a.w[(size_t)(n0 + wm + 32 * i + l32) * K + 2 * s + lk];
+  // input window: rows 2 oi0 - 1 .., columns 2 oj0 - 1 ..
+  {
+    const float* xb = a.x + (long long)b * a.xsb;
+    const int ih0 = 2 * oi0 - 1, iw0 = 2 * oj0 - 1;
+    for (int e = tid; e < CI * RS; e += 256) {
+      const int c = e / RS, r2 = e - c * RS, rr = r2 / RL, cc = r2 - rr * RL;
+      const int ih = ih0 + rr, iw = iw0 + cc;
+      win[e] = ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                   ? xb[(long long)c * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
+                   : 0.f;
+    }
+  }
+  __syncthreads();
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // per-lane pixel bases in the window (pixel p = wn + 32 j + l32 of the tile; k parity = lk)
+  int base[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int p = wn + 32 * j + l32, pr = p / WT, pc = p - pr * WT;
+    base[j] = 2 * pr * RL + 2 * pc + lk;
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    // k = 2 s + lk = 16 ci + 4 kh + kw; the lk part is in base[] (kw parity)
+    const int k0 = 2 * s, ci = k0 >> 4, kh = (k0 >> 2) & 3, kw = k0 & 3;
+    const int off = ci * RS + kh * RL + kw;
+    float bv[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bv[j] = win[base[j] + off];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[i][s], bv[j], acc[i][j], 0, 0, 0);
+  }
+  // epilogue: per pixel tile j, stage [32 pixels][64 channels] then write 256-B runs
+  const float wsc = a.wscale ? a.wscale[0] : 1.f;
+  float* T = stg[wid];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int cl = 32 * i + 8 * g + 4 * lk;  // wave-local channel of register 4g
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = n0 + wm + cl + e;
+          v[e] = act_fwd(acc[i][j][4 * g + e] * wsc + (a.bias ? a.bias[c] : 0.f), a.act, a.alpha);
+        }
+        *reinterpret_cast<float4*>(T + l32 * ST_LD + cl) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    __syncthreads();  // (wave-private buffer; a block barrier keeps the waves' phases aligned)
+    const int q = lane & 15;  // channel quad of the 64-channel run
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int pl = 4 * t + (lane >> 4);          // pixel within the 32
+      const int p = wn + 32 * j + pl, pr = p / WT, pc = p - pr * WT;
+      const long long o = (long long)b * a.ysb + (long long)(oi0 + pr) * a.ysh + (long long)(oj0 + pc) * a.ysw;
+      *reinterpret_cast<float4*>(a.y + o + n0 + wm + 4 * q) = *reinterpret_cast<const float4*>(T + pl * ST_LD + 4 * q);
+    }
+    __syncthreads();
+  }
+}
+
 // k4 s2 p1 ConvTranspose2d with NC <= 4 output channels on v_mfma_f32_4x4x1_16b_f32: 16
 // independent 4x4 outer products per instruction, so the 4 output channels fill the N
 // dimension (75% useful at NC = 3 against 9% for a 32-wide tile) and the 64 lanes are 64
@@ -1529,6 +1632,7 @@ struct Plan {
   // one-output dense layer (MODE_DENSE1): which = 0 fwd, 1 dgrad, 2 wgrad
   DenseArgs da{};
   int dense_op = 0;
+  bool img_in = false;  // MODE_NARROW_IN on the windowed kernel (conv_img_in)
   // BatchNorm moments in the vector epilogue (rgan_conv_fwd_bn): caller's [S][2][C] buffer,
   // equal batch segments whose statistics are kept apart, and whether the launch wrote them
   double* bn_part = nullptr;
@@ -1537,6 +1641,11 @@ struct Plan {
 };
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+static bool getenv_flag(const char* name) {  // A/B switches for experiments
+  const char* e = getenv(name);
+  return e && e[0] && e[0] != '0';
+}
 
 static void tile_dims(int cfg, int& bm, int& bn) {
   bm = cfg == CFG_N ? 256 : 128;
@@ -1703,6 +1812,13 @@ static bool plan_narrow_in(Plan& p, const RganConv* d, const float* x, const flo
                            const float* bias, float* y, int act, float alpha) {
   if (d->transposed || d->cin > 4 || d->kh != 4 || d->kw != 4) return false;
   p.mode = MODE_NARROW_IN;
+  // the windowed kernel (conv_img_in): k4 s2 p1 halving, 128-channel tiles, NHWC output,
+  // 128-pixel tiles that are 128-wide row segments or 128 / Wo whole rows
+  const int wt = std::min(d->wout, 128);
+  p.img_in = !getenv_flag("RGAN_NO_IMG_IN") && d->stride == 2 && d->pad == 1 && d->hout * 2 == d->hin &&
+             d->wout * 2 == d->win && d->cout % 128 == 0 && vec_nhwc(y, d->ys, d->cout) &&
+             ((long long)d->hout * d->wout) % 128 == 0 && (wt == 16 || wt == 32 || wt == 64 || wt == 128) &&
+             d->wout % wt == 0 && ((long long)d->batch * d->hout * d->wout / 128) < (1LL << 31);
   NarrowArgs& a = p.na;
   a.x = x; a.xsb = d->xs[0]; a.xsc = d->xs[1]; a.xsh = d->xs[2]; a.xsw = d->xs[3];
   a.B = d->batch; a.H = d->hin; a.W = d->win; a.C = d->cin;
@@ -1965,7 +2081,7 @@ static std::vector<ProfRec> g_recs;
 static std::vector<std::string> g_kernel_names;
 static double g_cur_flops = 0.0;
 
-constexpr int N_KERNEL_IDS = 50;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense
+constexpr int N_KERNEL_IDS = 51;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in
 
 static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
   const int id = mode == MODE_NARROW_T ? 45
@@ -1997,6 +2113,7 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
     g_kernel_names[47] = "void rgan::dense1_fwd<VEC>(rgan::DenseArgs)";
     g_kernel_names[48] = "void rgan::dense1_dgrad<VEC>(rgan::DenseArgs, rgan::FastDiv)";
     g_kernel_names[49] = "rgan::dense1_wgrad(rgan::DenseArgs)";
+    g_kernel_names[50] = "void rgan::conv_img_in<CI, WT>(rgan::NarrowArgs)";
   }
   return id;
 }
@@ -2022,6 +2139,22 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
       case 3: convt2_narrow_mfma<3><<<blocks, 256, 0, s>>>(a); break;
       default: convt2_narrow_mfma<4><<<blocks, 256, 0, s>>>(a); break;
     }
+  } else if (p.img_in) {
+    const dim3 grid(a.B * a.Ho * a.Wo / 128, a.Cout / 128);
+#define RGAN_IMG(CC)                                                          \
+  switch (std::min(a.Wo, 128)) {                                              \
+    case 16: conv_img_in<CC, 16><<<grid, 256, 0, s>>>(a); break;              \
+    case 32: conv_img_in<CC, 32><<<grid, 256, 0, s>>>(a); break;              \
+    case 64: conv_img_in<CC, 64><<<grid, 256, 0, s>>>(a); break;              \
+    default: conv_img_in<CC, 128><<<grid, 256, 0, s>>>(a); break;             \
+  }
+    switch (a.C) {
+      case 1: RGAN_IMG(1) break;
+      case 2: RGAN_IMG(2) break;
+      case 3: RGAN_IMG(3) break;
+      default: RGAN_IMG(4) break;
+    }
+#undef RGAN_IMG
   } else {
     // persistent: two resident blocks per CU loop over the M tiles
     dim3 grid(std::min(ceil_div(a.B * a.Ho * a.Wo, 128), 512), ceil_div(a.Cout, 128));
@@ -2086,6 +2219,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
       rec.b = g_pool[g_recs.size() * 2 + 1];
       rec.flops = g_cur_flops;
       rec.kid = kernel_id(p.mode, p.mode == MODE_DENSE1 ? p.dense_op : 0, false, false);
+      if (p.mode == MODE_NARROW_IN && p.img_in) rec.kid = 50;
       hipEventRecord(rec.a, s);
     }
     if (p.mode == MODE_DENSE1) run_dense1(p, packed, s);
