@@ -1293,56 +1293,45 @@ __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
 
 // Conv2d k4 s2 p1 over an image with CI <= 4 channels producing Cout % 128 == 0 channels
 // NHWC (D's image layer GLI:410, and G's image-layer data gradient): an MFMA-bound layer
-// (K = 16 CI) that also streams its 128-channel output.  One block per 128 output pixels
-// (WT = 128-wide row segments, or 128 / WT whole rows) x 128 channels:
-//   * the tile's input window (2R+2 rows x 2WT+2 columns x CI, zero padded) is loaded once
-//     into LDS with row-contiguous loads (no per-element im2col gather from global);
-//   * the product is formed transposed (rows = channels from the weights, held in 48
-//     VGPRs for the whole tile; columns = pixels): every MFMA's im2col operand is ONE
-//     ds_read_b32 at a compile-time offset from a per-lane pixel base (64 distinct banks);
+// (K = 16 CI) that also streams its 128-channel output.  Persistent blocks over tiles of 128
+// output pixels (WT = 128-wide row segments, or 128 / WT whole rows) x 128 channels:
+//   * the block's 128 x K weights are loaded once into VGPRs (48 per lane at CI = 3);
+//   * each tile's input window (2R+2 rows x 2WT+2 columns x CI, zero padded) sits in LDS,
+//     double buffered: the next tile's window is loaded into registers (row-contiguous,
+//     no per-element im2col gather) while this tile's MFMAs run;
+//   * the product is formed transposed (rows = channels, columns = pixels): every MFMA's
+//     im2col operand is ONE ds_read_b32 at a compile-time offset from a per-lane pixel base
+//     (the 64 lanes hit 64 distinct banks);
 //   * the epilogue stages 32 pixels x 64 channels per wave in LDS and writes whole 256-B
-//     channel runs per pixel (16 lanes x float4), instead of 32-B pieces per pixel.
+//     channel runs per pixel (16 lanes x float4) instead of 32-B pieces per pixel.
 template <int CI, int WT>
-__global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a) {
+__global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
   constexpr int K = CI * 16, NS = K / 2;          // MFMA steps (32x32x2)
   constexpr int R = WT >= 128 ? 1 : 128 / WT;     // output rows per tile
   constexpr int RL = 2 * WT + 2, RR = 2 * R + 2;  // window row length, rows
   constexpr int RS = RR * RL;                     // window floats per channel
+  constexpr int WIN = CI * RS, WPT = (WIN + 255) / 256;  // window floats, per thread
   constexpr int ST_LD = 68;                       // staging row (pixel) stride, floats
-  __shared__ __attribute__((aligned(16))) float win[CI * RS];
+  __shared__ __attribute__((aligned(16))) float win[2][WIN];
   __shared__ __attribute__((aligned(16))) float stg[4][32 * ST_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, lk = lane >> 5;
   const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;   // channel rows, pixel columns of this wave
   const int n0 = blockIdx.y * 128;
-  // tile -> (b, oi0, oj0)
-  const int HWo = a.Ho * a.Wo, m0 = blockIdx.x * 128;
-  const int b = m0 / HWo, rem = m0 - b * HWo, oi0 = rem / a.Wo, oj0 = rem - oi0 * a.Wo;
+  const int HWo = a.Ho * a.Wo;
   // weights: wa[i][s] = W[n0 + wm + 32 i + l32][2 s + lk]  (torch [Cout][CI][4][4] = [n][k])
   float wa[2][NS];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int s = 0; s < NS; ++s) wa[i][s] = a.w[(size_t)(n0 + wm + 32 * i + l32) * K + 2 * s + lk];
-  // input window: rows 2 oi0 - 1 .., columns 2 oj0 - 1 ..
-  {
-    const float* xb = a.x + (long long)b * a.xsb;
-    const int ih0 = 2 * oi0 - 1, iw0 = 2 * oj0 - 1;
-    for (int e = tid; e < CI * RS; e += 256) {
-      const int c = e / RS, r2 = e - c * RS, rr = r2 / RL, cc = r2 - rr * RL;
-      const int ih = ih0 + rr, iw = iw0 + cc;
-      win[e] = ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
-                   ? xb[(long long)c * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
-                   : 0.f;
-    }
-  }
-  __syncthreads();
-  f32x16 acc[2][2];
+  const float wsc = a.wscale ? a.wscale[0] : 1.f;
+  float bias[2][4][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int g = 0; g < 4; ++g)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int e = 0; e < 4; ++e) bias[i][g][e] = a.bias ? a.bias[n0 + wm + 32 * i + 8 * g + 4 * lk + e] : 0.f;
   // per-lane pixel bases in the window (pixel p = wn + 32 j + l32 of the tile; k parity = lk)
   int base[2];
 #pragma unroll
@@ -1350,47 +1339,88 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a) {
     const int p = wn + 32 * j + l32, pr = p / WT, pc = p - pr * WT;
     base[j] = 2 * pr * RL + 2 * pc + lk;
   }
+  // window of tile t into registers: rows 2 oi0 - 1 .., columns 2 oj0 - 1 ..
+  float wv[WPT];
+  auto fetch = [&](int t) {
+    const int m0 = t * 128, b = m0 / HWo, rem = m0 - b * HWo, oi0 = rem / a.Wo, oj0 = rem - oi0 * a.Wo;
+    const float* xb = a.x + (long long)b * a.xsb;
+    const int ih0 = 2 * oi0 - 1, iw0 = 2 * oj0 - 1;
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    // k = 2 s + lk = 16 ci + 4 kh + kw; the lk part is in base[] (kw parity)
-    const int k0 = 2 * s, ci = k0 >> 4, kh = (k0 >> 2) & 3, kw = k0 & 3;
-    const int off = ci * RS + kh * RL + kw;
-    float bv[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) bv[j] = win[base[j] + off];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[i][s], bv[j], acc[i][j], 0, 0, 0);
-  }
-  // epilogue: per pixel tile j, stage [32 pixels][64 channels] then write 256-B runs
-  const float wsc = a.wscale ? a.wscale[0] : 1.f;
-  float* T = stg[wid];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int cl = 32 * i + 8 * g + 4 * lk;  // wave-local channel of register 4g
-        float v[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int c = n0 + wm + cl + e;
-          v[e] = act_fwd(acc[i][j][4 * g + e] * wsc + (a.bias ? a.bias[c] : 0.f), a.act, a.alpha);
-        }
-        *reinterpret_cast<float4*>(T + l32 * ST_LD + cl) = make_float4(v[0], v[1], v[2], v[3]);
-      }
-    __syncthreads();  // (wave-private buffer; a block barrier keeps the waves' phases aligned)
-    const int q = lane & 15;  // channel quad of the 64-channel run
-#pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int pl = 4 * t + (lane >> 4);          // pixel within the 32
-      const int p = wn + 32 * j + pl, pr = p / WT, pc = p - pr * WT;
-      const long long o = (long long)b * a.ysb + (long long)(oi0 + pr) * a.ysh + (long long)(oj0 + pc) * a.ysw;
-      *reinterpret_cast<float4*>(a.y + o + n0 + wm + 4 * q) = *reinterpret_cast<const float4*>(T + pl * ST_LD + 4 * q);
+    for (int q = 0; q < WPT; ++q) {
+      const int e = tid + 256 * q;
+      const int c = e / RS, r2 = e - c * RS, rr = r2 / RL, cc = r2 - rr * RL;
+      const int ih = ih0 + rr, iw = iw0 + cc;
+      wv[q] = (e < WIN && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                  ? xb[(long long)c * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
+                  : 0.f;
     }
-    __syncthreads();
+  };
+  auto put = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < WPT; ++q) {
+      const int e = tid + 256 * q;
+      if (e < WIN) win[buf][e] = wv[q];
+    }
+  };
+  int t = blockIdx.x, cur = 0;
+  if (t < tiles) {
+    fetch(t);
+    put(0);
+  }
+  __syncthreads();
+  float* T = stg[wid];
+  for (; t < tiles; t += gridDim.x, cur ^= 1) {
+    const int tn = t + (int)gridDim.x;
+    if (tn < tiles) fetch(tn);  // in flight during this tile's MFMAs
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    const float* W0 = win[cur];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      // k = 2 s + lk = 16 ci + 4 kh + kw; the lk part is in base[] (kw parity)
+      const int k0 = 2 * s, ci = k0 >> 4, kh = (k0 >> 2) & 3, kw = k0 & 3;
+      const int off = ci * RS + kh * RL + kw;
+      float bv[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bv[j] = W0[base[j] + off];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[i][s], bv[j], acc[i][j], 0, 0, 0);
+    }
+    // epilogue: per pixel tile j, stage [32 pixels][64 channels] then write 256-B runs
+    const int m0 = t * 128, b = m0 / HWo, rem = m0 - b * HWo, oi0 = rem / a.Wo, oj0 = rem - oi0 * a.Wo;
+    float* yb = a.y + (long long)b * a.ysb + n0 + wm;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int cl = 32 * i + 8 * g + 4 * lk;  // wave-local channel of register 4g
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = act_fwd(acc[i][j][4 * g + e] * wsc + bias[i][g][e], a.act, a.alpha);
+          *reinterpret_cast<float4*>(T + l32 * ST_LD + cl) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      // T is wave-private and a wave's LDS operations complete in order: no barrier
+      const int q = lane & 15;  // channel quad of the 64-channel run
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int pl = 4 * u + (lane >> 4);  // pixel within the 32
+        const int p = wn + 32 * j + pl, pr = p / WT, pc = p - pr * WT;
+        *reinterpret_cast<float4*>(yb + (long long)(oi0 + pr) * a.ysh + (long long)(oj0 + pc) * a.ysw + 4 * q) =
+            *reinterpret_cast<const float4*>(T + pl * ST_LD + 4 * q);
+      }
+    }
+    if (tn < tiles) put(cur ^ 1);
+    __syncthreads();  // next window in place; this window free
   }
 }
 
@@ -2140,13 +2170,15 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
       default: convt2_narrow_mfma<4><<<blocks, 256, 0, s>>>(a); break;
     }
   } else if (p.img_in) {
-    const dim3 grid(a.B * a.Ho * a.Wo / 128, a.Cout / 128);
+    // persistent: two resident blocks per CU loop over the 128-pixel tiles
+    const int tiles = a.B * a.Ho * a.Wo / 128;
+    const dim3 grid(std::min(tiles, 512), a.Cout / 128);
 #define RGAN_IMG(CC)                                                          \
   switch (std::min(a.Wo, 128)) {                                              \
-    case 16: conv_img_in<CC, 16><<<grid, 256, 0, s>>>(a); break;              \
-    case 32: conv_img_in<CC, 32><<<grid, 256, 0, s>>>(a); break;              \
-    case 64: conv_img_in<CC, 64><<<grid, 256, 0, s>>>(a); break;              \
-    default: conv_img_in<CC, 128><<<grid, 256, 0, s>>>(a); break;             \
+    case 16: conv_img_in<CC, 16><<<grid, 256, 0, s>>>(a, tiles); break;       \
+    case 32: conv_img_in<CC, 32><<<grid, 256, 0, s>>>(a, tiles); break;       \
+    case 64: conv_img_in<CC, 64><<<grid, 256, 0, s>>>(a, tiles); break;       \
+    default: conv_img_in<CC, 128><<<grid, 256, 0, s>>>(a, tiles); break;      \
   }
     switch (a.C) {
       case 1: RGAN_IMG(1) break;
