@@ -19,7 +19,21 @@ namespace rgan {
 
 constexpr int WAVE = 64;
 
+// The transcendental activations (tanh, sigmoid, SELU) behind a call: the piecewise-linear
+// ones the hot epilogues run (none, ReLU, LeakyReLU) are one select, and a per-element
+// inlined six-way switch with expf/tanhf bodies no longer bloats every unrolled epilogue
+// (it cost the image-layer conv ~10k issue cycles per tile).
+__device__ __noinline__ float act_fwd_curved(float v, int act, float alpha);
+
 __device__ __forceinline__ float act_fwd(float v, int act, float alpha) {
+  if (act <= RGAN_ACT_LRELU) {
+    const float neg = act == RGAN_ACT_NONE ? 1.f : (act == RGAN_ACT_RELU ? 0.f : alpha);
+    return v > 0.f ? v : v * neg;
+  }
+  return act_fwd_curved(v, act, alpha);
+}
+
+__device__ __noinline__ float act_fwd_curved(float v, int act, float alpha) {
   switch (act) {
     case RGAN_ACT_RELU: return v > 0.f ? v : 0.f;
     case RGAN_ACT_LRELU: return v > 0.f ? v : v * alpha;

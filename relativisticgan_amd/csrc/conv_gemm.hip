@@ -741,19 +741,26 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
           emoff[i] = m < g.M ? row_offset(g.out, m, MODE == MODE_CONVT2 ? phase : 0) : 0;
         }
       }
+      // the activation branch is taken once per tile (uniform), not once per element
+      auto stage = [&](auto actf) {
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int cl = 32 * j + l32, col = n0 + wn + cl;
-        const float bv = (!slab_out && g.bias && col < g.N) ? g.bias[col] : 0.f;
+        for (int j = 0; j < TN; ++j) {
+          const int cl = 32 * j + l32, col = n0 + wn + cl;
+          const float bv = (!slab_out && g.bias && col < g.N) ? g.bias[col] : 0.f;
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+          for (int i = 0; i < TM; ++i)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int rl = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
-            float v = acc[i][j][r];
-            if (!slab_out) v = act_fwd(v * wsc + bv, g.act, g.alpha);
-            T[rl * EP_LD + cl] = v;
-          }
+            for (int r = 0; r < 16; ++r) {
+              const int rl = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+              T[rl * EP_LD + cl] = actf(acc[i][j][r] * wsc + bv);
+            }
+        }
+      };
+      if (slab_out || g.act <= RGAN_ACT_LRELU) {
+        const float neg = (slab_out || g.act == RGAN_ACT_NONE) ? 1.f : (g.act == RGAN_ACT_RELU ? 0.f : g.alpha);
+        stage([neg](float v) { return v > 0.f ? v : v * neg; });
+      } else {
+        stage([&](float v) { return act_fwd_curved(v, g.act, g.alpha); });
       }
       __syncthreads();
       if (!slab_out && g.bnp) {
@@ -830,20 +837,28 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
       const int cl = wn + 32 * j + l32;
       const int col = n0 + cl;
       const float bv = (g.bias && col < g.N) ? g.bias[col] : 0.f;
+      auto put = [&](auto actf) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rl = wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
-        if (m0 + rl < g.M && col < g.N) {
-          float v = acc[i][j][r] * wsc + bv;
+        for (int r = 0; r < 16; ++r) {
+          const int rl = wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+          if (m0 + rl < g.M && col < g.N) {
+            float v = acc[i][j][r] * wsc + bv;
 #if RGAN_EXP_NOSTORE  // timing-only experiment: drop the output stores
-          if (v == 1234.5f)
+            if (v == 1234.5f)
 #endif
-          {
-            float* dst = g.C + moff[rl] + noff[cl];
-            v = act_fwd(v, g.act, g.alpha);
-            *dst = (MODE == MODE_WGRAD && g.accum) ? *dst + v : v;
+            {
+              float* dst = g.C + moff[rl] + noff[cl];
+              v = actf(v);
+              *dst = (MODE == MODE_WGRAD && g.accum) ? *dst + v : v;
+            }
           }
         }
+      };
+      if (g.act <= RGAN_ACT_LRELU) {
+        const float neg = g.act == RGAN_ACT_NONE ? 1.f : (g.act == RGAN_ACT_RELU ? 0.f : g.alpha);
+        put([neg](float v) { return v > 0.f ? v : v * neg; });
+      } else {
+        put([&](float v) { return act_fwd_curved(v, g.act, g.alpha); });
       }
     }
 }
@@ -1152,6 +1167,7 @@ struct NarrowArgs {
   const float* wscale;
   int act;
   float alpha;
+  int exp;                // timing experiments (RGAN_IMG_EXP): 1 skip stores, 2 skip MFMAs, 4 skip window loads
 };
 
 // Conv2d with a 4x4 kernel and CI <= 4 input channels (D's image layer, GLI:410) as ONE MFMA
@@ -1371,7 +1387,7 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
   float* T = stg[wid];
   for (; t < tiles; t += gridDim.x, cur ^= 1) {
     const int tn = t + (int)gridDim.x;
-    if (tn < tiles) fetch(tn);  // in flight during this tile's MFMAs
+    if (tn < tiles && !(a.exp & 4)) fetch(tn);  // in flight during this tile's MFMAs
     f32x16 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -1392,13 +1408,12 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[i][s], bv[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = (a.exp & 2) ? acc[i][j] : __builtin_amdgcn_mfma_f32_32x32x2f32(wa[i][s], bv[j], acc[i][j], 0, 0, 0);
     }
     // epilogue: per pixel tile j, stage [32 pixels][64 channels] then write 256-B runs
     const int m0 = t * 128, b = m0 / HWo, rem = m0 - b * HWo, oi0 = rem / a.Wo, oj0 = rem - oi0 * a.Wo;
     float* yb = a.y + (long long)b * a.ysb + n0 + wm;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    auto stage = [&](int j, auto actf) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1406,17 +1421,27 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
           const int cl = 32 * i + 8 * g + 4 * lk;  // wave-local channel of register 4g
           float v[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = act_fwd(acc[i][j][4 * g + e] * wsc + bias[i][g][e], a.act, a.alpha);
+          for (int e = 0; e < 4; ++e) v[e] = actf(acc[i][j][4 * g + e] * wsc + bias[i][g][e]);
           *reinterpret_cast<float4*>(T + l32 * ST_LD + cl) = make_float4(v[0], v[1], v[2], v[3]);
         }
+    };
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (a.act <= RGAN_ACT_LRELU) {  // one uniform branch per 32 values, not one per value
+        const float neg = a.act == RGAN_ACT_NONE ? 1.f : (a.act == RGAN_ACT_RELU ? 0.f : a.alpha);
+        stage(j, [neg](float v) { return v > 0.f ? v : v * neg; });
+      } else {
+        stage(j, [&](float v) { return act_fwd_curved(v, a.act, a.alpha); });
+      }
       // T is wave-private and a wave's LDS operations complete in order: no barrier
       const int q = lane & 15;  // channel quad of the 64-channel run
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int pl = 4 * u + (lane >> 4);  // pixel within the 32
         const int p = wn + 32 * j + pl, pr = p / WT, pc = p - pr * WT;
-        *reinterpret_cast<float4*>(yb + (long long)(oi0 + pr) * a.ysh + (long long)(oj0 + pc) * a.ysw + 4 * q) =
-            *reinterpret_cast<const float4*>(T + pl * ST_LD + 4 * q);
+        const float4 v = *reinterpret_cast<const float4*>(T + pl * ST_LD + 4 * q);
+        if (!(a.exp & 1) || v.x == 1234.5f)
+          *reinterpret_cast<float4*>(yb + (long long)(oi0 + pr) * a.ysh + (long long)(oj0 + pc) * a.ysw + 4 * q) = v;
       }
     }
     if (tn < tiles) put(cur ^ 1);
@@ -2170,6 +2195,11 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
       default: convt2_narrow_mfma<4><<<blocks, 256, 0, s>>>(a); break;
     }
   } else if (p.img_in) {
+    static const int exp_flags = [] {
+      const char* e = getenv("RGAN_IMG_EXP");
+      return e ? atoi(e) : 0;
+    }();
+    a.exp = exp_flags;
     // persistent: two resident blocks per CU loop over the 128-pixel tiles
     const int tiles = a.B * a.Ho * a.Wo / 128;
     const dim3 grid(std::min(tiles, 512), a.Cout / 128);
