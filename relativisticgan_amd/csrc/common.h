@@ -25,6 +25,19 @@ constexpr int WAVE = 64;
 // (it cost the image-layer conv ~10k issue cycles per tile).
 __device__ __noinline__ float act_fwd_curved(float v, int act, float alpha);
 
+// Bare v_max_f32 / v_min_f32: fmaxf's IEEE semantics make the compiler canonicalize both
+// inputs first (two extra VALU per call); the epilogue values here are never sNaN.
+__device__ __forceinline__ float vmaxf(float a, float b) {
+  float r;
+  asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ float vminf(float a, float b) {
+  float r;
+  asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
 __device__ __forceinline__ float act_fwd(float v, int act, float alpha) {
   if (act <= RGAN_ACT_LRELU) {
     const float neg = act == RGAN_ACT_NONE ? 1.f : (act == RGAN_ACT_RELU ? 0.f : alpha);

@@ -1167,7 +1167,7 @@ struct NarrowArgs {
   const float* wscale;
   int act;
   float alpha;
-  int exp;                // timing experiments (RGAN_IMG_EXP): 1 skip stores, 2 skip MFMAs, 4 skip window loads
+  int x_bytes, y_bytes;   // conv_img_in: byte extents of x and y (< 2^31, buffer descriptors)
 };
 
 // Conv2d with a 4x4 kernel and CI <= 4 input channels (D's image layer, GLI:410) as ONE MFMA
@@ -1310,16 +1310,30 @@ __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
 // Conv2d k4 s2 p1 over an image with CI <= 4 channels producing Cout % 128 == 0 channels
 // NHWC (D's image layer GLI:410, and G's image-layer data gradient): an MFMA-bound layer
 // (K = 16 CI) that also streams its 128-channel output.  Persistent blocks over tiles of 128
-// output pixels (WT = 128-wide row segments, or 128 / WT whole rows) x 128 channels:
-//   * the block's 128 x K weights are loaded once into VGPRs (48 per lane at CI = 3);
-//   * each tile's input window (2R+2 rows x 2WT+2 columns x CI, zero padded) sits in LDS,
-//     double buffered: the next tile's window is loaded into registers (row-contiguous,
-//     no per-element im2col gather) while this tile's MFMAs run;
+// output pixels (WT = 128-wide row segments, or 128 / WT whole rows) x 128 channels.
+// fp32 MFMA and VALU share one issue pipe on gfx950, so the kernel is built to issue as
+// little VALU as possible around its 96 MFMAs per wave-tile:
+//   * the block's 128 x K weights (x the spectral 1/sigma) sit in VGPRs for every tile, and
+//     the bias is the accumulator's initial value (first MFMA's C operand);
+//   * each tile's input window (2R+2 rows x 2WT+2 columns x CI) is loaded by LDS-DMA
+//     (buffer_load ... lds, lane-linear, no VGPRs), double buffered one tile ahead; the zero
+//     padding is the buffer's out-of-range read (per-element edge flags against a per-tile
+//     mask: 4 VALU per element);
 //   * the product is formed transposed (rows = channels, columns = pixels): every MFMA's
 //     im2col operand is ONE ds_read_b32 at a compile-time offset from a per-lane pixel base
-//     (the 64 lanes hit 64 distinct banks);
+//     (64 lanes on 64 distinct banks), all read before the MFMA chain starts;
 //   * the epilogue stages 32 pixels x 64 channels per wave in LDS and writes whole 256-B
-//     channel runs per pixel (16 lanes x float4) instead of 32-B pieces per pixel.
+//     channel runs per pixel (16 lanes x float4) with buffer stores whose per-(tile, row)
+//     part is a scalar offset.
+#ifndef IMGX_NOMFMA  // timing experiments only (tools/build_variant.py -DIMGX_...=1)
+#define IMGX_NOMFMA 0
+#endif
+#ifndef IMGX_NOSTORE
+#define IMGX_NOSTORE 0
+#endif
+#ifndef IMGX_NOFETCH
+#define IMGX_NOFETCH 0
+#endif
 template <int CI, int WT>
 __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
   constexpr int K = CI * 16, NS = K / 2;          // MFMA steps (32x32x2)
@@ -1328,26 +1342,41 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
   constexpr int RS = RR * RL;                     // window floats per channel
   constexpr int WIN = CI * RS, WPT = (WIN + 255) / 256;  // window floats, per thread
   constexpr int ST_LD = 68;                       // staging row (pixel) stride, floats
-  __shared__ __attribute__((aligned(16))) float win[2][WIN];
+  constexpr int OOB_OFF = 0x7ffffff0;
+  // two named window buffers (not one indexed array): the tile loop is unrolled by two so
+  // every LDS read names its buffer and the compiler does not wait for the other buffer's
+  // in-flight DMA before reading this one
+  __shared__ __attribute__((aligned(16))) float winA[WPT * 256];
+  __shared__ __attribute__((aligned(16))) float winB[WPT * 256];
   __shared__ __attribute__((aligned(16))) float stg[4][32 * ST_LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, lk = lane >> 5;
   const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;   // channel rows, pixel columns of this wave
   const int n0 = blockIdx.y * 128;
   const int HWo = a.Ho * a.Wo;
-  // weights: wa[i][s] = W[n0 + wm + 32 i + l32][2 s + lk]  (torch [Cout][CI][4][4] = [n][k])
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, a.y_bytes, 0x00020000);
+  // weights: wa[i][s] = W[n0 + wm + 32 i + l32][2 s + lk] / sigma  (torch [Cout][CI][4][4] = [n][k])
   float wa[2][NS];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int s = 0; s < NS; ++s) wa[i][s] = a.w[(size_t)(n0 + wm + 32 * i + l32) * K + 2 * s + lk];
-  const float wsc = a.wscale ? a.wscale[0] : 1.f;
-  float bias[2][4][4];
+  if (a.wscale) {
+    const float wsc = a.wscale[0];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int s = 0; s < NS; ++s) wa[i][s] *= wsc;
+  }
+  // keep the weights resident (the compiler would otherwise re-load them inside the tile loop)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bias[i][g][e] = a.bias ? a.bias[n0 + wm + 32 * i + 8 * g + 4 * lk + e] : 0.f;
+    for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(wa[i][s]));
+  // the block's 128 biases in LDS: each tile's accumulators start from them (4 ds_read_b128
+  // per 32-channel group; register 4g+e of group i = channel 32 i + 8 g + 4 lk + e)
+  __shared__ __attribute__((aligned(16))) float bsh[128];
+  if (tid < 128) bsh[tid] = a.bias ? a.bias[n0 + tid] : 0.f;
   // per-lane pixel bases in the window (pixel p = wn + 32 j + l32 of the tile; k parity = lk)
   int base[2];
 #pragma unroll
@@ -1355,97 +1384,154 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
     const int p = wn + 32 * j + l32, pr = p / WT, pc = p - pr * WT;
     base[j] = 2 * pr * RL + 2 * pc + lk;
   }
-  // window of tile t into registers: rows 2 oi0 - 1 .., columns 2 oj0 - 1 ..
-  float wv[WPT];
-  auto fetch = [&](int t) {
-    const int m0 = t * 128, b = m0 / HWo, rem = m0 - b * HWo, oi0 = rem / a.Wo, oj0 = rem - oi0 * a.Wo;
-    const float* xb = a.x + (long long)b * a.xsb;
-    const int ih0 = 2 * oi0 - 1, iw0 = 2 * oj0 - 1;
+  // window element e = tid + 256 q = (c, rr, cc): source offset relative to the tile's
+  // (2 oi0, 2 oj0) corner and edge flags (1 left column, 2 right, 4 top row, 8 bottom,
+  // 16 beyond the window) -- tile-invariant, computed once
+  // kept in LDS as (byte offset << 5 | flags), one word per element (VGPRs are the limit here)
+  __shared__ int wtab[WPT * 256];
 #pragma unroll
-    for (int q = 0; q < WPT; ++q) {
-      const int e = tid + 256 * q;
-      const int c = e / RS, r2 = e - c * RS, rr = r2 / RL, cc = r2 - rr * RL;
-      const int ih = ih0 + rr, iw = iw0 + cc;
-      wv[q] = (e < WIN && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
-                  ? xb[(long long)c * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
-                  : 0.f;
-    }
-  };
-  auto put = [&](int buf) {
-#pragma unroll
-    for (int q = 0; q < WPT; ++q) {
-      const int e = tid + 256 * q;
-      if (e < WIN) win[buf][e] = wv[q];
-    }
-  };
-  int t = blockIdx.x, cur = 0;
-  if (t < tiles) {
-    fetch(t);
-    put(0);
+  for (int q = 0; q < WPT; ++q) {
+    const int e = tid + 256 * q;
+    const int c = e / RS, r2 = e - c * RS, rr = r2 / RL, cc = r2 - rr * RL;
+    const int o = (int)(((long long)c * a.xsc + (long long)(rr - 1) * a.xsh + (long long)(cc - 1) * a.xsw) * 4);
+    const int f = e >= WIN ? 16 : (cc == 0 ? 1 : 0) | (cc == RL - 1 ? 2 : 0) | (rr == 0 ? 4 : 0) | (rr == RR - 1 ? 8 : 0);
+    wtab[e] = (o << 5) | f;  // host: per-image byte extent < 2^26
   }
   __syncthreads();
+  auto tile_pos = [&](int t, int& b, int& oi0, int& oj0) {
+    const int m0 = t * 128;
+    b = m0 / HWo;
+    const int rem = m0 - b * HWo;
+    oi0 = rem / a.Wo;
+    oj0 = rem - oi0 * a.Wo;
+  };
+  // LDS-DMA of tile t's window into win[buf] (out-of-range lanes read the buffer past its end: 0)
+  auto fetch = [&](int t, float* dst) {
+    int b, oi0, oj0;
+    tile_pos(t, b, oi0, oj0);
+    const int mask = 16 | (oj0 == 0 ? 1 : 0) | (oj0 + WT >= a.Wo ? 2 : 0) | (oi0 == 0 ? 4 : 0) | (oi0 + R >= a.Ho ? 8 : 0);
+    const int tb = (int)(((long long)b * a.xsb + 2LL * oi0 * a.xsh + 2LL * oj0 * a.xsw) * 4);
+    int wt[WPT];  // all table reads first: a DMA may not start while an LDS read is pending
+#pragma unroll
+    for (int q = 0; q < WPT; ++q) wt[q] = wtab[tid + 256 * q];
+#pragma unroll
+    for (int q = 0; q < WPT; ++q) {
+      const int off = (wt[q] & mask) ? OOB_OFF : (wt[q] >> 5) + tb;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          xr, (__attribute__((address_space(3))) void*)(dst + 256 * q + 64 * wid), 4, off, 0, 0, 0);
+    }
+  };
+  int t = blockIdx.x;
+  if (t < tiles) fetch(t, winA);
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's window pieces landed
+  __builtin_amdgcn_s_barrier();
   float* T = stg[wid];
-  for (; t < tiles; t += gridDim.x, cur ^= 1) {
+  const int q4 = lane & 15;  // channel quad of a 64-channel run (epilogue)
+  const int wn_s = __builtin_amdgcn_readfirstlane(wn);  // wave-uniform (the compiler cannot tell)
+  const int ysh4 = (int)(a.ysh * 4), ysw4 = (int)(a.ysw * 4);
+  const int lvo = (int)(((long long)(lane >> 4) * a.ysw + 4 * q4 + n0 + wm) * 4);
+  auto tile = [&](int t, const float* W0, float* Wn) {
     const int tn = t + (int)gridDim.x;
-    if (tn < tiles && !(a.exp & 4)) fetch(tn);  // in flight during this tile's MFMAs
-    f32x16 acc[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    const float* W0 = win[cur];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
+    if (tn < tiles && !IMGX_NOFETCH) fetch(tn, Wn);  // lands during this tile's MFMAs
+    // im2col operands read RD steps ahead of their MFMAs (sched barriers pin the order: the
+    // scheduler would otherwise sink each read next to its use and expose the LDS latency)
+#ifndef IMGX_RD
+#define IMGX_RD 3
+#endif
+    constexpr int RD = IMGX_RD;
+    float bv[NS][2];
+    auto read_step = [&](int s) {
       // k = 2 s + lk = 16 ci + 4 kh + kw; the lk part is in base[] (kw parity)
       const int k0 = 2 * s, ci = k0 >> 4, kh = (k0 >> 2) & 3, kw = k0 & 3;
       const int off = ci * RS + kh * RL + kw;
-      float bv[2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bv[j] = W0[base[j] + off];
+      for (int j = 0; j < 2; ++j) bv[s][j] = W0[base[j] + off];
+    };
+    f32x16 b0[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 v = *reinterpret_cast<const float4*>(bsh + wm + 32 * i + 8 * g + 4 * lk);
+        b0[i][4 * g] = v.x; b0[i][4 * g + 1] = v.y; b0[i][4 * g + 2] = v.z; b0[i][4 * g + 3] = v.w;
+      }
+#pragma unroll
+    for (int s = 0; s < RD; ++s) read_step(s);
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s + RD < NS) read_step(s + RD);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = (a.exp & 2) ? acc[i][j] : __builtin_amdgcn_mfma_f32_32x32x2f32(wa[i][s], bv[j], acc[i][j], 0, 0, 0);
+#if !IMGX_NOMFMA
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[i][s], bv[s][j], s == 0 ? b0[i] : acc[i][j], 0, 0, 0);
+#else
+          acc[i][j] = s == 0 ? b0[i] : acc[i][j], acc[i][j][s & 15] += bv[s][j];
+#endif
+      __builtin_amdgcn_sched_barrier(0);
     }
+    // the next window's DMA pieces (issued at the top of this tile) have landed by now; the
+    // wait sits before this tile's stores so that it never waits for them (vmcnt counts both)
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     // epilogue: per pixel tile j, stage [32 pixels][64 channels] then write 256-B runs
-    const int m0 = t * 128, b = m0 / HWo, rem = m0 - b * HWo, oi0 = rem / a.Wo, oj0 = rem - oi0 * a.Wo;
-    float* yb = a.y + (long long)b * a.ysb + n0 + wm;
+    int b, oi0, oj0;
+    tile_pos(t, b, oi0, oj0);
+    // the store offsets are built in SGPRs: a VALU write right behind a buffer_store may
+    // clobber its data registers before they are read (hipcc 7.2 / gfx950 inserts no wait
+    // state for v_lshl_add_u64 there -- observed as corrupted lanes 12-15 of the first store)
+    const int tb4 = (int)(((long long)b * a.ysb + (long long)oi0 * a.ysh + (long long)oj0 * a.ysw) * 4);
     auto stage = [&](int j, auto actf) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int cl = 32 * i + 8 * g + 4 * lk;  // wave-local channel of register 4g
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = actf(acc[i][j][4 * g + e] * wsc + bias[i][g][e]);
-          *reinterpret_cast<float4*>(T + l32 * ST_LD + cl) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(T + l32 * ST_LD + cl) =
+              make_float4(actf(acc[i][j][4 * g]), actf(acc[i][j][4 * g + 1]), actf(acc[i][j][4 * g + 2]),
+                          actf(acc[i][j][4 * g + 3]));
         }
     };
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      if (a.act <= RGAN_ACT_LRELU) {  // one uniform branch per 32 values, not one per value
-        const float neg = a.act == RGAN_ACT_NONE ? 1.f : (a.act == RGAN_ACT_RELU ? 0.f : a.alpha);
-        stage(j, [neg](float v) { return v > 0.f ? v : v * neg; });
+      // one uniform branch per 32 values, not one per value
+      if (a.act == RGAN_ACT_NONE) {
+        stage(j, [](float v) { return v; });
+      } else if (a.act <= RGAN_ACT_LRELU) {
+        const float neg = a.act == RGAN_ACT_RELU ? 0.f : a.alpha;
+        if (neg <= 1.f) stage(j, [neg](float v) { return vmaxf(v, v * neg); });
+        else stage(j, [neg](float v) { return vminf(v, v * neg); });
       } else {
         stage(j, [&](float v) { return act_fwd_curved(v, a.act, a.alpha); });
       }
       // T is wave-private and a wave's LDS operations complete in order: no barrier
-      const int q = lane & 15;  // channel quad of the 64-channel run
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(T + (4 * u + (lane >> 4)) * ST_LD + 4 * q4);
+      __builtin_amdgcn_sched_barrier(0);  // all 8 reads in flight before the first store waits
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int pl = 4 * u + (lane >> 4);  // pixel within the 32
-        const int p = wn + 32 * j + pl, pr = p / WT, pc = p - pr * WT;
-        const float4 v = *reinterpret_cast<const float4*>(T + pl * ST_LD + 4 * q);
-        if (!(a.exp & 1) || v.x == 1234.5f)
-          *reinterpret_cast<float4*>(yb + (long long)(oi0 + pr) * a.ysh + (long long)(oj0 + pc) * a.ysw + 4 * q) = v;
+        // pixel wn + 32 j + 4 u + lane / 16: its row is uniform per (j, u) (WT >= 16)
+        const int p = wn_s + 32 * j + 4 * u, pr = p / WT, pc = p - pr * WT;
+        const int so = tb4 + pr * ysh4 + pc * ysw4;  // scalar (SALU) arithmetic only
+#if IMGX_NOSTORE
+        if (v[u].x == 1234.5f)
+#endif
+        __builtin_amdgcn_raw_buffer_store_b128(
+            u32x4{__float_as_uint(v[u].x), __float_as_uint(v[u].y), __float_as_uint(v[u].z), __float_as_uint(v[u].w)},
+            yr, lvo, so, 0);
       }
     }
-    if (tn < tiles) put(cur ^ 1);
-    __syncthreads();  // next window in place; this window free
+    // every wave's window pieces landed (each waited for its own above), this window and
+    // the staging free; the stores stay in flight
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+  };
+  for (; t < tiles; t += 2 * (int)gridDim.x) {
+    tile(t, winA, winB);
+    if (t + (int)gridDim.x < tiles) tile(t + (int)gridDim.x, winB, winA);
   }
 }
 
@@ -1874,12 +1960,21 @@ static bool plan_narrow_in(Plan& p, const RganConv* d, const float* x, const flo
              d->wout * 2 == d->win && d->cout % 128 == 0 && vec_nhwc(y, d->ys, d->cout) &&
              ((long long)d->hout * d->wout) % 128 == 0 && (wt == 16 || wt == 32 || wt == 64 || wt == 128) &&
              d->wout % wt == 0 && ((long long)d->batch * d->hout * d->wout / 128) < (1LL << 31);
+  const long long xext = 4 * (1 + (d->batch - 1) * d->xs[0] + (d->cin - 1) * d->xs[1] + (d->hin - 1) * d->xs[2] +
+                              (d->win - 1) * d->xs[3]);
+  const long long yext = 4 * (1 + (d->batch - 1) * d->ys[0] + (d->cout - 1) * d->ys[1] + (d->hout - 1) * d->ys[2] +
+                              (d->wout - 1) * d->ys[3]);
+  const long long ximg = 4 * (1 + (d->cin - 1) * d->xs[1] + (d->hin - 1) * d->xs[2] + (d->win - 1) * d->xs[3]);
+  p.img_in = p.img_in && d->xs[0] >= 0 && d->xs[1] >= 0 && d->xs[2] >= 0 && d->xs[3] >= 0 && xext < (1LL << 31) &&
+             yext < (1LL << 31) && ximg < (1LL << 25);
   NarrowArgs& a = p.na;
   a.x = x; a.xsb = d->xs[0]; a.xsc = d->xs[1]; a.xsh = d->xs[2]; a.xsw = d->xs[3];
   a.B = d->batch; a.H = d->hin; a.W = d->win; a.C = d->cin;
   a.w = w; a.y = y; a.ysb = d->ys[0]; a.ysc = d->ys[1]; a.ysh = d->ys[2]; a.ysw = d->ys[3];
   a.Ho = d->hout; a.Wo = d->wout; a.Cout = d->cout; a.stride = d->stride; a.pad = d->pad;
   a.bias = bias; a.wscale = wscale; a.act = act; a.alpha = alpha;
+  a.x_bytes = (int)std::min(xext, (1LL << 31) - 1);
+  a.y_bytes = (int)std::min(yext, (1LL << 31) - 1);
   p.pack = false;
   return true;
 }
@@ -2195,11 +2290,6 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
       default: convt2_narrow_mfma<4><<<blocks, 256, 0, s>>>(a); break;
     }
   } else if (p.img_in) {
-    static const int exp_flags = [] {
-      const char* e = getenv("RGAN_IMG_EXP");
-      return e ? atoi(e) : 0;
-    }();
-    a.exp = exp_flags;
     // persistent: two resident blocks per CU loop over the 128-pixel tiles
     const int tiles = a.B * a.Ho * a.Wo / 128;
     const dim3 grid(std::min(tiles, 512), a.Cout / 128);

@@ -1,13 +1,16 @@
 #!/bin/bash
-# PMC passes over tools/narrow_micro.py (GPU box).  usage: tools/narrow_pmc.sh OUTDIR
+# PMC passes over tools/narrow_micro.py (GPU box).  usage: tools/narrow_pmc.sh OUTDIR [lib]
+# (lib: an experiment build from tools/build_variant.py, loaded through RGAN_LIB)
 set -u
 out=$(realpath -m "$1")
 root=$(pwd)
+[ -n "${2:-}" ] && export RGAN_LIB=$(realpath "$2")
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
 passes=(
   "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA"
-  "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAIT_INST_LDS"
+  "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_WAVES SQ_INSTS_SMEM"
+  "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_FLAT"
   "FETCH_SIZE"
   "WRITE_SIZE"
 )
@@ -28,7 +31,7 @@ for f in glob.glob(out + "/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         agg[r["Kernel_Name"][:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
-    if "narrow" not in k and "gemm" not in k:
+    if not any(s in k for s in ("narrow", "gemm", "img_in")):
         continue
     print(k)
     for c, v in sorted(d.items()):
