@@ -22,6 +22,7 @@
 #include "common.h"
 
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace rgan {
@@ -1158,7 +1159,7 @@ struct NarrowArgs {
   const float* x;
   long long xsb, xsc, xsh, xsw;
   int B, H, W, C;         // input grid
-  const float* w;         // NARROW_T: packed [C][4][4][NC];  NARROW_IN: torch [Cout][C][KH][KW]
+  const float* w;         // NARROW_T: packed [C][4][64] (pack_narrow);  NARROW_IN: torch [Cout][C][KH][KW]
   float* y;
   long long ysb, ysc, ysh, ysw;
   int Ho, Wo, Cout;
@@ -1307,231 +1308,234 @@ __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
   }
 }
 
-// Conv2d k4 s2 p1 over an image with CI <= 4 channels producing Cout % 128 == 0 channels
-// NHWC (D's image layer GLI:410, and G's image-layer data gradient): an MFMA-bound layer
-// (K = 16 CI) that also streams its 128-channel output.  Persistent blocks over tiles of 128
-// output pixels (WT = 128-wide row segments, or 128 / WT whole rows) x 128 channels.
-// fp32 MFMA and VALU share one issue pipe on gfx950, so the kernel is built to issue as
-// little VALU as possible around its 96 MFMAs per wave-tile:
-//   * the block's 128 x K weights (x the spectral 1/sigma) sit in VGPRs for every tile, and
-//     the bias is the accumulator's initial value (first MFMA's C operand);
-//   * each tile's input window (2R+2 rows x 2WT+2 columns x CI) is loaded by LDS-DMA
-//     (buffer_load ... lds, lane-linear, no VGPRs), double buffered one tile ahead; the zero
-//     padding is the buffer's out-of-range read (per-element edge flags against a per-tile
-//     mask: 4 VALU per element);
-//   * the product is formed transposed (rows = channels, columns = pixels): every MFMA's
-//     im2col operand is ONE ds_read_b32 at a compile-time offset from a per-lane pixel base
-//     (64 lanes on 64 distinct banks), all read before the MFMA chain starts;
-//   * the epilogue stages 32 pixels x 64 channels per wave in LDS and writes whole 256-B
-//     channel runs per pixel (16 lanes x float4) with buffer stores whose per-(tile, row)
-//     part is a scalar offset.
-#ifndef IMGX_NOMFMA  // timing experiments only (tools/build_variant.py -DIMGX_...=1)
-#define IMGX_NOMFMA 0
-#endif
-#ifndef IMGX_NOSTORE
-#define IMGX_NOSTORE 0
-#endif
-#ifndef IMGX_NOFETCH
-#define IMGX_NOFETCH 0
-#endif
-template <int CI, int WT>
+// Conv2d k4 s2 p1 over an image with CI <= 3 channels producing Cout % 128 == 0 channels
+// NHWC (D's image layer GLI:410, and G's image-layer data gradient).  K = 16 CI is too
+// short for the pipelined GEMM, and the layer both runs 6.4 GFLOP of fp32 MFMA and streams
+// a 128-channel output (C3 shard: 268 MB).  Every WAVE is an independent persistent worker
+// (no block barrier anywhere in the loop: the per-tile barrier of a block-shared window held
+// the MFMA pipe at ~50 % through convoys of waves waiting for each other):
+//   * a wave tile is 32 consecutive output pixels (a row segment, or 2 rows of 16) x the
+//     block's 128 channels: 4 accumulators of 32 x 32, channels as MFMA rows;
+//   * the wave's 128 x K weights (x the spectral 1/sigma) stay in VGPRs, so each MFMA step
+//     reads ONE im2col operand from LDS (a ds_read_b32 at a compile-time offset) for 4
+//     MFMAs; the bias is the accumulators' initial value;
+//   * its input window (2R+2 rows x 2 WS+8 columns x CI, 16-B aligned) arrives by LDS-DMA
+//     (buffer_load_dwordx4 ... lds into a wave-private double buffer, one tile ahead); the
+//     zero padding is the buffer's out-of-range read (whole float4s lie inside or outside
+//     the image: W % 4 == 0);
+//   * epilogue per 32-channel group: activation, staging in a wave-private XOR-swizzled LDS
+//     tile, read back as 128-B channel runs, buffer stores with SGPR offsets.
+// fp32 MFMA and VALU share an issue pipe on gfx950: the VALU left is 2 per activated value
+// and 4 per DMA piece; two waves per SIMD hide each other's epilogue behind their MFMAs.
+// Measured at the C3 shape (32 x 3 x 256^2 -> 128 ch, tools/narrow_micro.py, HIP events
+// incl. a ~6 us launch floor): 133 us for the block-tiled predecessor, 79 us here.  The
+// same loop without the epilogue runs at the MFMA roof (~43 us); the prologue's weight
+// staging must be bank-conflict free (row stride K + 1: an 8-way conflicted version cost
+// 9 us per launch).
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+// byte address of an LDS location, wave-uniform (M0 operand of an LDS-DMA)
+__device__ __forceinline__ int lds_addr(const float* p) {
+  return __builtin_amdgcn_readfirstlane((int)(uintptr_t)(const __attribute__((address_space(3))) float*)p);
+}
+// One 16-B-per-lane LDS-DMA piece: lane l's 16 bytes at byte offset voff of the raw buffer
+// land at LDS byte m0 + 16 l (an out-of-range voff writes zeros).
+__device__ __forceinline__ void dma_lds16(int m0, int voff, i32x4 rsrc) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(m0), "v"(voff), "s"(rsrc)
+               : "memory", "m0");
+}
+
+template <int CI, int WS, int ACT>  // ACT 0: identity, 1: max(v, v * neg) (ReLU / LeakyReLU, neg <= 1), 2: act_fwd
 __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
   constexpr int K = CI * 16, NS = K / 2;          // MFMA steps (32x32x2)
-  constexpr int R = WT >= 128 ? 1 : 128 / WT;     // output rows per tile
-  constexpr int RL = 2 * WT + 2, RR = 2 * R + 2;  // window row length, rows
-  constexpr int RS = RR * RL;                     // window floats per channel
-  constexpr int WIN = CI * RS, WPT = (WIN + 255) / 256;  // window floats, per thread
-  constexpr int ST_LD = 68;                       // staging row (pixel) stride, floats
+  constexpr int RW = 32 / WS;                     // output rows per wave tile (1 or 2)
+  constexpr int RR = 2 * RW + 2, CW = 2 * WS + 8; // window rows, columns (image cols 2 oj0 - 4 ..)
+  constexpr int WCH = RR * CW;                    // window floats per channel
+  constexpr int WIN = CI * WCH, NQ = WIN / 4;     // window floats, float4s
+  constexpr int QPL = (NQ + 63) / 64;             // DMA pieces per lane
+  constexpr int WSTG = (128 * (K + 1) + 511) / 512 * 64;  // 1/8 of the prologue's weight staging
+  constexpr int WBUF = QPL * 256 > WSTG ? QPL * 256 : WSTG;  // one window buffer (floats)
+  constexpr int RD = 4;                           // im2col read-ahead (MFMA steps)
   constexpr int OOB_OFF = 0x7ffffff0;
-  // two named window buffers (not one indexed array): the tile loop is unrolled by two so
-  // every LDS read names its buffer and the compiler does not wait for the other buffer's
-  // in-flight DMA before reading this one
-  __shared__ __attribute__((aligned(16))) float winA[WPT * 256];
-  __shared__ __attribute__((aligned(16))) float winB[WPT * 256];
-  __shared__ __attribute__((aligned(16))) float stg[4][32 * ST_LD];
+  static_assert(CW % 4 == 0 && WIN % 4 == 0, "window rows are float4-aligned");
+  __shared__ __attribute__((aligned(16))) float win[4][2][WBUF];
+  __shared__ __attribute__((aligned(16))) float stg[4][32 * 32];  // per wave [pixel][channel quad ^ swz]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, lk = lane >> 5;
-  const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;   // channel rows, pixel columns of this wave
   const int n0 = blockIdx.y * 128;
   const int HWo = a.Ho * a.Wo;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
+  // raw buffer descriptor of x for the DMA pieces (stride 0, num_records = byte extent)
+  const i32x4 xd = {(int)(uintptr_t)a.x, (int)((uintptr_t)a.x >> 32), a.x_bytes, 0x00020000};
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, a.y_bytes, 0x00020000);
-  // weights: wa[i][s] = W[n0 + wm + 32 i + l32][2 s + lk] / sigma  (torch [Cout][CI][4][4] = [n][k])
-  float wa[2][NS];
+  // weights: wa[i][s] = W[n0 + 32 i + l32][2 s + lk] / sigma  (torch [Cout][CI][4][4] = [n][k])
+  // (staged through LDS by the whole block with coalesced loads: 128 x K floats, once)
+  // (every global load of the prologue is issued before the first wait: at ~1-2 us per
+  // round trip, a dependent sequence of them costs as much as several tiles)
+  constexpr int WLD = (128 * K + 255) / 256;
+  float wtmp[WLD];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int q = 0; q < WLD; ++q) {
+    const int e = tid + 256 * q;
+    wtmp[q] = e < 128 * K ? a.w[(size_t)n0 * K + e] : 0.f;
+  }
+  const float wsc = a.wscale ? a.wscale[0] : 1.f;
+  float wb[4];  // bias column (see below)
 #pragma unroll
-    for (int s = 0; s < NS; ++s) wa[i][s] = a.w[(size_t)(n0 + wm + 32 * i + l32) * K + 2 * s + lk];
+  for (int i = 0; i < 4; ++i) wb[i] = (a.bias && lk == 0) ? a.bias[n0 + 32 * i + l32] : 0.f;
+  {
+    float* wst = &win[0][0][0];  // the window buffers are free until the first DMA
+    static_assert(4 * 2 * WBUF >= 128 * (K + 1), "weight staging fits the window buffers");
+#pragma unroll
+    for (int q = 0; q < WLD; ++q) {
+      const int e = tid + 256 * q, r = e / K;  // row stride K + 1: conflict-free reads below
+      if (e < 128 * K) wst[e + r] = wtmp[q];
+    }
+    __syncthreads();
+  }
+  float wa[4][NS];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int s = 0; s < NS; ++s) wa[i][s] = win[0][0][(32 * i + l32) * (K + 1) + 2 * s + lk];
   if (a.wscale) {
-    const float wsc = a.wscale[0];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int s = 0; s < NS; ++s) wa[i][s] *= wsc;
   }
-  // keep the weights resident (the compiler would otherwise re-load them inside the tile loop)
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(wa[i][s]));
-  // the block's 128 biases in LDS: each tile's accumulators start from them (4 ds_read_b128
-  // per 32-channel group; register 4g+e of group i = channel 32 i + 8 g + 4 lk + e)
-  __shared__ __attribute__((aligned(16))) float bsh[128];
-  if (tid < 128) bsh[tid] = a.bias ? a.bias[n0 + tid] : 0.f;
-  // per-lane pixel bases in the window (pixel p = wn + 32 j + l32 of the tile; k parity = lk)
-  int base[2];
+    for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(wa[i][s]));  // resident: no re-load in the loop
+  // bias as one extra MFMA step per accumulator (wb: k0 = bias, k1 = 0, against a column of
+  // ones): the accumulators start from it exactly, with no per-tile LDS reads
+  const float one_k0 = lk == 0 ? 1.f : 0.f;
+  __syncthreads();  // weight staging read before the window buffers are reused
+  // this lane's pixel: row pr, column pc of the wave tile; window base of its im2col reads
+  const int pr = l32 / WS, pc = l32 - pr * WS;
+  const int base = 2 * pr * CW + 2 * pc + 3 + lk;
+  // DMA piece q of this lane = window float4 f = 64 q + lane = (c, rr, c4): source byte offset
+  // relative to the tile's (2 oi0, 2 oj0) corner, and edge flags (1 left float4, 2 right,
+  // 4 top row, 8 bottom row, 16 beyond the window), 5 bits per piece
+  int wofs[QPL], wflag = 0;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int p = wn + 32 * j + l32, pr = p / WT, pc = p - pr * WT;
-    base[j] = 2 * pr * RL + 2 * pc + lk;
+  for (int q = 0; q < QPL; ++q) {
+    const int f = 64 * q + lane;
+    const int c = f / (WCH / 4), r2 = f - c * (WCH / 4), rr = r2 / (CW / 4), c4 = r2 - rr * (CW / 4);
+    wofs[q] = (int)(((long long)c * a.xsc + (long long)(rr - 1) * a.xsh + (long long)(4 * c4 - 4)) * 4);
+    const int fl = f >= NQ ? 16 : (c4 == 0 ? 1 : 0) | (c4 == CW / 4 - 1 ? 2 : 0) | (rr == 0 ? 4 : 0) | (rr == RR - 1 ? 8 : 0);
+    wflag |= fl << (5 * q);
   }
-  // window element e = tid + 256 q = (c, rr, cc): source offset relative to the tile's
-  // (2 oi0, 2 oj0) corner and edge flags (1 left column, 2 right, 4 top row, 8 bottom,
-  // 16 beyond the window) -- tile-invariant, computed once
-  // kept in LDS as (byte offset << 5 | flags), one word per element (VGPRs are the limit here)
-  __shared__ int wtab[WPT * 256];
-#pragma unroll
-  for (int q = 0; q < WPT; ++q) {
-    const int e = tid + 256 * q;
-    const int c = e / RS, r2 = e - c * RS, rr = r2 / RL, cc = r2 - rr * RL;
-    const int o = (int)(((long long)c * a.xsc + (long long)(rr - 1) * a.xsh + (long long)(cc - 1) * a.xsw) * 4);
-    const int f = e >= WIN ? 16 : (cc == 0 ? 1 : 0) | (cc == RL - 1 ? 2 : 0) | (rr == 0 ? 4 : 0) | (rr == RR - 1 ? 8 : 0);
-    wtab[e] = (o << 5) | f;  // host: per-image byte extent < 2^26
-  }
-  __syncthreads();
   auto tile_pos = [&](int t, int& b, int& oi0, int& oj0) {
-    const int m0 = t * 128;
+    const int m0 = t * 32;
     b = m0 / HWo;
     const int rem = m0 - b * HWo;
     oi0 = rem / a.Wo;
     oj0 = rem - oi0 * a.Wo;
   };
-  // LDS-DMA of tile t's window into win[buf] (out-of-range lanes read the buffer past its end: 0)
   auto fetch = [&](int t, float* dst) {
     int b, oi0, oj0;
     tile_pos(t, b, oi0, oj0);
-    const int mask = 16 | (oj0 == 0 ? 1 : 0) | (oj0 + WT >= a.Wo ? 2 : 0) | (oi0 == 0 ? 4 : 0) | (oi0 + R >= a.Ho ? 8 : 0);
-    const int tb = (int)(((long long)b * a.xsb + 2LL * oi0 * a.xsh + 2LL * oj0 * a.xsw) * 4);
-    int wt[WPT];  // all table reads first: a DMA may not start while an LDS read is pending
+    const int mask = 16 | (oj0 == 0 ? 1 : 0) | (oj0 + WS >= a.Wo ? 2 : 0) | (oi0 == 0 ? 4 : 0) | (oi0 + RW >= a.Ho ? 8 : 0);
+    const int tb = (int)(((long long)b * a.xsb + 2LL * oi0 * a.xsh + 2LL * oj0) * 4);
 #pragma unroll
-    for (int q = 0; q < WPT; ++q) wt[q] = wtab[tid + 256 * q];
-#pragma unroll
-    for (int q = 0; q < WPT; ++q) {
-      const int off = (wt[q] & mask) ? OOB_OFF : (wt[q] >> 5) + tb;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          xr, (__attribute__((address_space(3))) void*)(dst + 256 * q + 64 * wid), 4, off, 0, 0, 0);
+    for (int q = 0; q < QPL; ++q) {
+      const int off = ((wflag >> (5 * q)) & mask) ? OOB_OFF : wofs[q] + tb;
+      dma_lds16(lds_addr(dst + 256 * q), off, xd);
     }
   };
-  int t = blockIdx.x;
-  if (t < tiles) fetch(t, winA);
-  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): this wave's window pieces landed
-  __builtin_amdgcn_s_barrier();
+  // epilogue geometry: staging T[pixel][quad ^ ((pixel >> 1) & 7)] (conflict-free writes of
+  // (pixel l32, quad 2g + lk) and reads of (pixel 8u + lane / 8, quad lane % 8)); each store
+  // instruction writes 8 pixels x 128 B
   float* T = stg[wid];
-  const int q4 = lane & 15;  // channel quad of a 64-channel run (epilogue)
-  const int wn_s = __builtin_amdgcn_readfirstlane(wn);  // wave-uniform (the compiler cannot tell)
+  const int rq = lane & 7, rp = lane >> 3;
+  const int lvo = (int)(((long long)rp * a.ysw + 4 * rq + n0) * 4);
   const int ysh4 = (int)(a.ysh * 4), ysw4 = (int)(a.ysw * 4);
-  const int lvo = (int)(((long long)(lane >> 4) * a.ysw + 4 * q4 + n0 + wm) * 4);
-  auto tile = [&](int t, const float* W0, float* Wn) {
-    const int tn = t + (int)gridDim.x;
-    if (tn < tiles && !IMGX_NOFETCH) fetch(tn, Wn);  // lands during this tile's MFMAs
-    // im2col operands read RD steps ahead of their MFMAs (sched barriers pin the order: the
-    // scheduler would otherwise sink each read next to its use and expose the LDS latency)
-#ifndef IMGX_RD
-#define IMGX_RD 3
-#endif
-    constexpr int RD = IMGX_RD;
-    float bv[NS][2];
+  const float neg = a.act == RGAN_ACT_RELU ? 0.f : a.alpha;
+  auto actf = [&](float v) {
+    if constexpr (ACT == 0) return v;
+    else if constexpr (ACT == 1) return vmaxf(v, v * neg);
+    else return act_fwd(v, a.act, a.alpha);
+  };
+  const int G = (int)gridDim.x * 4;
+  int t = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wid);  // wave-uniform (SGPR)
+  if (t >= tiles) return;
+  float* W0 = win[wid][0];
+  float* W1 = win[wid][1];
+  fetch(t, W0);
+  // one wave tile: MFMAs from window Wr, then the next tile's window into Wn, then the
+  // epilogue.  The DMA pieces are inline asm (dma_lds16), invisible to the compiler's wait
+  // insertion -- which cannot tell the buffers apart and would stall every later LDS read on
+  // them -- so the waits for them are the explicit vmcnt below, and nothing else in the loop
+  // loads from global memory
+  auto tile = [&](int t, const float* Wr, float* Wn, auto first_c) {
+    const int tn = t + G;
+    const bool more = tn < tiles;
+    // this tile's window landed: the previous tile's 16 stores went out after its DMA and
+    // may stay in flight (vmcnt retires in issue order)
+    if constexpr (decltype(first_c)::value) __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+    else __builtin_amdgcn_s_waitcnt(0x4f70);                                      // vmcnt(16)
+    float bv[NS];
     auto read_step = [&](int s) {
-      // k = 2 s + lk = 16 ci + 4 kh + kw; the lk part is in base[] (kw parity)
+      // k = 2 s + lk = 16 ci + 4 kh + kw; the lk part is in base (kw parity)
       const int k0 = 2 * s, ci = k0 >> 4, kh = (k0 >> 2) & 3, kw = k0 & 3;
-      const int off = ci * RS + kh * RL + kw;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bv[s][j] = W0[base[j] + off];
+      bv[s] = Wr[base + ci * WCH + kh * CW + kw];
     };
-    f32x16 b0[2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int s = 0; s < RD && s < NS; ++s) read_step(s);
+    f32x16 acc[4];
+    const f32x16 zero = {};
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 v = *reinterpret_cast<const float4*>(bsh + wm + 32 * i + 8 * g + 4 * lk);
-        b0[i][4 * g] = v.x; b0[i][4 * g + 1] = v.y; b0[i][4 * g + 2] = v.z; b0[i][4 * g + 3] = v.w;
-      }
-#pragma unroll
-    for (int s = 0; s < RD; ++s) read_step(s);
-    f32x16 acc[2][2];
+    for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[i], one_k0, zero, 0, 0, 0);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (s + RD < NS) read_step(s + RD);
-      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#if !IMGX_NOMFMA
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[i][s], bv[s][j], s == 0 ? b0[i] : acc[i][j], 0, 0, 0);
-#else
-          acc[i][j] = s == 0 ? b0[i] : acc[i][j], acc[i][j][s & 15] += bv[s][j];
-#endif
-      __builtin_amdgcn_sched_barrier(0);
+      for (int i = 0; i < 4; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[i][s], bv[s], acc[i], 0, 0, 0);
     }
-    // the next window's DMA pieces (issued at the top of this tile) have landed by now; the
-    // wait sits before this tile's stores so that it never waits for them (vmcnt counts both)
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-    // epilogue: per pixel tile j, stage [32 pixels][64 channels] then write 256-B runs
+    if (more) fetch(tn, Wn);
     int b, oi0, oj0;
     tile_pos(t, b, oi0, oj0);
-    // the store offsets are built in SGPRs: a VALU write right behind a buffer_store may
-    // clobber its data registers before they are read (hipcc 7.2 / gfx950 inserts no wait
-    // state for v_lshl_add_u64 there -- observed as corrupted lanes 12-15 of the first store)
     const int tb4 = (int)(((long long)b * a.ysb + (long long)oi0 * a.ysh + (long long)oj0 * a.ysw) * 4);
-    auto stage = [&](int j, auto actf) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int cl = 32 * i + 8 * g + 4 * lk;  // wave-local channel of register 4g
-          *reinterpret_cast<float4*>(T + l32 * ST_LD + cl) =
-              make_float4(actf(acc[i][j][4 * g]), actf(acc[i][j][4 * g + 1]), actf(acc[i][j][4 * g + 2]),
-                          actf(acc[i][j][4 * g + 3]));
-        }
-    };
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      // one uniform branch per 32 values, not one per value
-      if (a.act == RGAN_ACT_NONE) {
-        stage(j, [](float v) { return v; });
-      } else if (a.act <= RGAN_ACT_LRELU) {
-        const float neg = a.act == RGAN_ACT_RELU ? 0.f : a.alpha;
-        if (neg <= 1.f) stage(j, [neg](float v) { return vmaxf(v, v * neg); });
-        else stage(j, [neg](float v) { return vminf(v, v * neg); });
-      } else {
-        stage(j, [&](float v) { return act_fwd_curved(v, a.act, a.alpha); });
+      for (int g = 0; g < 4; ++g) {
+        const int quad = 2 * g + lk;
+        *reinterpret_cast<float4*>(T + l32 * 32 + 4 * (quad ^ ((l32 >> 1) & 7))) =
+            make_float4(actf(acc[i][4 * g]), actf(acc[i][4 * g + 1]), actf(acc[i][4 * g + 2]), actf(acc[i][4 * g + 3]));
       }
-      // T is wave-private and a wave's LDS operations complete in order: no barrier
-      float4 v[8];
+      float4 ev[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const float4*>(T + (4 * u + (lane >> 4)) * ST_LD + 4 * q4);
-      __builtin_amdgcn_sched_barrier(0);  // all 8 reads in flight before the first store waits
+      for (int u = 0; u < 4; ++u) {
+        const int pl = 8 * u + rp;
+        ev[u] = *reinterpret_cast<const float4*>(T + pl * 32 + 4 * (rq ^ ((pl >> 1) & 7)));
+      }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        // pixel wn + 32 j + 4 u + lane / 16: its row is uniform per (j, u) (WT >= 16)
-        const int p = wn_s + 32 * j + 4 * u, pr = p / WT, pc = p - pr * WT;
-        const int so = tb4 + pr * ysh4 + pc * ysw4;  // scalar (SALU) arithmetic only
-#if IMGX_NOSTORE
-        if (v[u].x == 1234.5f)
-#endif
+      for (int u = 0; u < 4; ++u) {
+        // pixels 8 u .. 8 u + 7 of the wave tile lie in one output row (WS >= 16).  The
+        // offsets stay in SGPRs: a VALU write right behind a buffer_store may clobber its
+        // data registers before they are read (hipcc 7.2 / gfx950 inserted no wait state
+        // after a v_lshl_add_u64 there -- observed as corrupted lanes 12-15 of a store)
+        const int p = 8 * u, prr = p / WS, pcc = p - prr * WS;
+        const int so = tb4 + prr * ysh4 + pcc * ysw4 + 128 * i;
         __builtin_amdgcn_raw_buffer_store_b128(
-            u32x4{__float_as_uint(v[u].x), __float_as_uint(v[u].y), __float_as_uint(v[u].z), __float_as_uint(v[u].w)},
+            u32x4{__float_as_uint(ev[u].x), __float_as_uint(ev[u].y), __float_as_uint(ev[u].z), __float_as_uint(ev[u].w)},
             yr, lvo, so, 0);
       }
     }
-    // every wave's window pieces landed (each waited for its own above), this window and
-    // the staging free; the stores stay in flight
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
   };
-  for (; t < tiles; t += 2 * (int)gridDim.x) {
-    tile(t, winA, winB);
-    if (t + (int)gridDim.x < tiles) tile(t + (int)gridDim.x, winB, winA);
+  using F = std::integral_constant<bool, false>;
+  using Tr = std::integral_constant<bool, true>;
+  tile(t, W0, W1, Tr{});
+  for (;;) {
+    t += G;
+    if (t >= tiles) break;
+    tile(t, W1, W0, F{});
+    t += G;
+    if (t >= tiles) break;
+    tile(t, W0, W1, F{});
   }
 }
 
@@ -1553,28 +1557,33 @@ constexpr int NM_XPT = (NM_XQ + 255) / 256;         // ... per thread
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// 4x4x1 MFMA whose B operand is lane group g (lanes 16 g .. 16 g + 15) of b, broadcast to
+// all 16 blocks (BLGP = 4 + g; g must fold to a constant)
+__device__ __forceinline__ f32x4 mfma4_bcast(float a, float b, f32x4 c, int g) {
+  switch (g) {
+    case 0: return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 4);
+    case 1: return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 5);
+    case 2: return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 6);
+    default: return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 7);
+  }
+}
+
 template <int NC>
-__global__ __launch_bounds__(256, 2) void convt2_narrow_mfma(NarrowArgs a) {
+__global__ __launch_bounds__(256, 2) void convt2_narrow_mfma(NarrowArgs a, int ntiles) {
   __shared__ __attribute__((aligned(16))) float xs[NM_HR * NM_HC * NM_LD];
-  __shared__ __attribute__((aligned(16))) float wl[4 * NM_CH * 16];
+  __shared__ __attribute__((aligned(16))) float wl[NM_CH * 256];  // [c][r][lane] (pack_narrow order)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int tiles_c = (a.W + NM_TC - 1) / NM_TC, tiles_r = (a.H + NM_TR - 1) / NM_TR;
   const int per_img = tiles_c * tiles_r;
-  const int b = blockIdx.x / per_img, trem = blockIdx.x - b * per_img;
-  const int tr = trem / tiles_c, tc = trem - tr * tiles_c;
-  const int r0 = tr * NM_TR, c0p = tc * NM_TC;
-  const float* xb = a.x + (long long)b * a.xsb;
   const int co = lane & 3;
   // this lane's pixel in each group (tile coords): row 4 wid + lane / 16, col 16 g + lane % 16
   const int pr = 4 * wid + (lane >> 4), pc = lane & 15;
-  f32x4 acc[2][4];
-#pragma unroll
-  for (int g = 0; g < 2; ++g)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[g][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int ch0 = 0; ch0 < a.C; ch0 += NM_CH) {
-    const int nch = min(NM_CH, a.C - ch0);
-    float4 stage[NM_XPT];
+  // Persistent over (image, 16 x 32 tile) with the next channel chunk's halo and weights
+  // loaded into registers while the current chunk's MFMAs run (the one-shot grid of 1024
+  // blocks ran a 3-blocks-per-CU round plus a 1-block tail, every chunk's loads exposed).
+  float4 stage[NM_XPT];
+  float4 wv[4];
+  auto load_chunk = [&](const float* xb, int r0, int c0p, int ch0) {
 #pragma unroll
     for (int t = 0; t < NM_XPT; ++t) {
       const int e = tid + 256 * t, pix = e >> 2, q = e & 3;
@@ -1585,83 +1594,123 @@ __global__ __launch_bounds__(256, 2) void convt2_narrow_mfma(NarrowArgs a) {
         v = *reinterpret_cast<const float4*>(xb + (long long)ih * a.xsh + (long long)iw * a.xsw + c);
       stage[t] = v;
     }
-    // weights: packed [4][C][16]; this chunk's [co][c][tap] (c >= nch -> 0)
-    const int wc = tid >> 4, wq = (tid >> 2) & 3, wco = tid & 3;  // 16 ch x 4 quads x 4 co = 256
-    float4 wv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (wc < nch) wv = *reinterpret_cast<const float4*>(a.w + ((size_t)wco * a.C + ch0 + wc) * 16 + 4 * wq);
-    __syncthreads();  // previous chunk's reads are done
+    // weights: this chunk's [c][r][lane] slice of the pack, contiguous (c >= C -> 0)
 #pragma unroll
-    for (int t = 0; t < NM_XPT; ++t) {
-      const int e = tid + 256 * t;
-      if (e < NM_XQ) *reinterpret_cast<float4*>(xs + (e >> 2) * NM_LD + 4 * (e & 3)) = stage[t];
+    for (int q = 0; q < 4; ++q) {
+      const int e = 4 * (tid + 256 * q);  // float index within the chunk's 16 x 256
+      wv[q] = ch0 + (e >> 8) < a.C ? *reinterpret_cast<const float4*>(a.w + (size_t)ch0 * 256 + e)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    *reinterpret_cast<float4*>(wl + (wco * NM_CH + wc) * 16 + 4 * wq) = wv;
-    __syncthreads();
-    for (int c4 = 0; c4 < nch / 4; ++c4) {
-      float4 xv[2][3][3];
+  };
+  auto tile_of = [&](int t, int& b, int& r0, int& c0p) {
+    b = t / per_img;
+    const int trem = t - b * per_img, tr = trem / tiles_c;
+    r0 = tr * NM_TR;
+    c0p = (trem - tr * tiles_c) * NM_TC;
+  };
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  {
+    int b, r0, c0p;
+    tile_of(t, b, r0, c0p);
+    load_chunk(a.x + (long long)b * a.xsb, r0, c0p, 0);
+  }
+  for (; t < ntiles; t += gridDim.x) {
+    int b, r0, c0p;
+    tile_of(t, b, r0, c0p);
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc[g][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ch0 = 0; ch0 < a.C; ch0 += NM_CH) {
+      const int nch = min(NM_CH, a.C - ch0);
+      __syncthreads();  // previous chunk's (or tile's) LDS reads are done
+#pragma unroll
+      for (int q = 0; q < NM_XPT; ++q) {
+        const int e = tid + 256 * q;
+        if (e < NM_XQ) *reinterpret_cast<float4*>(xs + (e >> 2) * NM_LD + 4 * (e & 3)) = stage[q];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(wl + 4 * (tid + 256 * q)) = wv[q];
+      __syncthreads();
+      // the next chunk (or the next tile's first chunk) into registers during the MFMAs
+      if (ch0 + NM_CH < a.C) {
+        load_chunk(a.x + (long long)b * a.xsb, r0, c0p, ch0 + NM_CH);
+      } else if (t + (int)gridDim.x < ntiles) {
+        int b2, r2, c2;
+        tile_of(t + (int)gridDim.x, b2, r2, c2);
+        load_chunk(a.x + (long long)b2 * a.xsb, r2, c2, 0);
+      }
+      for (int c4 = 0; c4 < nch / 4; ++c4) {
+        float4 xv[2][3][3];
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+          for (int u = 0; u < 3; ++u)
+#pragma unroll
+            for (int v = 0; v < 3; ++v)
+              xv[g][u][v] = *reinterpret_cast<const float4*>(xs + ((pr + u) * NM_HC + 16 * g + pc + v) * NM_LD + 4 * c4);
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          // B operands: 4 registers of 4 taps each (one ds_read_b32 apiece: 64 distinct
+          // words); the MFMA's BLGP = 4 + g broadcasts lane group g (tap 4 r + g, co = lane % 4)
+          // to all 16 blocks
+          float wr[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) wr[r] = wl[((4 * c4 + cc) * 4 + r) * 64 + lane];
+          // (th, tw) outermost: 8 consecutive MFMAs on 8 different accumulators
+#pragma unroll
+          for (int th = 0; th < 2; ++th)
+#pragma unroll
+            for (int tw = 0; tw < 2; ++tw)
+#pragma unroll
+              for (int ph = 0; ph < 2; ++ph)
+#pragma unroll
+                for (int pw = 0; pw < 2; ++pw) {
+                  const int tap = (2 * th + 1 - ph) * 4 + (2 * tw + 1 - pw);
+#pragma unroll
+                  for (int g = 0; g < 2; ++g) {
+                    const float4 xq = xv[g][ph - th + 1][pw - tw + 1];
+                    const float xa = cc == 0 ? xq.x : cc == 1 ? xq.y : cc == 2 ? xq.z : xq.w;
+                    acc[g][ph * 2 + pw] = mfma4_bcast(xa, wr[tap >> 2], acc[g][ph * 2 + pw], tap & 3);
+                  }
+                }
+        }
+      }
+    }
+    if (co < NC) {
+      const float wsc = a.wscale ? a.wscale[0] : 1.f;
+      const float bv = a.bias ? a.bias[co] : 0.f;
+      float* yb = a.y + (long long)b * a.ysb + (long long)co * a.ysc;
+      const int blk = lane >> 2;  // this lane holds pixels 4 blk + i of each group, channel co
 #pragma unroll
       for (int g = 0; g < 2; ++g)
 #pragma unroll
-        for (int u = 0; u < 3; ++u)
+        for (int i = 0; i < 4; ++i) {
+          const int q = 4 * blk + i;  // pixel index within the group (lane order)
+          const int gi = r0 + 4 * wid + (q >> 4), gj = c0p + 16 * g + (q & 15);
+          if (gi >= a.H || gj >= a.W) continue;
 #pragma unroll
-          for (int v = 0; v < 3; ++v)
-            xv[g][u][v] = *reinterpret_cast<const float4*>(xs + ((pr + u) * NM_HC + 16 * g + pc + v) * NM_LD + 4 * c4);
+          for (int ph = 0; ph < 2; ++ph)
 #pragma unroll
-      for (int cc = 0; cc < 4; ++cc) {
-        const float* wr = wl + (co * NM_CH + 4 * c4 + cc) * 16;
-        float wt[16];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float4 t4 = *reinterpret_cast<const float4*>(wr + 4 * q);
-          wt[4 * q] = t4.x; wt[4 * q + 1] = t4.y; wt[4 * q + 2] = t4.z; wt[4 * q + 3] = t4.w;
+            for (int pw = 0; pw < 2; ++pw)
+              yb[(long long)(2 * gi + ph) * a.ysh + (long long)(2 * gj + pw) * a.ysw] =
+                  act_fwd(acc[g][ph * 2 + pw][i] * wsc + bv, a.act, a.alpha);
         }
-#pragma unroll
-        for (int ph = 0; ph < 2; ++ph)
-#pragma unroll
-          for (int pw = 0; pw < 2; ++pw)
-#pragma unroll
-            for (int th = 0; th < 2; ++th)
-#pragma unroll
-              for (int tw = 0; tw < 2; ++tw) {
-                const int tap = (2 * th + 1 - ph) * 4 + (2 * tw + 1 - pw);
-#pragma unroll
-                for (int g = 0; g < 2; ++g) {
-                  const float4 xq = xv[g][ph - th + 1][pw - tw + 1];
-                  const float xa = cc == 0 ? xq.x : cc == 1 ? xq.y : cc == 2 ? xq.z : xq.w;
-                  acc[g][ph * 2 + pw] = __builtin_amdgcn_mfma_f32_4x4x1f32(xa, wt[tap], acc[g][ph * 2 + pw], 0, 0, 0);
-                }
-              }
-      }
     }
   }
-  if (co >= NC) return;
-  const float wsc = a.wscale ? a.wscale[0] : 1.f;
-  const float bv = a.bias ? a.bias[co] : 0.f;
-  float* yb = a.y + (long long)b * a.ysb + (long long)co * a.ysc;
-  const int blk = lane >> 2;  // this lane holds pixels 4 blk + i of each group, channel co
-#pragma unroll
-  for (int g = 0; g < 2; ++g)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = 4 * blk + i;  // pixel index within the group (lane order)
-      const int gi = r0 + 4 * wid + (q >> 4), gj = c0p + 16 * g + (q & 15);
-      if (gi >= a.H || gj >= a.W) continue;
-#pragma unroll
-      for (int ph = 0; ph < 2; ++ph)
-#pragma unroll
-        for (int pw = 0; pw < 2; ++pw)
-          yb[(long long)(2 * gi + ph) * a.ysh + (long long)(2 * gj + pw) * a.ysw] =
-              act_fwd(acc[g][ph * 2 + pw][i] * wsc + bv, a.act, a.alpha);
-    }
 }
 
-// packed narrow-ConvT weights [4][C][16]: out[co][ci][kh*4+kw] = W[ci * s_in + co * s_out + kh * 4 + kw]
-// (rows co >= NC are zero: the MFMA's fourth column)
+// packed narrow-ConvT weights in MFMA B-operand lane order, [C][4][64]: register r of input
+// channel ci holds, in lane l, W[ci][co = l % 4][tap = 4 r + l / 16] (co >= NC: 0, the
+// MFMA's fourth column) -- lane group l / 16 is one tap, selected by the MFMA's BLGP
+// broadcast (convt2_narrow_mfma)
 __global__ void pack_narrow(const float* __restrict__ W, float* __restrict__ out, int C, int NC, long long s_in,
                             long long s_out) {
   const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= 4 * C * 16) return;
-  const int t = e & 15, ci = (e >> 4) % C, co = e / (16 * C);
+  if (e >= C * 256) return;
+  const int l = e & 63, r = (e >> 6) & 3, ci = e >> 8, co = l & 3, t = 4 * r + (l >> 4);
   out[e] = co < NC ? W[ci * s_in + co * s_out + t] : 0.f;
 }
 
@@ -1942,7 +1991,7 @@ static bool plan_narrow_t(Plan& p, int batch, const float* x, const long long* x
   a.Ho = 2 * H; a.Wo = 2 * W; a.Cout = nc; a.stride = 2; a.pad = 1;
   a.bias = bias; a.wscale = wscale; a.act = act; a.alpha = alpha;
   p.pack = true;
-  p.pack_floats = (size_t)4 * C * 16;
+  p.pack_floats = (size_t)C * 256;
   p.pn_s_in = s_in; p.pn_s_out = s_out;
   p.pk.W = w;
   return true;
@@ -1953,20 +2002,18 @@ static bool plan_narrow_in(Plan& p, const RganConv* d, const float* x, const flo
                            const float* bias, float* y, int act, float alpha) {
   if (d->transposed || d->cin > 4 || d->kh != 4 || d->kw != 4) return false;
   p.mode = MODE_NARROW_IN;
-  // the windowed kernel (conv_img_in): k4 s2 p1 halving, 128-channel tiles, NHWC output,
-  // 128-pixel tiles that are 128-wide row segments or 128 / Wo whole rows
-  const int wt = std::min(d->wout, 128);
-  p.img_in = !getenv_flag("RGAN_NO_IMG_IN") && d->stride == 2 && d->pad == 1 && d->hout * 2 == d->hin &&
-             d->wout * 2 == d->win && d->cout % 128 == 0 && vec_nhwc(y, d->ys, d->cout) &&
-             ((long long)d->hout * d->wout) % 128 == 0 && (wt == 16 || wt == 32 || wt == 64 || wt == 128) &&
-             d->wout % wt == 0 && ((long long)d->batch * d->hout * d->wout / 128) < (1LL << 31);
+  // the wave-tiled kernel (conv_img_in): k4 s2 p1 halving of an image with <= 3 channels,
+  // 128-channel tiles, NHWC output, 32-pixel wave tiles (row segments or two 16-wide rows),
+  // 16-B window pieces (input rows contiguous and 16-B aligned)
   const long long xext = 4 * (1 + (d->batch - 1) * d->xs[0] + (d->cin - 1) * d->xs[1] + (d->hin - 1) * d->xs[2] +
                               (d->win - 1) * d->xs[3]);
   const long long yext = 4 * (1 + (d->batch - 1) * d->ys[0] + (d->cout - 1) * d->ys[1] + (d->hout - 1) * d->ys[2] +
                               (d->wout - 1) * d->ys[3]);
-  const long long ximg = 4 * (1 + (d->cin - 1) * d->xs[1] + (d->hin - 1) * d->xs[2] + (d->win - 1) * d->xs[3]);
-  p.img_in = p.img_in && d->xs[0] >= 0 && d->xs[1] >= 0 && d->xs[2] >= 0 && d->xs[3] >= 0 && xext < (1LL << 31) &&
-             yext < (1LL << 31) && ximg < (1LL << 25);
+  p.img_in = !getenv_flag("RGAN_NO_IMG_IN") && d->stride == 2 && d->pad == 1 && d->hout * 2 == d->hin &&
+             d->wout * 2 == d->win && d->cin <= 3 && d->cout % 128 == 0 && vec_nhwc(y, d->ys, d->cout) &&
+             (d->wout == 16 || d->wout % 32 == 0) && ((long long)d->batch * d->hout * d->wout / 32) < (1LL << 31) &&
+             d->xs[3] == 1 && d->xs[0] % 4 == 0 && d->xs[1] % 4 == 0 && d->xs[2] % 4 == 0 && d->xs[0] >= 0 &&
+             d->xs[1] >= 0 && d->xs[2] >= 0 && ((uintptr_t)x & 15) == 0 && xext < (1LL << 31) && yext < (1LL << 31);
   NarrowArgs& a = p.na;
   a.x = x; a.xsb = d->xs[0]; a.xsc = d->xs[1]; a.xsh = d->xs[2]; a.xsw = d->xs[3];
   a.B = d->batch; a.H = d->hin; a.W = d->win; a.C = d->cin;
@@ -2263,14 +2310,14 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
     g_kernel_names[47] = "void rgan::dense1_fwd<VEC>(rgan::DenseArgs)";
     g_kernel_names[48] = "void rgan::dense1_dgrad<VEC>(rgan::DenseArgs, rgan::FastDiv)";
     g_kernel_names[49] = "rgan::dense1_wgrad(rgan::DenseArgs)";
-    g_kernel_names[50] = "void rgan::conv_img_in<CI, WT>(rgan::NarrowArgs)";
+    g_kernel_names[50] = "void rgan::conv_img_in<CI, WT, ACT>(rgan::NarrowArgs)";
   }
   return id;
 }
 
 static void launch_pack_plan(Plan& p, float* out, hipStream_t s) {
   if (p.mode == MODE_NARROW_T) {
-    const int n = 4 * p.na.C * 16;
+    const int n = p.na.C * 256;
     pack_narrow<<<ceil_div(n, 256), 256, 0, s>>>(p.pk.W, out, p.na.C, p.na.Cout, p.pn_s_in, p.pn_s_out);
   } else {
     p.pk.out = out;
@@ -2282,31 +2329,35 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
   NarrowArgs a = p.na;
   if (p.mode == MODE_NARROW_T) {
     a.w = packed;
-    const int blocks = a.B * ceil_div(a.H, NM_TR) * ceil_div(a.W, NM_TC);
+    const int ntiles = a.B * ceil_div(a.H, NM_TR) * ceil_div(a.W, NM_TC);
+    const int blocks = std::min(ntiles, 512);  // persistent: two resident blocks per CU
     switch (a.Cout) {
-      case 1: convt2_narrow_mfma<1><<<blocks, 256, 0, s>>>(a); break;
-      case 2: convt2_narrow_mfma<2><<<blocks, 256, 0, s>>>(a); break;
-      case 3: convt2_narrow_mfma<3><<<blocks, 256, 0, s>>>(a); break;
-      default: convt2_narrow_mfma<4><<<blocks, 256, 0, s>>>(a); break;
+      case 1: convt2_narrow_mfma<1><<<blocks, 256, 0, s>>>(a, ntiles); break;
+      case 2: convt2_narrow_mfma<2><<<blocks, 256, 0, s>>>(a, ntiles); break;
+      case 3: convt2_narrow_mfma<3><<<blocks, 256, 0, s>>>(a, ntiles); break;
+      default: convt2_narrow_mfma<4><<<blocks, 256, 0, s>>>(a, ntiles); break;
     }
   } else if (p.img_in) {
-    // persistent: two resident blocks per CU loop over the 128-pixel tiles
-    const int tiles = a.B * a.Ho * a.Wo / 128;
-    const dim3 grid(std::min(tiles, 512), a.Cout / 128);
-#define RGAN_IMG(CC)                                                          \
-  switch (std::min(a.Wo, 128)) {                                              \
-    case 16: conv_img_in<CC, 16><<<grid, 256, 0, s>>>(a, tiles); break;       \
-    case 32: conv_img_in<CC, 32><<<grid, 256, 0, s>>>(a, tiles); break;       \
-    case 64: conv_img_in<CC, 64><<<grid, 256, 0, s>>>(a, tiles); break;       \
-    default: conv_img_in<CC, 128><<<grid, 256, 0, s>>>(a, tiles); break;      \
+    // persistent waves (two resident blocks of 4 per CU) loop over the 32-pixel wave tiles
+    const int tiles = a.B * a.Ho * a.Wo / 32;
+    const dim3 grid(std::min(ceil_div(tiles, 4), 512), a.Cout / 128);
+    const int act_kind = a.act == RGAN_ACT_NONE ? 0
+                         : (a.act == RGAN_ACT_RELU || (a.act == RGAN_ACT_LRELU && a.alpha <= 1.f)) ? 1 : 2;
+#define RGAN_IMG_A(CC, WW)                                                            \
+  switch (act_kind) {                                                                 \
+    case 0: conv_img_in<CC, WW, 0><<<grid, 256, 0, s>>>(a, tiles); break;             \
+    case 1: conv_img_in<CC, WW, 1><<<grid, 256, 0, s>>>(a, tiles); break;             \
+    default: conv_img_in<CC, WW, 2><<<grid, 256, 0, s>>>(a, tiles); break;            \
   }
+#define RGAN_IMG(CC)                                                          \
+  if (a.Wo == 16) RGAN_IMG_A(CC, 16) else RGAN_IMG_A(CC, 32)
     switch (a.C) {
       case 1: RGAN_IMG(1) break;
       case 2: RGAN_IMG(2) break;
-      case 3: RGAN_IMG(3) break;
-      default: RGAN_IMG(4) break;
+      default: RGAN_IMG(3) break;
     }
 #undef RGAN_IMG
+#undef RGAN_IMG_A
   } else {
     // persistent: two resident blocks per CU loop over the M tiles
     dim3 grid(std::min(ceil_div(a.B * a.Ho * a.Wo, 128), 512), ceil_div(a.Cout, 128));
