@@ -283,10 +283,10 @@ size_t rgan_spectral_ws_bytes(int rows, int cols);
 int rgan_spectral_power(const float* W, int rows, int cols, long long rs, long long hs, int lo,
                         float eps, float* u, float* v, float* inv_sigma, int do_iter,
                         void* ws, void* stream);
-/* All spectral layers of one net call in TWO launches (instead of four per layer):
+/* All spectral layers of one net call in FOUR launches (instead of four per layer):
  * each layer gets one power iteration exactly as rgan_spectral_power(do_iter=1).
- * n <= 16 layers; counters: 16 device uints, zero-initialised once and left zeroed by
- * every call; ws: rgan_spectral_batch_ws_bytes(n, layers). */
+ * n <= 16 layers; counters: unused, may be NULL (kept in the signature); ws:
+ * rgan_spectral_batch_ws_bytes(n, layers). */
 typedef struct RganSnLayer {
   const float* W;
   int rows, cols, lo;
@@ -301,7 +301,7 @@ typedef struct RganSnLayer {
 size_t rgan_spectral_batch_ws_bytes(int n, const RganSnLayer* layers);
 int rgan_spectral_power_batch(int n, const RganSnLayer* layers, float eps, void* ws, unsigned* counters,
                               void* stream);
-/* dW_orig = dW_eff/sigma - (<dW_eff, W_orig>/sigma^2) u v^T (u, v constants); ws >= 1 KiB. */
+/* dW_orig = dW_eff/sigma - (<dW_eff, W_orig>/sigma^2) u v^T (u, v constants); ws >= 2 KiB. */
 int rgan_spectral_backward(const float* W, const float* dWeff, int rows, int cols,
                            long long rs, long long hs, int lo, const float* u, const float* v,
                            const float* inv_sigma, float* dW, int accumulate, void* ws, void* stream);

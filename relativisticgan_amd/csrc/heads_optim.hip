@@ -423,15 +423,22 @@ extern "C" int rgan_spectral_power(const float* W, int rows, int cols, long long
   return 0;
 }
 
-// ---- all of a net's spectral layers in two launches (one power iteration each) ----
-// Phase V: blocks over (layer, 64-column chunk); 4 waves split the rows, lanes take
-// consecutive columns (coalesced rows of W), t[c] = sum_r W(r,c) u[r] complete per block;
-// the layer's last block (a counter, reset by that block) sums the per-block squares in
-// block order and writes v = t / max(||t||, eps).
-// Phase U: blocks over (layer, 4-row chunk), a wave per row: w[r] = sum_c W(r,c) v[c];
-// the layer's last block: u = w / max(||w||, eps), sigma = u . w, inv_sigma = 1/sigma.
-// Both phases are deterministic (fixed-order sums; only the completion counter is atomic).
+// ---- all of a net's spectral layers in four launches (one power iteration each) ----
+// W is read once for t = W^T u and once for w = W v: 2 x sizeof(W) of HBM traffic.  When W
+// is not cache-resident (a training step), HBM latency bounds any dependent sequence of row
+// loads, so every phase issues all of a thread's row loads at once over many blocks:
+//   V1: blocks over (layer, 1024-column chunk, 16-row chunk): a thread's 4 columns summed
+//       over the chunk's 16 rows (16 float4 loads in flight) -> row-chunk partials;
+//   V2: blocks over (layer, 256 columns): t = sum of the partials (row-chunk order), and
+//       per-block sums of t^2;
+//   U:  blocks over (layer, row), the block's threads splitting the row: w = (W t) / ||t||
+//       (8 float4 loads in flight per thread); every block forms ||t|| from the V2 partials
+//       (same fixed order) and writes its slice of v = t / max(||t||, eps);
+//   fin: a block per layer writes u = w / max(||w||, eps) and 1/sigma, sigma = u . w.
+// All sums are in a fixed order (deterministic); no atomics, no cross-block hand-off.
 constexpr int SNB_MAX = 16;
+constexpr int SNB_CC = 1024;           // columns per V1 block
+constexpr int SNB_RC = 16;             // rows per V1 block
 struct SnBatch {
   SnView w[SNB_MAX];
   float* u[SNB_MAX];
@@ -439,10 +446,13 @@ struct SnBatch {
   float* u2[SNB_MAX];       // nullable second copies (the autograd-saved u, v of this call)
   float* v2[SNB_MAX];
   float* inv_sigma[SNB_MAX];
-  float* t[SNB_MAX];        // workspace: [cols] (phase V) / [rows] (phase U)
-  float* part[SNB_MAX];     // workspace: per-block squares
-  int first[SNB_MAX + 1];   // block prefix per layer
-  unsigned* counter;        // [SNB_MAX] zero-initialised, reset by each layer's last block
+  float* t[SNB_MAX];        // workspace: [cols] t, then [rows] w
+  float* part[SNB_MAX];     // workspace: V1 [nrc][cols] row-chunk partials
+  float* sq[SNB_MAX];       // workspace: V2 per-block sums of t^2 [nt]
+  float* wv[SNB_MAX];       // workspace: [rows] w
+  int vec[SNB_MAX];         // 16-B contiguous 4-column runs
+  int ncc[SNB_MAX], nrc[SNB_MAX], nt[SNB_MAX];
+  int first[SNB_MAX + 1];   // block prefix per layer (of the launch this struct is for)
   int n;
   float eps;
 };
@@ -451,30 +461,6 @@ __device__ __forceinline__ int snb_layer(const SnBatch& b, int blk) {
   int l = 0;
   while (l + 1 < b.n && blk >= b.first[l + 1]) ++l;
   return l;
-}
-
-// The layer's last block to finish, with every other block's plain global writes visible
-// to it (the in-launch split-K hand-off of cdna_hip_programming.md: per-wave vmcnt drain,
-// barrier, ONE agent-scope release by lane 0, ticket via a relaxed agent-scope vector
-// atomic; the last arriver resets the ticket and takes ONE agent-scope acquire).  Blocks may
-// sit on different XCDs (private L2s): plain stores + a fence-free counter would be stale.
-__device__ __forceinline__ bool snb_last(unsigned* counter, int nblocks) {
-  __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned done = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = done == (unsigned)(nblocks - 1) ? 1 : 0;
-    if (last) {
-      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  return last != 0;
 }
 
 // fixed-order sum of n per-block partials by wave 0 with lane-indexed (vector) loads; the
@@ -489,153 +475,297 @@ __device__ __forceinline__ float snb_sum_parts(const float* part, int n) {
 }
 
 __global__ __launch_bounds__(256) void sn_batch_v(SnBatch b) {
-  __shared__ float red[4][64];
   const int l = snb_layer(b, blockIdx.x), blk = blockIdx.x - b.first[l];
   const SnView& w = b.w[l];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int c = blk * 64 + lane;
-  float s = 0.f;
+  const int ncc = b.ncc[l];
+  const int cc = blk % ncc, rc = blk / ncc;
+  const int tid = threadIdx.x;
+  const int r0 = rc * SNB_RC, r1 = min(w.rows, r0 + SNB_RC);
+  const float* u = b.u[l];
+  float* part = b.part[l] + (size_t)rc * w.cols;
+  const int c0 = cc * SNB_CC;
+  float ur[SNB_RC];
+#pragma unroll
+  for (int q = 0; q < SNB_RC; ++q) ur[q] = r0 + q < r1 ? u[r0 + q] : 0.f;
+  if (b.vec[l]) {
+    const int c = c0 + 4 * tid;
+    if (c >= w.cols) return;
+    const float* wc = w.W + w.off(0, c) + (long long)r0 * w.rs;
+    float4 x[SNB_RC];
+#pragma unroll
+    for (int q = 0; q < SNB_RC; ++q)
+      x[q] = r0 + q < r1 ? *reinterpret_cast<const float4*>(wc + (long long)q * w.rs) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll
+    for (int q = 0; q < SNB_RC; ++q) {
+      a0 += x[q].x * ur[q]; a1 += x[q].y * ur[q]; a2 += x[q].z * ur[q]; a3 += x[q].w * ur[q];
+    }
+    *reinterpret_cast<float4*>(part + c) = make_float4(a0, a1, a2, a3);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int c = c0 + tid + 256 * k;
+      if (c >= w.cols) continue;
+      float x[SNB_RC];
+#pragma unroll
+      for (int q = 0; q < SNB_RC; ++q) x[q] = r0 + q < r1 ? w.W[w.off(r0 + q, c)] : 0.f;
+      float a = 0.f;
+#pragma unroll
+      for (int q = 0; q < SNB_RC; ++q) a += x[q] * ur[q];
+      part[c] = a;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void sn_batch_t(SnBatch b) {
+  __shared__ float red[16];
+  const int l = snb_layer(b, blockIdx.x), blk = blockIdx.x - b.first[l];
+  const SnView& w = b.w[l];
+  const int c = blk * 256 + threadIdx.x, nrc = b.nrc[l];
+  float t = 0.f;
   if (c < w.cols) {
-    const float* u = b.u[l];
-    for (int r = wid; r < w.rows; r += 4) s += w.W[w.off(r, c)] * u[r];
+    const float* part = b.part[l] + c;
+    int q = 0;
+    for (; q + 16 <= nrc; q += 16) {  // 16 loads in flight, summed in row-chunk order
+      float x[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) x[k] = part[(size_t)(q + k) * w.cols];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) t += x[k];
+    }
+    for (; q < nrc; ++q) t += part[(size_t)q * w.cols];
+    b.t[l][c] = t;
   }
-  red[wid][lane] = s;
-  __syncthreads();
-  if (wid == 0) {
-    const float t = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    if (c < w.cols) b.t[l][c] = t;
-    const float sq = wave_sum(c < w.cols ? t * t : 0.f);
-    if (lane == 0) b.part[l][blk] = sq;
-  }
-  const int nblk = b.first[l + 1] - b.first[l];
-  if (!snb_last(b.counter + l, nblk)) return;
-  __shared__ float den;
-  const float a = snb_sum_parts(b.part[l], nblk);
-  if (threadIdx.x == 0) den = fmaxf(sqrtf(a), b.eps);
-  __syncthreads();
-  float* v2 = b.v2[l];
-  for (int i = threadIdx.x; i < w.cols; i += blockDim.x) {
-    const float x = b.t[l][i] / den;
-    b.v[l][i] = x;
-    if (v2) v2[i] = x;
-  }
+  const float s2 = block_sum(c < w.cols ? t * t : 0.f, red);
+  if (threadIdx.x == 0) b.sq[l][blk] = s2;
 }
 
 __global__ __launch_bounds__(256) void sn_batch_u(SnBatch b) {
   __shared__ float red[16];
-  const int l = snb_layer(b, blockIdx.x), blk = blockIdx.x - b.first[l];
+  __shared__ float den_s;
+  const int l = snb_layer(b, blockIdx.x), row = blockIdx.x - b.first[l];
+  const int nblk = b.first[l + 1] - b.first[l];  // = rows: a block per row
   const SnView& w = b.w[l];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int row = blk * 4 + wid;
-  float s = 0.f;
-  if (row < w.rows) {
-    const float* v = b.v[l];
-    for (int c = lane; c < w.cols; c += 64) s += w.W[w.off(row, c)] * v[c];
-  }
-  s = wave_sum(s);
-  if (lane == 0) red[wid] = row < w.rows ? s : 0.f;
+  const int tid = threadIdx.x;
+  const float* t = b.t[l];
+  // ||t|| from V2's per-block sums (the same fixed order in every block)
+  const float tsq = snb_sum_parts(b.sq[l], b.nt[l]);
+  if (tid == 0) den_s = fmaxf(sqrtf(tsq), b.eps);
   __syncthreads();
-  if (threadIdx.x < 4) {  // lane-indexed stores
-    const int i = threadIdx.x;
-    if (blk * 4 + i < w.rows) b.t[l][blk * 4 + i] = red[i];
-    if (i == 0) b.part[l][blk] = red[0] * red[0] + red[1] * red[1] + red[2] * red[2] + red[3] * red[3];
+  const float den = den_s;
+  // this block's slice of v = t / max(||t||, eps)
+  {
+    const int per = (w.cols + nblk - 1) / nblk, c0 = row * per, c1 = min(w.cols, c0 + per);
+    float* v2 = b.v2[l];
+    for (int c = c0 + tid; c < c1; c += blockDim.x) {
+      const float x = t[c] / den;
+      b.v[l][c] = x;
+      if (v2) v2[c] = x;
+    }
   }
-  const int nblk = b.first[l + 1] - b.first[l];
-  if (!snb_last(b.counter + l, nblk)) return;
-  __shared__ float den;
-  const float a = snb_sum_parts(b.part[l], nblk);
-  if (threadIdx.x == 0) den = fmaxf(sqrtf(a), b.eps);
+  // w[row] = (W t)[row] / ||t||: the block's 256 threads split the row, 8 float4 in flight each
+  float s = 0.f;
+  if (b.vec[l] && w.lo < w.cols && w.lo == 16) {
+    // dim-1 (ConvTranspose) view: runs of 16 contiguous columns at row * rs + ch * hs
+    const float* wr = w.W + (long long)row * w.rs;
+    const int nq = w.cols / 4;  // float4 quarters of runs
+    for (int e0 = 0; e0 < nq; e0 += 2048) {
+      float4 x[8], y[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = e0 + tid + 256 * k;
+        const bool ok = e < nq;
+        x[k] = ok ? *reinterpret_cast<const float4*>(wr + (long long)(e >> 2) * w.hs + 4 * (e & 3)) : make_float4(0.f, 0.f, 0.f, 0.f);
+        y[k] = ok ? *reinterpret_cast<const float4*>(t + 4 * e) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += x[k].x * y[k].x + x[k].y * y[k].y + x[k].z * y[k].z + x[k].w * y[k].w;
+    }
+  } else if (b.vec[l] && w.lo >= w.cols) {
+    // dim-0 view: the row is one contiguous run
+    const float* wr = w.W + (long long)row * w.rs;
+    for (int c0 = 0; c0 < w.cols; c0 += 8 * 1024) {
+      float4 x[8], y[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = c0 + 4 * tid + 1024 * k;
+        const bool ok = c < w.cols;
+        x[k] = ok ? *reinterpret_cast<const float4*>(wr + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+        y[k] = ok ? *reinterpret_cast<const float4*>(t + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += x[k].x * y[k].x + x[k].y * y[k].y + x[k].z * y[k].z + x[k].w * y[k].w;
+    }
+  } else {
+    for (int c = tid; c < w.cols; c += 256) s += w.W[w.off(row, c)] * t[c];
+  }
+  s = block_sum(s, red) / den;  // (W t) / ||t|| = W v
+  if (tid == 0) b.wv[l][row] = s;
+}
+
+// one block per layer: u = w / max(||w||, eps), sigma = u . w (fixed-order sums).  A launch
+// of its own: a completion counter in sn_batch_u would cost every one of its (row) blocks
+// an agent-scope release, which measured slower than the whole phase.
+__global__ __launch_bounds__(256) void sn_batch_fin(SnBatch b) {
+  __shared__ float red[16];
+  __shared__ float wden;
+  const int l = blockIdx.x, tid = threadIdx.x;
+  const SnView& w = b.w[l];
+  float q = 0.f;
+  for (int r = tid; r < w.rows; r += blockDim.x) q += b.wv[l][r] * b.wv[l][r];
+  q = block_sum(q, red);
+  if (tid == 0) wden = fmaxf(sqrtf(q), b.eps);
   __syncthreads();
   float d = 0.f;
   float* u2 = b.u2[l];
-  for (int r = threadIdx.x; r < w.rows; r += blockDim.x) {
-    const float wr = b.t[l][r], ur = wr / den;
+  for (int r = tid; r < w.rows; r += blockDim.x) {
+    const float wr = b.wv[l][r], ur = wr / wden;
     b.u[l][r] = ur;
     if (u2) u2[r] = ur;
     d += ur * wr;
   }
   d = block_sum(d, red);
-  if (threadIdx.x == 0) b.inv_sigma[l][0] = 1.f / d;
+  if (tid == 0) b.inv_sigma[l][0] = 1.f / d;
+}
+
+struct SnGeom {
+  int ncc, nrc, nt, nu;
+  size_t floats;
+};
+static SnGeom snb_geom(const RganSnLayer& L) {
+  SnGeom g;
+  g.ncc = ceil_div(L.cols, SNB_CC);
+  g.nrc = ceil_div(L.rows, SNB_RC);
+  g.nt = ceil_div(L.cols, 256);
+  g.nu = L.rows;  // U: a block per row
+  auto al = [](size_t f) { return (f + 63) / 64 * 64; };  // 256-B aligned pieces (float4 partials)
+  g.floats = al(L.cols) + al((size_t)g.nrc * L.cols) + al(g.nt) + al(L.rows);
+  return g;
 }
 
 extern "C" size_t rgan_spectral_batch_ws_bytes(int n, const RganSnLayer* layers) {
   if (n <= 0 || n > SNB_MAX || !layers) return 0;
   size_t f = 0;
-  for (int i = 0; i < n; ++i) {
-    const int cols = layers[i].cols, rows = layers[i].rows;
-    f += (size_t)std::max(cols, rows) + (size_t)std::max(ceil_div(cols, 64), ceil_div(rows, 4)) + 64;
-  }
+  for (int i = 0; i < n; ++i) f += snb_geom(layers[i]).floats;
   return f * sizeof(float) + 256;
 }
 
 extern "C" int rgan_spectral_power_batch(int n, const RganSnLayer* layers, float eps, void* ws, unsigned* counters,
                                          void* stream) {
-  RGAN_REQUIRE(n > 0 && n <= SNB_MAX && layers && ws && counters);
-  SnBatch bv{}, bu{};
-  float* p = (float*)ws;
-  int nv = 0, nu = 0;
+  RGAN_REQUIRE(n > 0 && n <= SNB_MAX && layers && ws);
+  (void)counters;  // no cross-block hand-off any more (kept in the signature)
+  SnBatch bv{}, bt{}, bu{};
+  float* p = (float*)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
+  int nv = 0, nt = 0, nu = 0;
   for (int i = 0; i < n; ++i) {
     const RganSnLayer& L = layers[i];
     RGAN_REQUIRE(L.W && L.u && L.v && L.inv_sigma && L.rows > 0 && L.cols > 0 && L.lo > 0);
+    const SnGeom g = snb_geom(L);
     const SnView w{L.W, L.rows, L.cols, L.lo, L.rs, L.hs};
-    const int cv = ceil_div(L.cols, 64), cu = ceil_div(L.rows, 4);
+    auto al = [](size_t f) { return (f + 63) / 64 * 64; };
     float* t = p;
-    float* part = t + std::max(L.cols, L.rows);
-    p = part + std::max(cv, cu) + 64;
-    for (SnBatch* b : {&bv, &bu}) {
+    float* part = t + al(L.cols);
+    float* sq = part + al((size_t)g.nrc * L.cols);
+    float* wv = sq + al(g.nt);
+    p += g.floats;
+    const int vec = L.lo % 4 == 0 && L.rs % 4 == 0 && L.hs % 4 == 0 && L.cols % 4 == 0 && ((uintptr_t)L.W & 15) == 0;
+    for (SnBatch* b : {&bv, &bt, &bu}) {
       b->w[i] = w; b->u[i] = L.u; b->v[i] = L.v; b->inv_sigma[i] = L.inv_sigma; b->t[i] = t; b->part[i] = part;
-      b->u2[i] = L.u_copy; b->v2[i] = L.v_copy;
+      b->sq[i] = sq; b->wv[i] = wv; b->u2[i] = L.u_copy; b->v2[i] = L.v_copy; b->vec[i] = vec;
+      b->ncc[i] = g.ncc; b->nrc[i] = g.nrc; b->nt[i] = g.nt;
     }
-    bv.first[i] = nv; nv += cv;
-    bu.first[i] = nu; nu += cu;
+    bv.first[i] = nv; nv += g.ncc * g.nrc;
+    bt.first[i] = nt; nt += g.nt;
+    bu.first[i] = nu; nu += g.nu;
   }
-  bv.first[n] = nv; bu.first[n] = nu;
-  bv.n = bu.n = n; bv.eps = bu.eps = eps; bv.counter = bu.counter = counters;
+  bv.first[n] = nv; bt.first[n] = nt; bu.first[n] = nu;
+  for (SnBatch* b : {&bv, &bt, &bu}) { b->n = n; b->eps = eps; }
   hipStream_t s = (hipStream_t)stream;
   sn_batch_v<<<nv, 256, 0, s>>>(bv);
   RGAN_CHECK_LAUNCH();
+  sn_batch_t<<<nt, 256, 0, s>>>(bt);
+  RGAN_CHECK_LAUNCH();
   sn_batch_u<<<nu, 256, 0, s>>>(bu);
+  RGAN_CHECK_LAUNCH();
+  sn_batch_fin<<<n, 256, 0, s>>>(bu);
   RGAN_CHECK_LAUNCH();
   return 0;
 }
 
-// <dWeff, W> over the view, per-block partials then one block reduces
-__global__ __launch_bounds__(256) void sn_dot_kernel(SnView w, const float* __restrict__ dWe,
-                                                     float* __restrict__ part) {
+// <dWeff, W>: the view enumerates every element once, so this is the flat dot product of the
+// two (same-layout) tensors: float4 grid-stride per-block partials, summed in block order
+// by the backward kernel.
+constexpr int SN_DOT_PARTS = 512;
+__global__ __launch_bounds__(256) void sn_dot_kernel(const float* __restrict__ a, const float* __restrict__ w,
+                                                     long long n, float* __restrict__ part) {
   __shared__ float red[16];
-  const long long total = (long long)w.rows * w.cols;
   float s = 0.f;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int r = (int)(i / w.cols), c = (int)(i - (long long)r * w.cols);
-    const long long o = w.off(r, c);
-    s += dWe[o] * w.W[o];
+  const long long n4 = ((((uintptr_t)a | (uintptr_t)w) & 15) == 0) ? n / 4 : 0;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    const float4 x = reinterpret_cast<const float4*>(a)[i], y = reinterpret_cast<const float4*>(w)[i];
+    s += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
   }
+  for (long long i = 4 * n4 + blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) s += a[i] * w[i];
   s = block_sum(s, red);
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
+// dW (+)= dWe / sigma - (<dWe, W> / sigma^2) u[r] v[c]: a block per view row r (u[r]
+// uniform), its columns in 4-column runs (float4 when the runs are 16-B contiguous)
 __global__ __launch_bounds__(256) void sn_bwd_kernel(SnView w, const float* __restrict__ dWe,
                                                      const float* __restrict__ part, int nparts,
                                                      const float* __restrict__ u, const float* __restrict__ v,
                                                      const float* __restrict__ inv_sigma, float* __restrict__ dW,
-                                                     int accum) {
+                                                     int accum, int vec) {
+  __shared__ float red[16];
   __shared__ float kk;
-  if (threadIdx.x == 0) {
-    float d = 0.f;
-    for (int i = 0; i < nparts; ++i) d += part[i];
-    const float is = inv_sigma[0];
-    kk = d * is * is;
-  }
+  float d = 0.f;
+  if (threadIdx.x < 64)
+    for (int i = threadIdx.x; i < nparts; i += 64) d += part[i];
+  d = threadIdx.x < 64 ? wave_sum(d) : 0.f;
+  (void)red;
+  const float is = inv_sigma[0];
+  if (threadIdx.x == 0) kk = d * is * is;
   __syncthreads();
-  const float is = inv_sigma[0], k = kk;
-  const long long total = (long long)w.rows * w.cols;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int r = (int)(i / w.cols), c = (int)(i - (long long)r * w.cols);
-    const long long o = w.off(r, c);
-    const float g = dWe[o] * is - k * u[r] * v[c];
-    dW[o] = accum ? dW[o] + g : g;
+  const float k = kk;
+  const int r = blockIdx.x;
+  const float ku = k * u[r];
+  const bool flat = w.lo >= w.cols;
+  auto at = [&](int c) { return flat ? (long long)r * w.rs + c : w.off(r, c); };
+  if (vec && !flat && w.lo == 16) {
+    // dim-1 (ConvTranspose) view: a thread takes 4-column quarters of 16-column runs
+    const float* wd = dWe + (long long)r * w.rs;
+    float* od = dW + (long long)r * w.rs;
+    for (int e = threadIdx.x; e < w.cols / 4; e += 256) {
+      const int ch = e >> 2, c = 4 * e;
+      const long long o = (long long)ch * w.hs + 4 * (e & 3);
+      const float4 g = *reinterpret_cast<const float4*>(wd + o);
+      const float4 vv = *reinterpret_cast<const float4*>(v + c);
+      float4 y = make_float4(g.x * is - ku * vv.x, g.y * is - ku * vv.y, g.z * is - ku * vv.z, g.w * is - ku * vv.w);
+      if (accum) {
+        const float4 o4 = *reinterpret_cast<const float4*>(od + o);
+        y.x += o4.x; y.y += o4.y; y.z += o4.z; y.w += o4.w;
+      }
+      *reinterpret_cast<float4*>(od + o) = y;
+    }
+  } else if (vec) {
+    for (int c = 4 * threadIdx.x; c < w.cols; c += 1024) {
+      const long long o = at(c);
+      const float4 g = *reinterpret_cast<const float4*>(dWe + o);
+      const float4 vv = *reinterpret_cast<const float4*>(v + c);
+      float4 y = make_float4(g.x * is - ku * vv.x, g.y * is - ku * vv.y, g.z * is - ku * vv.z, g.w * is - ku * vv.w);
+      if (accum) {
+        const float4 o4 = *reinterpret_cast<const float4*>(dW + o);
+        y.x += o4.x; y.y += o4.y; y.z += o4.z; y.w += o4.w;
+      }
+      *reinterpret_cast<float4*>(dW + o) = y;
+    }
+  } else {
+    for (int c = threadIdx.x; c < w.cols; c += 256) {
+      const long long o = at(c);
+      const float g = dWe[o] * is - ku * v[c];
+      dW[o] = accum ? dW[o] + g : g;
+    }
   }
 }
 
@@ -646,11 +776,13 @@ extern "C" int rgan_spectral_backward(const float* W, const float* dWeff, int ro
   hipStream_t s = (hipStream_t)stream;
   SnView w{W, rows, cols, lo, rs, hs};
   const long long total = (long long)rows * cols;
-  const int nparts = (int)std::min<long long>(256, (total + 255) / 256);
+  const int nparts = (int)std::min<long long>(SN_DOT_PARTS, (total + 1023) / 1024);
   float* part = (float*)ws;
-  sn_dot_kernel<<<nparts, 256, 0, s>>>(w, dWeff, part);
+  sn_dot_kernel<<<nparts, 256, 0, s>>>(dWeff, W, total, part);
   RGAN_CHECK_LAUNCH();
-  sn_bwd_kernel<<<grid1(total), 256, 0, s>>>(w, dWeff, part, nparts, u, v, inv_sigma, dW, accumulate);
+  const int vec = lo % 4 == 0 && rs % 4 == 0 && hs % 4 == 0 && cols % 4 == 0 &&
+                  (((uintptr_t)dWeff | (uintptr_t)dW | (uintptr_t)v) & 15) == 0;
+  sn_bwd_kernel<<<rows, 256, 0, s>>>(w, dWeff, part, nparts, u, v, inv_sigma, dW, accumulate, vec);
   RGAN_CHECK_LAUNCH();
   return 0;
 }

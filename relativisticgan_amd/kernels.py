@@ -678,7 +678,7 @@ _SN_COUNTERS = {}
 
 
 def spectral_power_batch(layers, eps=1e-12):
-    """One power iteration for every (w, u, v, transposed) of a net call, in two launches
+    """One power iteration for every (w, u, v, transposed) of a net call, in four launches
     (rgan_spectral_power_batch): u, v updated in place; returns [(u_copy, v_copy, inv_sigma)]
     per layer (the copies autograd saves, as torch spectral_norm's clones)."""
     n = len(layers)

@@ -202,7 +202,7 @@ class _Net(nn.Module):
         return type(self).__name__[1]  # "G" / "D": activation-trace tag (parity tests)
 
     def _spectral(self):
-        """One power iteration for every spectral layer of this call, all in two launches
+        """One power iteration for every spectral layer of this call, all in four launches
         (torch's spectral_norm pre-hook runs one per layer per train-mode call,
         spectral_norm.py:97-116; u and v of different layers are independent)."""
         idx = [li for li, l in enumerate(self._plan) if l.spec is not None and l.spec.spectral]

@@ -7,7 +7,8 @@ inputs and keeps its shard).  fp32, different summation orders: outputs / losses
 gradients rel-L2 <= TOL (1e-4, the oracle-parity tolerance: the
 rank split reorders fp32 reductions, and the WGAN-GP double backward amplifies it), parameters after Adam within 2*lr*1.01 with >= 99% of
 elements within 1e-6 (Adam step-1 sign flips).  One GPU box has one GPU, so the
-collectives run over gloo here; on the 8-GPU node the same code runs over RCCL.
+collectives run over gloo here; on the 8-GPU node the same code runs over RCCL, and
+test_dp2_rccl_matches_single_process checks it there (skipped with fewer than 2 GPUs).
 """
 import os
 import socket
@@ -52,12 +53,12 @@ def _capture(t, store):
 N_ITER = {"ralsgan_pac2": 1}
 
 
-def _run(name, world, rank, n_iter=None):
+def _run(name, world, rank, n_iter=None, device="cuda:0"):
     n_iter = n_iter or N_ITER.get(name, 2)
     from relativisticgan_amd.train import Trainer
     p = param_for(name)
     p.rgan_rng = "host"
-    t = Trainer(p, dataset_for(name).to("cuda:0"))
+    t = Trainer(p, dataset_for(name).to(device))
     out = []
     for i in range(n_iter):
         st = {}
@@ -69,21 +70,23 @@ def _run(name, world, rank, n_iter=None):
     return out
 
 
-def _worker(rank, world, port, name, path, sync_bn=True, n_iter=None):
+def _worker(rank, world, port, name, path, sync_bn=True, n_iter=None, backend="gloo"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = rank if backend == "nccl" else 0  # RCCL: one GPU per rank; gloo: both ranks on cuda:0
+    torch.cuda.set_device(dev)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     from relativisticgan_amd import dp
     dp.setup(sync_bn=sync_bn)
     try:
-        res = _run(name, world, rank, n_iter)
+        res = _run(name, world, rank, n_iter, device=f"cuda:{dev}")
         # gather the per-rank D outputs so rank 0 holds the global vectors
         for st in res:
             for k in ("y_pred", "y_pred_fake"):
-                parts = [torch.empty_like(st[k]) for _ in range(world)]
-                dist.all_gather(parts, st[k])
-                st[k] = torch.cat(parts)
+                x = st[k].to(f"cuda:{dev}") if backend == "nccl" else st[k]
+                parts = [torch.empty_like(x) for _ in range(world)]
+                dist.all_gather(parts, x)
+                st[k] = torch.cat(parts).cpu()
         if rank == 0:
             torch.save(res, path)
     finally:
@@ -95,11 +98,11 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-def _spawn(name, sync_bn=True, n_iter=None):
+def _spawn(name, sync_bn=True, n_iter=None, backend="gloo"):
     path = os.path.join(tempfile.mkdtemp(), "dp.pt")
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, path, sync_bn, n_iter)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, path, sync_bn, n_iter, backend)) for r in range(2)]
     for pr in procs:
         pr.start()
     for pr in procs:
@@ -112,6 +115,17 @@ def _spawn(name, sync_bn=True, n_iter=None):
 def test_dp2_matches_single_process(name):
     single = _run(name, 1, 0)
     dpres = _spawn(name)
+    _compare(name, dpres, single)
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL data parallelism needs 2 GPUs")
+@pytest.mark.parametrize("name", ["ralsgan", "wgangp", "rahinge_spectral"])
+def test_dp2_rccl_matches_single_process(name):
+    """The same comparison over RCCL with one GPU per rank: the code paths only nccl takes
+    (all_gather_into_tensor, the bucketed async all-reduce on the second communicator, the
+    deferred G step overlapping the next D forward).  Skipped on a 1-GPU box."""
+    single = _run(name, 1, 0)
+    dpres = _spawn(name, backend="nccl")
     _compare(name, dpres, single)
 
 

@@ -560,11 +560,14 @@ def test_gather(K):
 
 def test_spectral_power_batch(K):
     """All spectral layers of a call in two launches == one power iteration per layer
-    (torch spectral_norm, fp64 reference), incl. ConvT (dim 1) and the rows = 1 end layer;
-    the completion counters are left at zero for the next call."""
+    (torch spectral_norm, fp64 reference), incl. ConvT (dim 1), the rows = 1 end layer, a
+    non-float4 view and multi-chunk layers (cols > 1024, rows > 64); the completion counters
+    are left at zero for the next call."""
     torch.manual_seed(9)
     specs = [(torch.nn.Conv2d(3, 16, 4, 2, 1, bias=False), False), (torch.nn.Conv2d(16, 300, 4, 2, 1, bias=False), False),
-             (torch.nn.ConvTranspose2d(64, 24, 4, 2, 1, bias=False), True), (torch.nn.Conv2d(300, 1, 4, 1, 0, bias=False), False)]
+             (torch.nn.ConvTranspose2d(64, 24, 4, 2, 1, bias=False), True), (torch.nn.Conv2d(300, 1, 4, 1, 0, bias=False), False),
+             # scalar path (3-column rows, 2 row chunks) and the C5 D's largest layer (8 x 17 blocks)
+             (torch.nn.Conv2d(3, 70, 1, bias=False), False), (torch.nn.Conv2d(512, 1024, 4, 2, 1, bias=False), False)]
     layers, refs = [], []
     for conv, tr in specs:
         sn = torch.nn.utils.spectral_norm(conv)
