@@ -175,24 +175,64 @@ def run_workload(name, steps, warmup, world, args, K):
     t = Trainer(p, images)
     flops_iter = conv_flops_per_iteration(t)
 
-    for i in range(warmup):
-        t.iteration(i + 1)
-    t.flush()
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+    # graph mode runs every iteration on one side stream: autograd's per-parameter
+    # AccumulateGrad nodes keep the stream of the first backward, and the captured backward
+    # must accumulate on the capturing stream
+    side = torch.cuda.Stream() if use_graph else torch.cuda.current_stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for i in range(warmup):
+            t.iteration(i + 1)
+        t.flush()
+    torch.cuda.current_stream().wait_stream(side)
 
     def barrier():
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
 
-    barrier()
-    K.profile_begin(capacity=400 * steps + 64)
-    t0 = time.perf_counter()
-    for i in range(steps):
-        t.iteration(warmup + 1 + i)
-    t.flush()  # the last G step (deferred under DP) is inside the timed region
-    barrier()
-    elapsed = time.perf_counter() - t0
-    prof = K.profile_end()
+    it = warmup + 1
+    if use_graph:
+        # One iteration captured as a HIP graph and replayed: the same kernels, launches and
+        # state updates (Adam's device step counter, the device RNG's philox offsets), without
+        # the ~10-20 us of Python + ctypes per launch that leaves a small model's step
+        # launch-bound.
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=side):
+            t.iteration(it)
+        it += 1
+        graph.replay()  # one untimed replay
+        barrier()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            graph.replay()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        # per-kernel HIP events cannot be read out of graph replays: the kernel statistics
+        # of the roofline come from eager iterations of the same step, right after
+        nprof = max(3, min(steps, 10))
+        K.profile_begin(capacity=400 * nprof + 64)
+        with torch.cuda.stream(side):
+            for i in range(nprof):
+                t.iteration(it + i)
+            t.flush()
+        torch.cuda.current_stream().wait_stream(side)
+        barrier()
+        prof = K.profile_end()
+        prof["steps"] = nprof
+        del graph
+    else:
+        barrier()
+        K.profile_begin(capacity=400 * steps + 64)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            t.iteration(it + i)
+        t.flush()  # the last G step (deferred under DP) is inside the timed region
+        barrier()
+        elapsed = time.perf_counter() - t0
+        prof = K.profile_end()
+        prof["steps"] = steps
     if world > 1:
         e = torch.tensor([elapsed], device="cuda")
         torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
@@ -200,7 +240,7 @@ def run_workload(name, steps, warmup, world, args, K):
     res = {"name": name, "loss_D": loss_D, "size": size, "bpg": bpg, "h": h, "spectral": spectral,
            "arch": ARCH.get(name, 0), "batch_D": t.batch_D, "elapsed": elapsed, "steps": steps,
            "value": bpg * world * steps / elapsed, "ms_per_step": 1000.0 * elapsed / steps,
-           "flops_iter": flops_iter, "prof": prof}
+           "flops_iter": flops_iter, "prof": prof, "graph": use_graph}
     del t, images
     torch.cuda.empty_cache()
     return res
@@ -209,7 +249,7 @@ def run_workload(name, steps, warmup, world, args, K):
 def roofline_of(res, workload):
     """Dominant kernel = the conv kernel symbol with the most time (HIP events around each
     launch on its stream); the whole conv family is reported beside it."""
-    prof, steps = res["prof"], res["steps"]
+    prof, steps = res["prof"], res["prof"]["steps"]
     gemm_ms, gemm_flops = prof["ms"], prof["flops"]
     top = max(prof["kernels"], key=lambda k: k["ms"])
     achieved = top["flops"] / (top["ms"] / 1000.0)
@@ -243,6 +283,8 @@ def main():
     ap.add_argument("--batch-d", default="auto", choices=("auto", "on", "off"),
                     help="D(x), D(x_fake) as one batched pass (auto: on for 1 process, off under DP -- "
                          "'off' at N=1 is the like-for-like baseline of the N>1 runs)")
+    ap.add_argument("--graph", default="auto", choices=("auto", "on", "off"),
+                    help="time replays of one iteration captured as a HIP graph (auto: 1 process)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--sync-bn", action="store_true",
@@ -271,7 +313,7 @@ def main():
         for name in [w for w in args.extra.split(",") if w and w != args.workload]:
             r = run_workload(name, args.steps, min(args.warmup, 5), world, args, K)
             extras[name] = {"workload": describe(r), "value": r["value"], "unit": "images/s",
-                            "ms_per_step": r["ms_per_step"], "steps": r["steps"],
+                            "ms_per_step": r["ms_per_step"], "steps": r["steps"], "hip_graph": r["graph"],
                             "step_mfma_util": r["flops_iter"] / (r["ms_per_step"] / 1000.0) / FP32_MFMA_PEAK,
                             "roofline": {k: v for k, v in roofline_of(r, name).items() if k != "conv_family"}}
     if rank != 0:
@@ -284,7 +326,7 @@ def main():
         "config": {"workload": describe(res), "loss_D": res["loss_D"], "image_size": res["size"],
                    "batch_per_gpu": res["bpg"], "global_batch": res["bpg"] * world, "G_h_size": res["h"],
                    "D_h_size": res["h"], "arch": res["arch"], "parallelism": f"dp{world}",
-                   "batched_D_step": res["batch_D"],
+                   "batched_D_step": res["batch_D"], "hip_graph": res["graph"],
                    "batchnorm": "SyncBN" if args.sync_bn else "per-shard (reference DataParallel)"},
         "step_mfma_util": res["flops_iter"] * args.steps / res["elapsed"] / (world * FP32_MFMA_PEAK),
         "conv_tflop_per_step": res["flops_iter"] / 1e12,
