@@ -2,7 +2,7 @@
 # One GPU-box session.  usage: tools/gpu_session.sh TAG [step ...]
 #   tests           pytest -m gpu (parity audit JSON under gpurun_out/TAG/parity)
 #   bench[=W]       bench.py default line (or workload W, no extras) -> TAG/bench[_W].json
-#   prof[=W]        rocprofv3 --kernel-trace --stats of a short bench run -> TAG/prof[_W]/summary.txt
+#   prof[=W]        rocprofv3 --kernel-trace --stats of a short eager bench run -> TAG/prof[_W]/summary.txt
 #   pmc[=W]         FETCH_SIZE / WRITE_SIZE passes -> TAG/pmc[_W]/traffic.json
 #   smoke           __graft_entry__.smoke()
 # Default steps: tests bench prof pmc.  Stops at the first step that faults, aborts,
@@ -26,11 +26,11 @@ for s in $steps; do
       timeout -k 10 500 python -u bench.py $wl > "$out/bench$sfx.json" 2> "$out/bench$sfx.err"
       rc=$?; echo "bench$sfx rc=$rc"; stop $rc bench ;;
     prof*)
-      timeout -k 10 450 tools/profile_bench.sh "$out/prof$sfx" --steps 10 --warmup 3 --no-cpu-baseline \
+      timeout -k 10 450 tools/profile_bench.sh "$out/prof$sfx" --steps 10 --warmup 3 --no-cpu-baseline --graph off \
         --extra= $wl
       rc=$?; echo "prof$sfx rc=$rc"; head -25 "$out/prof$sfx/summary.txt"; stop $rc prof ;;
     pmc*)
-      timeout -k 10 850 tools/pmc_traffic.sh "$out/pmc$sfx" --steps 5 --warmup 2 --no-cpu-baseline \
+      timeout -k 10 850 tools/pmc_traffic.sh "$out/pmc$sfx" --steps 5 --warmup 2 --no-cpu-baseline --graph off \
         --extra= $wl
       rc=$?; echo "pmc$sfx rc=$rc"; stop $rc pmc ;;
     smoke)
