@@ -122,8 +122,8 @@ __device__ __forceinline__ long long col_offset(const OutMap& o, int n) {
 // WGRAD: the gradient rows are pixel-contiguous (offset = p * pixel stride: scalar
 // advance) and the im2col operand reads one tap per block tile (Cin % BN == 0) through
 // a per-tile table of pixel offsets built by one wave into LDS two tiles ahead.
-template <int MODE, int BM, int BN, int WM, int WN, bool AV, bool BV, bool FAST>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
+template <int MODE, int BM, int BN, int WM, int WN, bool AV, bool BV, bool FAST, bool EMU>
+__device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert(TM >= 1 && TN >= 1 && WM * WN == 4, "tile config");
   constexpr bool AK = (MODE == MODE_WGRAD);          // A staged k-major
@@ -147,7 +147,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
   constexpr int B_SZ = KROW ? BN * KROW_LD : BK * B_LD;
   constexpr int STAGE = A_SZ + B_SZ;
   constexpr int EPI_SZ = KROW ? 4 * 64 * 72 : 0;  // vector epilogue staging (4 waves x 64 x 72)
-  __shared__ __attribute__((aligned(16))) float smem[2 * STAGE > EPI_SZ ? 2 * STAGE : EPI_SZ];
+  // EMU: one (single-buffered) stage of six bf16 planes (A hi/mid/lo, B hi/mid/lo), rows of
+  // 32 bf16 = 16 dwords at a 20-dword stride (16 lanes' ds_read_b128 on 16 distinct quads)
+  constexpr int EMU_RS = 20, EMU_PLANE = 128 * EMU_RS;  // dwords
+  constexpr int MAIN_SZ = EMU ? 6 * EMU_PLANE : 2 * STAGE;
+  static_assert(!EMU || (FAST && MODE != MODE_WGRAD && BM == 128 && BN == 128), "bf16x6 path: FAST 128x128 CONV/CONVT2");
+  __shared__ __attribute__((aligned(16))) float smem[MAIN_SZ > EPI_SZ ? MAIN_SZ : EPI_SZ];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = (wid / WN) * (BM / WM), wn = (wid % WN) * (BN / WN);
@@ -604,13 +609,88 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
     __syncthreads();
   }
   if constexpr (FAST && MODE != MODE_WGRAD) set_tap(f_tap);
+  const int l32 = lane & 31, lk = lane >> 5;
+  if constexpr (EMU) {
+    // fp32 GEMM on the bf16 MFMA: every operand is split EXACTLY into three bf16 pieces
+    // (x = hi + mid + lo, 8 significant bits each: hi = x with the low 16 bits cleared,
+    // mid likewise of x - hi, lo = x - hi - mid, exact in bf16), and each product keeps the
+    // six terms down to 2^-16 relative: hh, hm, mh, hl, lh, mm (bf16 x bf16 products are
+    // exact in fp32; the dropped ml, lm, ll terms are <= 2^-23 relative -- one fp32
+    // rounding).  v_mfma_f32_32x32x16_bf16 has 16x the rate of the fp32 MFMA, so 6 of them
+    // are 2.67x fewer MFMA cycles; the split (about 6 VALU per element) overlaps the bf16
+    // MFMAs, which -- unlike fp32 MFMA -- co-execute with VALU.
+    typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+    uint32_t* P = reinterpret_cast<uint32_t*>(smem);  // planes 0-2 A, 3-5 B
+    auto split_store = [&](uint32_t* base, int row, int q, const float* v) {
+      uint32_t h[4], m[4], l[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t xb = __float_as_uint(v[e]);
+        h[e] = xb & 0xffff0000u;
+        const float r1 = v[e] - __uint_as_float(h[e]);
+        m[e] = __float_as_uint(r1) & 0xffff0000u;
+        l[e] = __float_as_uint(r1 - __uint_as_float(m[e]));
+      }
+      const int o = row * EMU_RS + 2 * q;  // k 4q .. 4q+3 = dwords 2q, 2q+1 of the row
+      *reinterpret_cast<uint2*>(base + o) = make_uint2((h[0] >> 16) | h[1], (h[2] >> 16) | h[3]);
+      *reinterpret_cast<uint2*>(base + EMU_PLANE + o) = make_uint2((m[0] >> 16) | m[1], (m[2] >> 16) | m[3]);
+      *reinterpret_cast<uint2*>(base + 2 * EMU_PLANE + o) =
+          make_uint2((l[0] >> 16) | (l[1] & 0xffff0000u), (l[2] >> 16) | (l[3] & 0xffff0000u));
+    };
+    auto store_emu = [&]() {
+      const int q = tid & 7;
+#pragma unroll
+      for (int i = 0; i < AR; ++i) split_store(P, (tid >> 3) + 32 * i, q, ra + 4 * i);
+#pragma unroll
+      for (int i = 0; i < FB_N; ++i) split_store(P + 3 * EMU_PLANE, (tid >> 3) + 32 * i, q, rb + 4 * i);
+    };
+    if (nk > 0) {
+      load_fast(kbeg, 0);
+      store_emu();
+    }
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) load_fast(kbeg + (kt + 1) * BK, 0);  // registers only: in flight during the MFMAs
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {  // two k16 steps per BK = 32 tile; lane half lk takes k 8 lk .. 8 lk + 7
+        bf16x8 af[3][TM], bfr[3][TN];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            af[pl][i] = *reinterpret_cast<const bf16x8*>(P + pl * EMU_PLANE + (wm + 32 * i + l32) * EMU_RS + 8 * t + 4 * lk);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            bfr[pl][j] = *reinterpret_cast<const bf16x8*>(P + (3 + pl) * EMU_PLANE + (wn + 32 * j + l32) * EMU_RS +
+                                                          8 * t + 4 * lk);
+        }
+        // (A first: rows of the product are pixels, columns output channels, as in the fp32 path)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            f32x16 c = acc[i][j];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bfr[2][j], c, 0, 0, 0);  // A hi x B lo
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][i], bfr[0][j], c, 0, 0, 0);  // A lo x B hi
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bfr[1][j], c, 0, 0, 0);  // A mid x B mid
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bfr[1][j], c, 0, 0, 0);  // A hi x B mid
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][i], bfr[0][j], c, 0, 0, 0);  // A mid x B hi
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][i], bfr[0][j], c, 0, 0, 0);  // A hi x B hi
+          }
+      }
+      __syncthreads();  // every wave's reads of this tile are done
+      if (kt + 1 < nk) {
+        store_emu();
+        __syncthreads();
+      }
+    }
+  } else {
   if (nk > 0) {
     if constexpr (FAST) load_fast(kbeg, 0);
     else load_tiles(kbeg);
     store_tiles(0);
   }
   __syncthreads();
-  const int l32 = lane & 31, lk = lane >> 5;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
@@ -718,6 +798,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
     if (kt + 1 < nk) store_tiles(cur ^ 1);
     __syncthreads();
   }
+  }  // EMU / fp32 main loop
 
   // ---------------- epilogue ----------------
   if constexpr (KROW && BM / WM == 64 && BN / WN == 64) {
@@ -862,6 +943,18 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
         put([&](float v) { return act_fwd_curved(v, g.act, g.alpha); });
       }
     }
+}
+
+template <int MODE, int BM, int BN, int WM, int WN, bool AV, bool BV, bool FAST>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
+  gemm_body<MODE, BM, BN, WM, WN, AV, BV, FAST, false>(g);
+}
+
+// Opt-in (RGAN_EMU_BF16X6=1): the FAST 128 x 128 CONV / CONVT2 GEMM with fp32 products
+// emulated on the bf16 MFMA (see gemm_body's EMU path).  Its own symbol, reported as such.
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void gemm_bf16x6(GemmArgs g) {
+  gemm_body<MODE, 128, 128, 2, 2, true, true, true, true>(g);
 }
 
 // Split-K reduce: out = act(sum_sp slab[sp] * wscale + bias), slabs summed in split order
@@ -2252,8 +2345,23 @@ static void launch_cfg(const Plan& p, dim3 grid, hipStream_t s) {
   else gemm_kernel<MODE, BM, BN, WM, WN, false, false, false><<<grid, 256, 0, s>>>(p.g);
 }
 
+// RGAN_EMU_BF16X6=1: FAST 128x128 CONV / CONVT2 GEMMs on the bf16x6 emulation (opt-in)
+static bool emu_bf16x6() {
+  static const bool on = getenv_flag("RGAN_EMU_BF16X6");
+  return on;
+}
+static bool plan_emu(const Plan& p) {
+  return p.fast && p.cfg == CFG_L && (p.mode == MODE_CONV || p.mode == MODE_CONVT2) && emu_bf16x6();
+}
+
 template <int MODE>
 static void launch_mode(const Plan& p, dim3 grid, hipStream_t s) {
+  if constexpr (MODE == MODE_CONV || MODE == MODE_CONVT2) {
+    if (plan_emu(p)) {
+      gemm_bf16x6<MODE><<<grid, 256, 0, s>>>(p.g);
+      return;
+    }
+  }
   switch (p.cfg) {
     case CFG_L: launch_cfg<MODE, 128, 128, 2, 2>(p, grid, s); break;
     case CFG_M: launch_cfg<MODE, 128, 64, 2, 2>(p, grid, s); break;
@@ -2278,7 +2386,7 @@ static std::vector<ProfRec> g_recs;
 static std::vector<std::string> g_kernel_names;
 static double g_cur_flops = 0.0;
 
-constexpr int N_KERNEL_IDS = 51;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in
+constexpr int N_KERNEL_IDS = 53;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in + 2 bf16x6
 
 static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
   const int id = mode == MODE_NARROW_T ? 45
@@ -2311,6 +2419,8 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
     g_kernel_names[48] = "void rgan::dense1_dgrad<VEC>(rgan::DenseArgs, rgan::FastDiv)";
     g_kernel_names[49] = "rgan::dense1_wgrad(rgan::DenseArgs)";
     g_kernel_names[50] = "void rgan::conv_img_in<CI, WT, ACT>(rgan::NarrowArgs)";
+    g_kernel_names[51] = "void rgan::gemm_bf16x6<0>(rgan::GemmArgs)";
+    g_kernel_names[52] = "void rgan::gemm_bf16x6<1>(rgan::GemmArgs)";
   }
   return id;
 }
@@ -2480,6 +2590,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     rec.b = g_pool[g_recs.size() * 2 + 1];
     rec.flops = g_cur_flops;
     rec.kid = kernel_id(p.mode, p.cfg, p.av, p.bv, p.fast);
+    if (plan_emu(p)) rec.kid = 51 + p.mode;
     hipEventRecord(rec.a, s);
   }
   switch (p.mode) {
