@@ -15,6 +15,9 @@ Prints ONE JSON line (rank 0).  Extra fields:
   roofline     -- the dominant kernel (the fp32-MFMA implicit-GEMM conv): algorithmic
                   FLOPs / its HIP-event-timed duration over the timed region, against
                   the fp32 MFMA peak (157.3 TFLOP/s);
+  fp32_emulated_bf16x6 -- (N=1) the same workload again with the forward / data-gradient
+                  conv GEMMs on the bf16x6 fp32 emulation (rgan_set_gemm_emulation): its
+                  throughput and roofline, priced against the bf16 MFMA peak / 6 products;
   cpu_baseline -- the oracle (CPU restatement of the reference step, torch CPU fp32) on
                   a bounded sample of the same workload on this host (rank 0, N=1).
 Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
@@ -32,6 +35,14 @@ sys.path.insert(0, ROOT)
 
 METRIC = "train images/sec (D+G step) RaLSGAN DCGAN 64²/256² at 1/2/4/8 GPU; MFMA util"
 FP32_MFMA_PEAK = 157.3e12  # MI355X_MICROARCH.md: Peak FP32 (matrix) = vector peak
+BF16_MFMA_PEAK = 2.5e15    # MI355X_MICROARCH.md: Peak BF16 MFMA, dense
+EMU_PRODUCTS = 6           # bf16 MFMA products per emulated fp32 product (bf16x6)
+
+
+def kernel_peak(symbol):
+    """fp32-equivalent FLOP/s ceiling of a conv kernel symbol: the fp32 MFMA peak, or for the
+    bf16x6 emulation the dense bf16 MFMA peak shared by its six products."""
+    return BF16_MFMA_PEAK / EMU_PRODUCTS if "bf16x6" in symbol else FP32_MFMA_PEAK
 
 WORKLOADS = {
     # name: (loss_D, image_size, batch per GPU, h)
@@ -160,9 +171,17 @@ def cpu_baseline(loss_D, size, batch, h, spectral, seconds_hint, arch=0):
                       f"torch {torch.__version__} CPU fp32, {threads} threads on {cpus['model']}"}
 
 
-def run_workload(name, steps, warmup, world, args, K):
+def run_workload(name, steps, warmup, world, args, K, emu=False):
     """Train `steps` timed iterations of workload `name` (after `warmup`); returns the
-    measurement (max over ranks)."""
+    measurement (max over ranks).  emu: forward / data-gradient GEMMs on bf16x6."""
+    prev_emu = K.set_gemm_emulation(emu)
+    try:
+        return _run_workload(name, steps, warmup, world, args, K)
+    finally:
+        K.set_gemm_emulation(prev_emu)
+
+
+def _run_workload(name, steps, warmup, world, args, K):
     from relativisticgan_amd.config import make_param
     from relativisticgan_amd.train import Trainer, synthetic_images
     loss_D, size, bpg, h = WORKLOADS[name]
@@ -253,15 +272,18 @@ def roofline_of(res, workload):
     gemm_ms, gemm_flops = prof["ms"], prof["flops"]
     top = max(prof["kernels"], key=lambda k: k["ms"])
     achieved = top["flops"] / (top["ms"] / 1000.0)
+    peak = kernel_peak(top["name"])
     traffic, traffic_src = pmc_traffic(workload, top["name"])
-    return {"bound": "mfma", "achieved": achieved / 1e12, "peak": FP32_MFMA_PEAK / 1e12, "unit": "TFLOP/s",
-            "frac": achieved / FP32_MFMA_PEAK, "traffic": traffic, "traffic_unit": "bytes/launch",
+    # conv family ceiling: each kernel's time at its own peak
+    fam_floor_s = sum(k["flops"] / kernel_peak(k["name"]) for k in prof["kernels"])
+    return {"bound": "mfma", "achieved": achieved / 1e12, "peak": peak / 1e12, "unit": "TFLOP/s",
+            "frac": achieved / peak, "traffic": traffic, "traffic_unit": "bytes/launch",
             "traffic_source": traffic_src, "kernel": top["name"], "launches": top["launches"],
             "avg_launch_us": 1000.0 * top["ms"] / top["launches"],
             "flops_per_launch": top["flops"] / top["launches"],
             "conv_family": {"achieved": gemm_flops / (gemm_ms / 1000.0) / 1e12, "launches": prof["launches"],
                             "ms_per_step": gemm_ms / steps,
-                            "frac": gemm_flops / (gemm_ms / 1000.0) / FP32_MFMA_PEAK,
+                            "frac": fam_floor_s / (gemm_ms / 1000.0),
                             "kernels": prof["kernels"]}}
 
 
@@ -285,6 +307,8 @@ def main():
                          "'off' at N=1 is the like-for-like baseline of the N>1 runs)")
     ap.add_argument("--graph", default="auto", choices=("auto", "on", "off"),
                     help="time replays of one iteration captured as a HIP graph (auto: 1 process)")
+    ap.add_argument("--no-emu-extra", action="store_true",
+                    help="skip the N=1 re-run of the workload with the bf16x6 fp32-emulated GEMMs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--sync-bn", action="store_true",
@@ -308,6 +332,9 @@ def main():
             dist.init_process_group(backend)
         dp.setup(sync_bn=args.sync_bn)
     res = run_workload(args.workload, args.steps, args.warmup, world, args, K)
+    emu_res = None
+    if world == 1 and not args.no_emu_extra:
+        emu_res = run_workload(args.workload, args.steps, min(args.warmup, 5), world, args, K, emu=True)
     extras = {}
     if world == 1:
         for name in [w for w in args.extra.split(",") if w and w != args.workload]:
@@ -334,6 +361,13 @@ def main():
     }
     if extras:
         out["extra_workloads"] = extras
+    if emu_res is not None:
+        out["fp32_emulated_bf16x6"] = {
+            "value": emu_res["value"], "unit": "images/s", "ms_per_step": emu_res["ms_per_step"],
+            "steps": emu_res["steps"], "hip_graph": emu_res["graph"],
+            "gemm_arith": "forward / data-gradient conv GEMMs: fp32 operands split exactly into 3 bf16 "
+                          "pieces, 6 bf16 MFMA products accumulated in fp32 (weight gradients: fp32 MFMA)",
+            "roofline": roofline_of(emu_res, args.workload)}
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(res["loss_D"], res["size"], res["bpg"], res["h"], res["spectral"],
                                            args.cpu_seconds, arch=res["arch"])

@@ -332,6 +332,16 @@ int rgan_profile_begin(int capacity);
 int rgan_profile_end(double* total_ms, double* total_flops, long long* launches);
 int rgan_profile_kernel(int idx, char* name, int name_len, double* ms, double* flops, long long* n);
 
+/* GEMM arithmetic of the FAST 128x128 forward and data-gradient GEMMs (Conv and ConvT; the
+ * weight gradients stay on the fp32 MFMA): 0 = fp32 MFMA (default),
+ * 1 = fp32 emulated on the bf16 MFMA (each operand split exactly into three bf16 pieces,
+ * the six products down to 2^-16 relative accumulated in fp32: per-product error <= 2^-23
+ * relative, the fp32 rounding scale).  Also settable at load by RGAN_EMU_BF16X6=1.  Read
+ * at launch time (a captured graph keeps the kernels it captured).  Returns the previous
+ * setting, or -1 for a value other than 0 / 1.  No reference counterpart (an MI355X
+ * arithmetic option; the reference computes fp32 on the CPU). */
+int rgan_set_gemm_emulation(int on);
+
 /* Library self-description: number of exported compute entry points, version string. */
 const char* rgan_version(void);
 

@@ -23,6 +23,7 @@
 
 #include <string>
 #include <type_traits>
+#include <atomic>
 #include <vector>
 
 namespace rgan {
@@ -650,7 +651,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
     }
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) load_fast(kbeg + (kt + 1) * BK, 0);  // registers only: in flight during the MFMAs
+      // registers only, in flight during the MFMAs.  Unconditional: a guarded load leaves
+      // the compiler a phi of (new, old) registers whose copies wait for the loads right
+      // here.  Past the last tile every offset is in-bounds or OOB (buffer loads return 0).
+      load_fast(kbeg + (kt + 1) * BK, 0);
+      __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMAs (not sunk for VGPRs)
 #pragma unroll
       for (int t = 0; t < 2; ++t) {  // two k16 steps per BK = 32 tile; lane half lk takes k 8 lk .. 8 lk + 7
         bf16x8 af[3][TM], bfr[3][TN];
@@ -2345,10 +2350,17 @@ static void launch_cfg(const Plan& p, dim3 grid, hipStream_t s) {
   else gemm_kernel<MODE, BM, BN, WM, WN, false, false, false><<<grid, 256, 0, s>>>(p.g);
 }
 
-// RGAN_EMU_BF16X6=1: FAST 128x128 CONV / CONVT2 GEMMs on the bf16x6 emulation (opt-in)
+// FAST 128x128 CONV / CONVT2 GEMMs (fwd + dgrad of Conv and ConvT) on the bf16x6 emulation: opt-in, by RGAN_EMU_BF16X6=1 at
+// load or rgan_set_gemm_emulation (read at every launch: a captured graph keeps its kernels)
+static std::atomic<int> g_emu{-1};
 static bool emu_bf16x6() {
-  static const bool on = getenv_flag("RGAN_EMU_BF16X6");
-  return on;
+  int v = g_emu.load(std::memory_order_relaxed);
+  if (v < 0) {
+    int expect = -1;
+    g_emu.compare_exchange_strong(expect, getenv_flag("RGAN_EMU_BF16X6") ? 1 : 0);
+    v = g_emu.load(std::memory_order_relaxed);
+  }
+  return v == 1;
 }
 static bool plan_emu(const Plan& p) {
   return p.fast && p.cfg == CFG_L && (p.mode == MODE_CONV || p.mode == MODE_CONVT2) && emu_bf16x6();
@@ -2779,6 +2791,13 @@ extern "C" int rgan_conv_wgrad(const RganConv* d, const float* x, const float* d
     return rgan_channel_sum(dy, P, d->cout, sp, d->ys[1], dbias, accumulate, (char*)ws + plan_bytes, stream);
   }
   return 0;
+}
+
+extern "C" int rgan_set_gemm_emulation(int on) {
+  if (on != 0 && on != 1) return -1;
+  const int prev = emu_bf16x6() ? 1 : 0;
+  g_emu.store(on, std::memory_order_relaxed);
+  return prev;
 }
 
 extern "C" int rgan_profile_begin(int capacity) {

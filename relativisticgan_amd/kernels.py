@@ -752,6 +752,16 @@ def gather_images(images, idx, out=None):
     return out
 
 
+# ------------------------------------------------------------------ GEMM arithmetic
+def set_gemm_emulation(on):
+    """Run the FAST 128x128 forward / data-gradient conv GEMMs as fp32 emulated on the bf16 MFMA
+    (bf16x6, see include/rgan.h) instead of the fp32 MFMA; returns the previous setting."""
+    prev = L.lib().rgan_set_gemm_emulation(1 if on else 0)
+    if prev < 0:
+        raise L.RganError("rgan_set_gemm_emulation failed")
+    return bool(prev)
+
+
 # ------------------------------------------------------------------ live launch timing
 def profile_begin(capacity=100000):
     L.check(L.lib().rgan_profile_begin(int(capacity)), "rgan_profile_begin")

@@ -325,6 +325,47 @@ def test_conv_c3_full_size(K, case):
     assert _rel(K.conv_wgrad(x, dyk, g, w.shape)[0], wr.grad) < 1e-5
 
 
+EMU_SHAPES = [
+    (32, 2048, 4096, 8, 4, 2, 1, False),   # C3 deepest D conv (K = 32768)
+    (32, 4096, 2048, 4, 4, 2, 1, True),    # C3 deepest G ConvT
+    (32, 256, 512, 64, 4, 2, 1, False),    # C3 mid layer
+    (3, 96, 160, 34, 4, 2, 1, False),      # ragged tiles: fwd M = 867, N = 160; dgrad M = 3468, N = 96
+    (5, 96, 160, 5, 4, 2, 1, True),        # ragged ConvT: 4 phases of M = 125, N = 160; dgrad N = 96
+]
+
+
+@pytest.mark.parametrize("case", EMU_SHAPES)
+def test_conv_bf16x6_emulation(K, case):
+    """fp32 GEMM emulated on the bf16 MFMA (rgan_set_gemm_emulation(1)): forward and data
+    gradient vs torch fp64 at the fp32 path's tolerance (rel L2 <= 1e-5), within 2x of the
+    fp32 MFMA path's own error, and the emulated kernel is the one that ran."""
+    B, cin, cout, H, k, s, p, tr = case
+    g = K.ConvGeom(k, s, p, tr)
+    torch.manual_seed(5)
+    x = _nhwc(torch.randn(B, cin, H, H, device=DEV))
+    w = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k), device=DEV) * 0.02
+    xr = x.detach().double().contiguous().requires_grad_(True)
+    with torch.backends.cudnn.flags(enabled=False):
+        ref = (F.conv_transpose2d if tr else F.conv2d)(xr, w.double(), stride=s, padding=p)
+        dy = torch.randn(ref.shape, device=DEV)
+        ref.backward(dy.double())
+    dyk = _nhwc(dy)
+    y32, dx32 = K.conv_fwd(x, w, g), K.conv_dgrad(dyk, w, g, x.shape, like=x)
+    prev = K.set_gemm_emulation(True)
+    try:
+        K.profile_begin(64)
+        y, dx = K.conv_fwd(x, w, g), K.conv_dgrad(dyk, w, g, x.shape, like=x)
+        names = [kk["name"] for kk in K.profile_end()["kernels"]]
+    finally:
+        K.set_gemm_emulation(prev)
+    assert any("bf16x6" in n for n in names), names
+    for got, fp32, want in ((y, y32, ref.detach()), (dx, dx32, xr.grad)):
+        e = _rel(got, want)
+        assert e < 1e-5
+        assert e < 2 * _rel(fp32, want) + 1e-7
+    assert K.set_gemm_emulation(prev) == prev
+
+
 def _bn_ref(y, gamma, beta, eps=1e-5):
     y64 = y.double().cpu()
     mean = y64.mean((0, 2, 3))

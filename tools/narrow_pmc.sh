@@ -1,6 +1,8 @@
 #!/bin/bash
 # PMC passes over tools/narrow_micro.py (GPU box).  usage: tools/narrow_pmc.sh OUTDIR [lib]
 # (lib: an experiment build from tools/build_variant.py, loaded through RGAN_LIB)
+# PMC_TARGET: the profiled script and its args (default "tools/narrow_micro.py 10"),
+# e.g. PMC_TARGET="tools/gemm_micro.py 10 fwd" for the GEMM kernels
 set -u
 out=$(realpath -m "$1")
 root=$(pwd)
@@ -18,7 +20,7 @@ i=0
 for p in "${passes[@]}"; do
   i=$((i + 1))
   timeout -k 10 120 rocprofv3 --pmc $p --kernel-trace -d "$out/p$i" -o run --output-format csv -- \
-    python3 "$root/tools/narrow_micro.py" 10 > "$out/p$i.log" 2>&1
+    python3 $root/${PMC_TARGET:-tools/narrow_micro.py 10} > "$out/p$i.log" 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   case $rc in 124|137|134|139) exit $rc ;; esac
