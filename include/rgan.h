@@ -73,8 +73,9 @@ int rgan_conv_fwd(const RganConv* d, const float* x, const float* w, const float
 
 /* Conv2d/ConvTranspose2d.forward feeding a train-mode BatchNorm2d (GLI:361-366,387-391,
  * 428-433): y = conv(x, w) * (*wscale) + bias, and -- when the GEMM's vector epilogue
- * covers the layer -- the BatchNorm batch statistics of y as per-64-row segment moments
- * bn_part[S][2][C] = (sum y, sum y^2) in double, computed from the finished tile in LDS (no re-read of y).
+ * or its split-K reduce covers the layer -- the BatchNorm batch statistics of y as per-64-row
+ * segment moments bn_part[S][2][C] = (sum y, sum y^2) in double, computed from the finished
+ * tile in LDS or from the reduced rows in registers (no re-read of y).
  * S = rgan_conv_bn_segments(d, segs) (0: the epilogue cannot, use rgan_bn_stats); `segs`
  * equal batch segments are kept apart (the batched D(x)/D(G(z)) call: segment k's rows are
  * segments [k*S/segs, (k+1)*S/segs)).  *fused (host int) = 1 when bn_part was written.

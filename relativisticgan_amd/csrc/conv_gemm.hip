@@ -1062,6 +1062,81 @@ __global__ __launch_bounds__(256) void splitk_reduce(GemmArgs g, FastDiv fdiv, u
   }
 }
 
+// Split-K reduce of a BatchNorm layer's conv forward with the batch statistics fused in:
+// the same rows the RED_VEC reduce writes (same split order, bitwise the same values), plus
+// the (sum y, sum y^2) of every 64-row segment of every channel in double -- the layout the
+// unsplit vector epilogue writes (bnp[(seg * 2 + {0,1}) * N + n], seg = phase * (M / 64) +
+// m / 64), so one segment merge serves both and the separate moments pass over y (4 B/elem
+// + a launch) is gone.  Block = one 64-row segment x 4*qb columns, thread (rl, q) reduces
+// rows rl and rl + RL (RL = 256 / qb) of quad q -- both rows' split loads in flight together,
+// as many threads as the plain reduce -- then the per-thread double sums are added over rl
+// by a fixed LDS tree (deterministic).  grid = (segments * column chunks, phases).
+constexpr int REDBN_QB = 8;
+
+__global__ __launch_bounds__(256) void splitk_reduce_bn(GemmArgs g, int mode_t2, int qb) {
+  __shared__ double sh[2][256][4];
+  const int phase = blockIdx.y;
+  const int Q = g.N >> 2, chunks = (Q + qb - 1) / qb;
+  const int segm = blockIdx.x / chunks, chunk = blockIdx.x - segm * chunks;
+  const int tid = threadIdx.x, lq = tid % qb, q = chunk * qb + lq, rl = tid / qb, RL = 256 / qb;
+  const size_t MN = (size_t)g.M * g.N;
+  const float* base = g.slab + (size_t)phase * g.splits * MN;
+  const float wsc = g.wscale ? g.wscale[0] : 1.f;
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  if (q < Q) {
+    const int n = 4 * q;
+    const long long noff = col_offset(g.out, n);
+    for (int r0 = rl; r0 < 64; r0 += 2 * RL) {  // RL <= 32: two rows per pass
+      const int m0 = segm * 64 + r0, m1 = m0 + RL;
+      const float* p0 = base + (size_t)m0 * g.N + n;
+      const float* p1 = base + (size_t)m1 * g.N + n;
+      float4 v0 = *reinterpret_cast<const float4*>(p0), v1 = *reinterpret_cast<const float4*>(p1);
+      for (int sp = 1; sp < g.splits; ++sp) {  // split order, as red_sum
+        const float4 a0 = *reinterpret_cast<const float4*>(p0 + (size_t)sp * MN);
+        const float4 a1 = *reinterpret_cast<const float4*>(p1 + (size_t)sp * MN);
+        v0.x += a0.x; v0.y += a0.y; v0.z += a0.z; v0.w += a0.w;
+        v1.x += a1.x; v1.y += a1.y; v1.z += a1.z; v1.w += a1.w;
+      }
+      const float4 o0 = make_float4(red_epi(g, v0.x, wsc, n), red_epi(g, v0.y, wsc, n + 1),
+                                    red_epi(g, v0.z, wsc, n + 2), red_epi(g, v0.w, wsc, n + 3));
+      const float4 o1 = make_float4(red_epi(g, v1.x, wsc, n), red_epi(g, v1.y, wsc, n + 1),
+                                    red_epi(g, v1.z, wsc, n + 2), red_epi(g, v1.w, wsc, n + 3));
+      *reinterpret_cast<float4*>(g.C + row_offset(g.out, m0, mode_t2 ? phase : 0) + noff) = o0;
+      *reinterpret_cast<float4*>(g.C + row_offset(g.out, m1, mode_t2 ? phase : 0) + noff) = o1;
+      const float a[2][4] = {{o0.x, o0.y, o0.z, o0.w}, {o1.x, o1.y, o1.z, o1.w}};
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const double d = (double)a[h][i];
+          s1[i] += d;
+          s2[i] += d * d;
+        }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { sh[0][tid][i] = s1[i]; sh[1][tid][i] = s2[i]; }
+  __syncthreads();
+  for (int h = RL / 2; h > 0; h >>= 1) {  // tid = rl * qb + lq: partner rl + h
+    if (rl < h) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        sh[0][tid][i] += sh[0][tid + h * qb][i];
+        sh[1][tid][i] += sh[1][tid + h * qb][i];
+      }
+    }
+    __syncthreads();
+  }
+  if (rl == 0 && q < Q) {
+    const size_t seg = (size_t)phase * (uint32_t)(g.M >> 6) + (uint32_t)segm;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      g.bnp[(seg * 2) * g.N + 4 * q + i] = sh[0][tid][i];
+      g.bnp[(seg * 2 + 1) * g.N + 4 * q + i] = sh[1][tid][i];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- one-output dense layer
 // D's closing Conv2d(C, 1, k, 1, 0) over a k x k map (GLI:455, GLI:306) covers the whole
 // map: per sample a dot product of C*k*k inputs with the single filter.  As an implicit GEMM
@@ -2525,6 +2600,26 @@ static bool bn_epilogue_ok(const Plan& p) {
   return true;
 }
 
+// The split-K reduce can emit the same segment moments (splitk_reduce_bn): channel-contiguous
+// float4 output rows (the RED_VEC shape), n = channel, 64-row segments as above.
+static bool red_vec_ok(const Plan& p, bool check_ptr) {
+  const GemmArgs& g = p.g;
+  const OutMap& o = g.out;
+  auto al4 = [](long long v) { return (v & 3) == 0; };
+  return p.mode != MODE_WGRAD && o.tc == 1 && o.fnc.d % 4 == 0 && g.N % 4 == 0 && al4(o.th) && al4(o.tw) &&
+         al4(o.sb) && al4(o.sh) && al4(o.sw) && (!check_ptr || aligned16(g.C));
+}
+
+static bool bn_reduce_ok(const Plan& p, bool check_ptr) {
+  const GemmArgs& g = p.g;
+  static const bool off = getenv_flag("RGAN_NO_REDUCE_BN");  // A/B switch
+  if (off || (p.mode != MODE_CONV && p.mode != MODE_CONVT2)) return false;
+  if (g.splits <= 1 || p.tap_stage || g.accum || !red_vec_ok(p, check_ptr) || g.N < 4 * REDBN_QB) return false;
+  if (g.out.fnc.d != (uint32_t)g.N || g.M % 64 != 0 || p.bn_segs < 1) return false;
+  if (p.bn_segs > 1 && (p.phases != 1 || g.M % p.bn_segs != 0 || (g.M / p.bn_segs) % 64 != 0)) return false;
+  return true;
+}
+
 static long long bn_epilogue_segments(const Plan& p) { return (long long)p.phases * (p.g.M / 64); }
 
 static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
@@ -2586,7 +2681,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     p.g.vec_out = p.mode != MODE_WGRAD && o.tc == 1 && o.fnc.d % 4 == 0 && p.g.N % 4 == 0 && al4(o.th) &&
                   al4(o.tw) && al4(o.sb) && al4(o.sh) && al4(o.sw) && aligned16(p.g.C);
   }
-  p.bn_fused = p.bn_part && bn_epilogue_ok(p);
+  p.bn_fused = p.bn_part && (bn_epilogue_ok(p) || bn_reduce_ok(p, true));
   p.g.bnp = p.bn_fused ? p.bn_part : nullptr;
   int bm, bn;
   tile_dims(p.cfg, bm, bn);
@@ -2637,6 +2732,15 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
       kind = RED_TAPS;
       per /= 4;
       d = o.fnc.d;
+    }
+    if (p.bn_fused) {  // bn_reduce_ok: the RED_VEC shape with segment moments
+      const int Q = g.N / 4;
+      int qb = 1;  // quads per block: 8 (32 channels, 128-B row pieces), fewer for narrow N
+      while (qb * 2 <= std::min(Q, REDBN_QB)) qb *= 2;
+      const dim3 bgrid((unsigned)((g.M / 64) * ceil_div(Q, qb)), p.phases);
+      splitk_reduce_bn<<<bgrid, 256, 0, s>>>(g, p.mode == MODE_CONVT2, qb);
+      RGAN_CHECK_LAUNCH();
+      return 0;
     }
     const dim3 rgrid((unsigned)std::min<uint32_t>((per + 255) / 256, 8192), p.phases);
     const FastDiv fd(d);
@@ -2726,7 +2830,7 @@ extern "C" long long rgan_conv_bn_segments(const RganConv* d, int segs) {
   p.g.vec_out = o.tc == 1 && o.fnc.d % 4 == 0 && p.g.N % 4 == 0 && al4(o.th) && al4(o.tw) && al4(o.sb) &&
                 al4(o.sh) && al4(o.sw);
   p.bn_segs = segs;
-  return bn_epilogue_ok(p) ? bn_epilogue_segments(p) : 0;
+  return (bn_epilogue_ok(p) || bn_reduce_ok(p, false)) ? bn_epilogue_segments(p) : 0;
 }
 
 extern "C" int rgan_conv_fwd_bn(const RganConv* d, const float* x, const float* w, const float* wpacked,

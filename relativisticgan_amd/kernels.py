@@ -263,7 +263,8 @@ BN_EPILOGUE = os.environ.get("RGAN_BN_EPILOGUE", "1") != "0"
 def conv_fwd_bn(x, w, geom, bias=None, wscale=None, cache=False, segs=1):
     """y = conv(x, w)*wscale + bias (NHWC) for a layer followed by train-mode BatchNorm.
 
-    Returns (y, part, S): when the GEMM's vector epilogue covered the layer, ``part`` is
+    Returns (y, part, S): when the GEMM's vector epilogue or its split-K reduce covered the
+    layer, ``part`` is
     its per-64-row segment sums (sum y, sum y^2) double[S][2][C] (merge with bn_segment_stats; batch
     segment k = segments [k*S/segs, (k+1)*S/segs)); otherwise (y, None, 0)."""
     if geom.upsample != 1 or not BN_EPILOGUE:

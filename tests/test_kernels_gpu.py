@@ -416,16 +416,21 @@ def test_batchnorm_train(K, shape, act):
     assert _rel(db, b64.grad) < 2e-5
 
 
-# conv feeding BatchNorm: (B, cin, cout, H, transposed, segs) -- FAST 128x128 layers whose
-# vector epilogue emits the BN segment moments (D conv, G k4s2 ConvT = 4 phases, batched
-# D halves), plus shapes that must fall back (split-K deep layer, ragged M, narrow N)
+# conv feeding BatchNorm: (B, cin, cout, H, transposed, segs, fused) -- FAST 128x128 layers
+# whose vector epilogue emits the BN segment moments (D conv, G k4s2 ConvT = 4 phases,
+# batched D halves), split-K layers whose reduce emits them (splitk_reduce_bn: deep D
+# layer, narrow N, 4-phase ConvT, batched halves, N = 1024 in 4 column chunks), and a
+# ragged M that must fall back to the moments pass
 BN_EPI = [
-    (16, 32, 128, 128, False, 1),    # >= 512 output tiles: no split-K
-    (32, 32, 128, 128, False, 2),
-    (16, 128, 128, 32, True, 1),
-    (4, 256, 128, 16, False, 1),     # M = 256 rows: split-K -> fallback
-    (3, 64, 128, 10, False, 1),      # M = 75: not a multiple of 64 -> fallback
-    (8, 64, 32, 32, False, 1),       # N = 32: narrow tile -> fallback
+    (16, 32, 128, 128, False, 1, True),    # >= 512 output tiles: no split-K
+    (32, 32, 128, 128, False, 2, True),
+    (16, 128, 128, 32, True, 1, True),
+    (4, 256, 128, 16, False, 1, True),     # M = 256 rows: split-K reduce
+    (8, 256, 128, 16, False, 2, True),     # split-K, two batch segments
+    (4, 256, 128, 8, True, 1, True),       # split-K ConvT, 4 phases
+    (4, 64, 1024, 8, False, 1, True),      # split-K, N = 1024
+    (3, 64, 128, 10, False, 1, False),     # M = 75: not a multiple of 64 -> fallback
+    (8, 64, 32, 32, False, 1, True),       # N = 32: narrow tile
 ]
 
 
@@ -433,13 +438,12 @@ BN_EPI = [
 def test_conv_bn_epilogue_stats(K, case):
     """rgan_conv_fwd_bn + rgan_bn_segment_stats == rgan_conv_fwd + rgan_bn_stats (fp64 torch)."""
     from relativisticgan_amd.kernels import ConvGeom
-    B, cin, cout, H, tr, segs = case
+    B, cin, cout, H, tr, segs, expect_fused = case
     torch.manual_seed(11)
     g = ConvGeom(4, 2, 1, tr)
     x = _nhwc(torch.randn(B, cin, H, H, device=DEV))
     w = torch.randn((cin, cout, 4, 4) if tr else (cout, cin, 4, 4), device=DEV) * 0.05 + 0.01
     y, part, S = K.conv_fwd_bn(x, w, g, segs=segs)
-    expect_fused = case[:4] not in {(4, 256, 128, 16), (3, 64, 128, 10), (8, 64, 32, 32)}
     assert (part is not None) == expect_fused
     y_ref = K.conv_fwd(x, w, g)
     assert torch.equal(y, y_ref)  # the epilogue statistics do not touch the stored output
