@@ -796,37 +796,88 @@ struct AdamTensor {
   long long n;
 };
 constexpr int ADAM_CHUNK = 48;
+// Work split in proportion to size: tensor j owns blocks [first[j], first[j+1]) of a 1-D
+// grid, ADAM_BLOCK_ELEMS elements per block (16 per thread: 4 float4 of each of p, g, m, v
+// in flight).  A block-per-(chunk, tensor) 2-D grid sized by the largest tensor left most
+// blocks of the small tensors idle and gave the big ones 1 scalar element per load.
+constexpr int ADAM_BLOCK_ELEMS = 4096;
 struct AdamBatch {
   AdamTensor t[ADAM_CHUNK];
+  int first[ADAM_CHUNK + 1];
+  int cnt;
 };
 
 __global__ void adam_step_inc(float* step) { step[0] += 1.f; }
 
+struct AdamConst {
+  float neg_step, bc2s, w, fb2, f1mb2, feps, fwd;
+  bool has_wd;
+};
+
+__device__ __forceinline__ void adam_elem(const AdamConst& k, float g, float& p, float& m, float& v) {
+  if (k.has_wd) g = g + k.fwd * p;
+  const float diff = g - m;
+  m = k.w < 0.5f ? m + k.w * diff : g - diff * (1.f - k.w);
+  v = v * k.fb2;
+  v = v + k.f1mb2 * g * g;
+  const float denom = sqrtf(v) / k.bc2s + k.feps;
+  p = p + k.neg_step * (m / denom);
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(AdamBatch b, const double* __restrict__ hyper,
                                                    const float* __restrict__ step) {
-  const AdamTensor T = b.t[blockIdx.y];
+  int j = 0;
+  while (j + 1 < b.cnt && (int)blockIdx.x >= b.first[j + 1]) ++j;
+  const AdamTensor T = b.t[j];
   const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
   const double st = (double)step[0];
   const double bc1 = 1.0 - pow(b1, st), bc2 = 1.0 - pow(b2, st);
-  const float neg_step = (float)(-(lr / bc1));
-  const float bc2s = (float)sqrt(bc2);
-  const float w = (float)(1.0 - b1);
-  const float fb2 = (float)b2, f1mb2 = (float)(1.0 - b2), feps = (float)eps, fwd = (float)wd;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < T.n;
-       i += (long long)gridDim.x * blockDim.x) {
-    float g = T.g[i];
-    float p = T.p[i];
-    if (wd != 0.0) g = g + fwd * p;
-    float m = T.m[i];
-    const float diff = g - m;
-    m = w < 0.5f ? m + w * diff : g - diff * (1.f - w);
-    float v = T.v[i] * fb2;
-    v = v + f1mb2 * g * g;
-    const float denom = sqrtf(v) / bc2s + feps;
-    p = p + neg_step * (m / denom);
-    T.m[i] = m;
-    T.v[i] = v;
-    T.p[i] = p;
+  AdamConst k;
+  k.neg_step = (float)(-(lr / bc1));
+  k.bc2s = (float)sqrt(bc2);
+  k.w = (float)(1.0 - b1);
+  k.fb2 = (float)b2;
+  k.f1mb2 = (float)(1.0 - b2);
+  k.feps = (float)eps;
+  k.fwd = (float)wd;
+  k.has_wd = wd != 0.0;
+  const long long e0 = (long long)((int)blockIdx.x - b.first[j]) * ADAM_BLOCK_ELEMS;
+  const long long e1 = min(T.n, e0 + ADAM_BLOCK_ELEMS);
+  const bool vec = (T.n & 3) == 0 && ((((uintptr_t)T.p | (uintptr_t)T.g | (uintptr_t)T.m | (uintptr_t)T.v) & 15) == 0);
+  if (vec) {
+    constexpr int U = ADAM_BLOCK_ELEMS / 1024;  // float4 per thread
+    float4 P[U], G[U], M[U], V[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = e0 + 4 * (threadIdx.x + 256 * u);
+      if (i < e1) {
+        P[u] = *reinterpret_cast<const float4*>(T.p + i);
+        G[u] = *reinterpret_cast<const float4*>(T.g + i);
+        M[u] = *reinterpret_cast<const float4*>(T.m + i);
+        V[u] = *reinterpret_cast<const float4*>(T.v + i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = e0 + 4 * (threadIdx.x + 256 * u);
+      if (i < e1) {
+        adam_elem(k, G[u].x, P[u].x, M[u].x, V[u].x);
+        adam_elem(k, G[u].y, P[u].y, M[u].y, V[u].y);
+        adam_elem(k, G[u].z, P[u].z, M[u].z, V[u].z);
+        adam_elem(k, G[u].w, P[u].w, M[u].w, V[u].w);
+        *reinterpret_cast<float4*>(T.m + i) = M[u];
+        *reinterpret_cast<float4*>(T.v + i) = V[u];
+        *reinterpret_cast<float4*>(T.p + i) = P[u];
+      }
+    }
+  } else {
+    for (long long i = e0 + threadIdx.x; i < e1; i += 256) {
+      float p = T.p[i], m = T.m[i], v = T.v[i];
+      adam_elem(k, T.g[i], p, m, v);
+      T.m[i] = m;
+      T.v[i] = v;
+      T.p[i] = p;
+    }
   }
 }
 
@@ -840,15 +891,19 @@ extern "C" int rgan_adam(int ntensors, float* const* params, const float* const*
   for (int base = 0; base < ntensors; base += ADAM_CHUNK) {
     const int cnt = std::min(ADAM_CHUNK, ntensors - base);
     AdamBatch b{};
-    long long maxn = 1;
+    b.cnt = cnt;
+    long long blocks = 0;
     for (int i = 0; i < cnt; ++i) {
       const int j = base + i;
       RGAN_REQUIRE(params[j] && grads[j] && exp_avg[j] && exp_avg_sq[j] && numel[j] >= 0);
       b.t[i] = AdamTensor{params[j], grads[j], exp_avg[j], exp_avg_sq[j], numel[j]};
-      maxn = std::max(maxn, numel[j]);
+      b.first[i] = (int)blocks;
+      blocks += (numel[j] + ADAM_BLOCK_ELEMS - 1) / ADAM_BLOCK_ELEMS;
+      RGAN_REQUIRE(blocks < (1LL << 30));
     }
-    const int bx = (int)std::max<long long>(1, std::min<long long>((maxn + 1023) / 1024, 2048));
-    adam_kernel<<<dim3(bx, cnt), 256, 0, s>>>(b, hyper, step);
+    b.first[cnt] = (int)blocks;
+    if (blocks == 0) continue;
+    adam_kernel<<<(unsigned)blocks, 256, 0, s>>>(b, hyper, step);
     RGAN_CHECK_LAUNCH();
   }
   return 0;

@@ -1,0 +1,56 @@
+"""bench.py's driver contract on the GPU box: the N=1 JSON line, and the N>1 path (torchrun,
+one process per rank, max-over-ranks timing) rehearsed with 2 gloo ranks on the one GPU
+(RGAN_BENCH_BACKEND=gloo: RCCL refuses two ranks on one device).  Small workload (C1),
+few steps: this checks the code path and the line's keys, not the numbers."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config", "roofline"}
+
+
+def _line(out):
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+def _env():
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return env
+
+
+def test_bench_one_gpu_line():
+    r = subprocess.run([sys.executable, "bench.py", "--workload", "C1", "--extra=", "--no-emu-extra",
+                        "--no-cpu-baseline", "--steps", "3", "--warmup", "1"], cwd=ROOT, env=_env(),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 1 and d["steps"] == 3 and d["value"] > 0 and d["dtype"] == "fp32"
+    assert d["config"]["parallelism"] == "dp1" and d["config"]["global_batch"] == 32
+    rf = d["roofline"]
+    assert rf["bound"] == "mfma" and 0 < rf["frac"] < 1 and rf["peak"] == 157.3
+
+
+def test_bench_two_rank_rehearsal():
+    env = _env()
+    env["RGAN_BENCH_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29613", "bench.py", "--gpus", "2",
+                        "--workload", "C1", "--extra=", "--steps", "2", "--warmup", "1"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)  # rank 0 only prints
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 64
+    assert d["config"]["batched_D_step"] is False and d["config"]["hip_graph"] is False
+    assert "cpu_baseline" not in d and d["value"] > 0
