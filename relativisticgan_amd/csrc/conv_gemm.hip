@@ -1342,6 +1342,8 @@ struct NarrowArgs {
   int act;
   float alpha;
   int x_bytes, y_bytes;   // conv_img_in: byte extents of x and y (< 2^31, buffer descriptors)
+  int splits = 1, cps = 0;  // convt2_narrow_mfma: input-channel splits (cps channels each, a multiple of 16)
+  float* slab = nullptr;  // ... their raw sums [split][b][co][oh][ow] when splits > 1 (narrow_split_reduce)
 };
 
 // Conv2d with a 4x4 kernel and CI <= 4 input channels (D's image layer, GLI:410) as ONE MFMA
@@ -1781,23 +1783,34 @@ __global__ __launch_bounds__(256, 2) void convt2_narrow_mfma(NarrowArgs a, int n
     r0 = tr * NM_TR;
     c0p = (trem - tr * tiles_c) * NM_TC;
   };
-  int t = blockIdx.x;
-  if (t >= ntiles) return;
+  // work item = (tile, input-channel split): item = tile * splits + split.  Small grids
+  // (G's 32 x 32 -> 64 x 64 image layer: 64 tiles) split the channel sum over blocks so the
+  // chip is filled; the raw partial sums then go to a slab reduced in split order.
+  const int items = ntiles * a.splits;
+  auto item_of = [&](int it, int& t, int& cb, int& ce) {
+    t = it / a.splits;
+    cb = (it - t * a.splits) * a.cps;
+    ce = min(a.C, cb + a.cps);
+  };
+  int it = blockIdx.x;
+  if (it >= items) return;
   {
-    int b, r0, c0p;
+    int t, cb, ce, b, r0, c0p;
+    item_of(it, t, cb, ce);
     tile_of(t, b, r0, c0p);
-    load_chunk(a.x + (long long)b * a.xsb, r0, c0p, 0);
+    load_chunk(a.x + (long long)b * a.xsb, r0, c0p, cb);
   }
-  for (; t < ntiles; t += gridDim.x) {
-    int b, r0, c0p;
+  for (; it < items; it += gridDim.x) {
+    int t, cb, ce, b, r0, c0p;
+    item_of(it, t, cb, ce);
     tile_of(t, b, r0, c0p);
     f32x4 acc[2][4];
 #pragma unroll
     for (int g = 0; g < 2; ++g)
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc[g][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int ch0 = 0; ch0 < a.C; ch0 += NM_CH) {
-      const int nch = min(NM_CH, a.C - ch0);
+    for (int ch0 = cb; ch0 < ce; ch0 += NM_CH) {
+      const int nch = min(NM_CH, ce - ch0);
       __syncthreads();  // previous chunk's (or tile's) LDS reads are done
 #pragma unroll
       for (int q = 0; q < NM_XPT; ++q) {
@@ -1808,12 +1821,13 @@ __global__ __launch_bounds__(256, 2) void convt2_narrow_mfma(NarrowArgs a, int n
       for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(wl + 4 * (tid + 256 * q)) = wv[q];
       __syncthreads();
       // the next chunk (or the next tile's first chunk) into registers during the MFMAs
-      if (ch0 + NM_CH < a.C) {
+      if (ch0 + NM_CH < ce) {
         load_chunk(a.x + (long long)b * a.xsb, r0, c0p, ch0 + NM_CH);
-      } else if (t + (int)gridDim.x < ntiles) {
-        int b2, r2, c2;
-        tile_of(t + (int)gridDim.x, b2, r2, c2);
-        load_chunk(a.x + (long long)b2 * a.xsb, r2, c2, 0);
+      } else if (it + (int)gridDim.x < items) {
+        int t2, cb2, ce2, b2, r2, c2;
+        item_of(it + (int)gridDim.x, t2, cb2, ce2);
+        tile_of(t2, b2, r2, c2);
+        load_chunk(a.x + (long long)b2 * a.xsb, r2, c2, cb2);
       }
       for (int c4 = 0; c4 < nch / 4; ++c4) {
         float4 xv[2][3][3];
@@ -1852,7 +1866,23 @@ __global__ __launch_bounds__(256, 2) void convt2_narrow_mfma(NarrowArgs a, int n
         }
       }
     }
-    if (co < NC) {
+    if (co < NC && a.splits > 1) {  // raw partial sums, [split][b][co][oh][ow]
+      float* sb = a.slab + ((long long)((it % a.splits) * a.B + b) * NC + co) * a.Ho * a.Wo;
+      const int blk = lane >> 2;
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int q = 4 * blk + i;
+          const int gi = r0 + 4 * wid + (q >> 4), gj = c0p + 16 * g + (q & 15);
+          if (gi >= a.H || gj >= a.W) continue;
+#pragma unroll
+          for (int ph = 0; ph < 2; ++ph)
+#pragma unroll
+            for (int pw = 0; pw < 2; ++pw)
+              sb[(long long)(2 * gi + ph) * a.Wo + 2 * gj + pw] = acc[g][ph * 2 + pw][i];
+        }
+    } else if (co < NC) {
       const float wsc = a.wscale ? a.wscale[0] : 1.f;
       const float bv = a.bias ? a.bias[co] : 0.f;
       float* yb = a.y + (long long)b * a.ysb + (long long)co * a.ysc;
@@ -1872,6 +1902,22 @@ __global__ __launch_bounds__(256, 2) void convt2_narrow_mfma(NarrowArgs a, int n
                   act_fwd(acc[g][ph * 2 + pw][i] * wsc + bv, a.act, a.alpha);
         }
     }
+  }
+}
+
+// y = act(sum over splits of convt2_narrow_mfma's partial sums * wscale + bias), splits
+// added in order (deterministic); one thread per output element, slab reads coalesced
+__global__ __launch_bounds__(256) void narrow_split_reduce(NarrowArgs a) {
+  const long long per = (long long)a.Ho * a.Wo, n = (long long)a.B * a.Cout * per;
+  const float wsc = a.wscale ? a.wscale[0] : 1.f;
+  for (long long e = blockIdx.x * 256LL + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    float v = a.slab[e];
+    for (int sp = 1; sp < a.splits; ++sp) v += a.slab[(long long)sp * n + e];
+    const long long bc = e / per, pix = e - bc * per;
+    const int b = (int)(bc / a.Cout), co = (int)(bc - (long long)b * a.Cout);
+    const int oh = (int)(pix / a.Wo), ow = (int)(pix - (long long)oh * a.Wo);
+    a.y[(long long)b * a.ysb + (long long)co * a.ysc + (long long)oh * a.ysh + (long long)ow * a.ysw] =
+        act_fwd(v * wsc + (a.bias ? a.bias[co] : 0.f), a.act, a.alpha);
   }
 }
 
@@ -2166,6 +2212,16 @@ static bool plan_narrow_t(Plan& p, int batch, const float* x, const long long* x
   p.pack = true;
   p.pack_floats = (size_t)C * 256;
   p.pn_s_in = s_in; p.pn_s_out = s_out;
+  // channel splits when the tiles alone cannot fill the chip (two resident blocks per CU)
+  const long long ntiles = (long long)batch * ceil_div(H, NM_TR) * ceil_div(W, NM_TC);
+  const int chunks = ceil_div(C, NM_CH);
+  int splits = 1;
+  if (ntiles < 256 && !getenv_flag("RGAN_NO_NARROW_SPLIT"))
+    splits = (int)std::min<long long>(std::min(chunks, 8), ceil_div(512, (int)std::max<long long>(ntiles, 1)));
+  a.cps = ceil_div(chunks, std::max(splits, 1)) * NM_CH;
+  a.splits = ceil_div(C, a.cps);
+  a.slab = nullptr;
+  p.slab_floats = a.splits > 1 ? (size_t)a.splits * batch * nc * 4 * H * W : 0;
   p.pk.W = w;
   return true;
 }
@@ -2527,12 +2583,16 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
   if (p.mode == MODE_NARROW_T) {
     a.w = packed;
     const int ntiles = a.B * ceil_div(a.H, NM_TR) * ceil_div(a.W, NM_TC);
-    const int blocks = std::min(ntiles, 512);  // persistent: two resident blocks per CU
+    const int blocks = std::min(ntiles * a.splits, 512);  // persistent: two resident blocks per CU
     switch (a.Cout) {
       case 1: convt2_narrow_mfma<1><<<blocks, 256, 0, s>>>(a, ntiles); break;
       case 2: convt2_narrow_mfma<2><<<blocks, 256, 0, s>>>(a, ntiles); break;
       case 3: convt2_narrow_mfma<3><<<blocks, 256, 0, s>>>(a, ntiles); break;
       default: convt2_narrow_mfma<4><<<blocks, 256, 0, s>>>(a, ntiles); break;
+    }
+    if (a.splits > 1) {
+      const long long n = (long long)a.B * a.Cout * a.Ho * a.Wo;
+      narrow_split_reduce<<<(unsigned)std::min<long long>(ceil_div(n, 256LL), 4096), 256, 0, s>>>(a);
     }
   } else if (p.img_in) {
     // persistent waves (two resident blocks of 4 per CU) loop over the 32-pixel wave tiles
@@ -2632,6 +2692,8 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
       RGAN_CHECK_LAUNCH();
       packed = (const float*)ws;
     }
+    if (p.slab_floats)  // narrow ConvT channel-split partial sums, after the pack
+      p.na.slab = (float*)((char*)ws + (p.prepacked ? 0 : align_up(p.pack_floats * 4, 256)));
     ProfRec rec{};
     const bool prof = g_prof && g_recs.size() * 2 + 2 <= g_pool.size();
     if (prof) {

@@ -214,6 +214,12 @@ def test_conv_narrow_paths(K, nc):
     for cache in (False, True, True):
         y = K.conv_fwd(x, w, gt, bias=b, act="tanh", wscale=s, nchw_out=True, cache=cache)
         assert _rel(y, torch.tanh(_ref_conv(x, w * 0.5, gt, b))) < 3e-6
+    # few tiles: the channel sum split over blocks (5 splits, the last one 8 channels) + reduce
+    x2 = _nhwc(torch.randn(2, 72, 10, 10, device=DEV))
+    w2 = torch.randn(72, nc, 4, 4, device=DEV) * 0.1
+    for cache in (False, True):
+        y = K.conv_fwd(x2, w2, gt, bias=b, act="tanh", wscale=s, nchw_out=True, cache=cache)
+        assert _rel(y, torch.tanh(_ref_conv(x2, w2 * 0.5, gt, b))) < 3e-6
     # the ConvT's dgrad (a Conv2d over the nc-channel image: narrow-in kernel), NCHW image grad
     gy = torch.randn(3, nc, 12, 12, device=DEV)
     x64 = x.double().cpu().requires_grad_(True)

@@ -55,6 +55,8 @@ def main():
                    print_every=10 ** 9, spectral=wl == "C5", rgan_rng="device")
     t = Trainer(p, synthetic_images(1024, size, device="cuda"))
     K.conv_fwd = wrap("fwd", K.conv_fwd, lambda x, w, geom, *a, **kw: (tuple(x.shape), tuple(w.shape), g(geom)))
+    K.conv_fwd_bn = wrap("fwd_bn", K.conv_fwd_bn, lambda x, w, geom, *a, **kw: (tuple(x.shape), tuple(w.shape),
+                                                                              g(geom)))
     K.conv_dgrad = wrap("dgrad", K.conv_dgrad, lambda dy, w, geom, xs, *a, **kw: (tuple(xs), tuple(w.shape), g(geom)))
     K.conv_wgrad = wrap("wgrad", K.conv_wgrad, lambda x, dy, geom, ws, *a, **kw: (tuple(x.shape), tuple(ws), g(geom)))
     for i in range(2):
