@@ -26,6 +26,10 @@
 #include <atomic>
 #include <vector>
 
+#ifndef RGAN_GEMM_SB
+#define RGAN_GEMM_SB 0
+#endif
+
 namespace rgan {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -147,11 +151,14 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   constexpr int B_LD = KROW ? KROW_LD : BN + 4;
   constexpr int B_SZ = KROW ? BN * KROW_LD : BK * B_LD;
   constexpr int STAGE = A_SZ + B_SZ;
-  constexpr int EPI_SZ = KROW ? 4 * 64 * 72 : 0;  // vector epilogue staging (4 waves x 64 x 72)
+  // RGAN_GEMM_SB (experiment): single-buffered LDS stage (two barriers per k tile) and the
+  // vector epilogue in two 32-row passes -- ~37 KB per block, four resident blocks per CU
+  constexpr bool GEMM_SB = RGAN_GEMM_SB && !EMU;
+  constexpr int EPI_SZ = KROW ? 4 * (GEMM_SB ? 32 : 64) * 72 : 0;  // vector epilogue staging (4 waves x rows x 72)
   // EMU: one (single-buffered) stage of six bf16 planes (A hi/mid/lo, B hi/mid/lo), rows of
   // 32 bf16 = 16 dwords at a 20-dword stride (16 lanes' ds_read_b128 on 16 distinct quads)
   constexpr int EMU_RS = 20, EMU_PLANE = 128 * EMU_RS;  // dwords
-  constexpr int MAIN_SZ = EMU ? 6 * EMU_PLANE : 2 * STAGE;
+  constexpr int MAIN_SZ = EMU ? 6 * EMU_PLANE : GEMM_SB ? STAGE : 2 * STAGE;
   static_assert(!EMU || (FAST && MODE != MODE_WGRAD && BM == 128 && BN == 128), "bf16x6 path: FAST 128x128 CONV/CONVT2");
   __shared__ __attribute__((aligned(16))) float smem[MAIN_SZ > EPI_SZ ? MAIN_SZ : EPI_SZ];
 
@@ -697,7 +704,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   }
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
+    const int cur = GEMM_SB ? 0 : kt & 1;
     if (kt + 1 < nk) {
       if constexpr (FAST) load_fast(kbeg + (kt + 1) * BK, (kt + 1) & 1);
       else load_tiles(kbeg + (kt + 1) * BK);
@@ -800,7 +807,14 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
     }
 #endif
     }
-    if (kt + 1 < nk) store_tiles(cur ^ 1);
+    if constexpr (GEMM_SB) {
+      if (kt + 1 < nk) {
+        __syncthreads();  // every wave's reads of the one stage are done
+        store_tiles(0);
+      }
+    } else if (kt + 1 < nk) {
+      store_tiles(cur ^ 1);
+    }
     __syncthreads();
   }
   }  // EMU / fp32 main loop
@@ -818,9 +832,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
 #else
     if ((slab_out && g.N % 4 == 0) || (!slab_out && g.vec_out)) {
 #endif
-      constexpr int EP_LD = 72;
+      // RGAN_GEMM_SB: the 64 rows in two passes of 32 (LDS for four resident blocks per CU)
+      constexpr int EP_LD = 72, EPR = GEMM_SB ? 32 : 64, NP = 64 / EPR;
       __shared__ long long emoff[BM];
-      float* T = smem + wid * (64 * EP_LD);
+      float* T = smem + wid * (EPR * EP_LD);
       const float wsc = (!slab_out && g.wscale) ? g.wscale[0] : 1.f;
       if (!slab_out) {
         for (int i = tid; i < BM; i += 256) {
@@ -829,62 +844,71 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
         }
       }
       // the activation branch is taken once per tile (uniform), not once per element
-      auto stage = [&](auto actf) {
+      auto stage = [&](auto actf, int pp) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int cl = 32 * j + l32, col = n0 + wn + cl;
           const float bv = (!slab_out && g.bias && col < g.N) ? g.bias[col] : 0.f;
 #pragma unroll
-          for (int i = 0; i < TM; ++i)
+          for (int i = 0; i < TM; ++i) {
+            if (NP > 1 && i != pp) continue;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const int rl = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+              const int rl = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk - EPR * pp;
               T[rl * EP_LD + cl] = actf(acc[i][j][r] * wsc + bv);
             }
+          }
         }
       };
-      if (slab_out || g.act <= RGAN_ACT_LRELU) {
-        const float neg = (slab_out || g.act == RGAN_ACT_NONE) ? 1.f : (g.act == RGAN_ACT_RELU ? 0.f : g.alpha);
-        stage([neg](float v) { return v > 0.f ? v : v * neg; });
-      } else {
-        stage([&](float v) { return act_fwd_curved(v, g.act, g.alpha); });
-      }
-      __syncthreads();
-      if (!slab_out && g.bnp) {
-        // BatchNorm batch statistics in the epilogue: the wave's 64 finished rows of column
-        // `lane` (one channel; conflict-free LDS row reads) -> (sum y, sum y^2) of the
-        // segment in double (fp32 products are exact in double; the merge is a plain
-        // fixed-order sum).  Host guarantees M % 64 == 0 and n == channel; segment =
-        // (phase, m / 64).
-        const int mrow = m0 + wm, col = n0 + wn + lane;
-        if (mrow < g.M && col < g.N) {
-          double s1 = 0.0, s2 = 0.0;
+      const bool bn_stats = !slab_out && g.bnp;
+      double s1 = 0.0, s2 = 0.0;
+      const int q = lane & 15, n = n0 + wn + 4 * q;
+      float* slab = slab_out ? g.slab + (size_t)z * g.M * g.N : nullptr;
+      const long long noff = (slab_out || n >= g.N) ? 0 : col_offset(g.out, n);
+#pragma unroll
+      for (int pp = 0; pp < NP; ++pp) {
+        if (pp > 0) __syncthreads();  // the previous pass's T reads are done
+        if (slab_out || g.act <= RGAN_ACT_LRELU) {
+          const float neg = (slab_out || g.act == RGAN_ACT_NONE) ? 1.f : (g.act == RGAN_ACT_RELU ? 0.f : g.alpha);
+          stage([neg](float v) { return v > 0.f ? v : v * neg; }, pp);
+        } else {
+          stage([&](float v) { return act_fwd_curved(v, g.act, g.alpha); }, pp);
+        }
+        __syncthreads();
+        if (bn_stats) {
+          // BatchNorm batch statistics in the epilogue: the wave's finished rows of column
+          // `lane` (one channel; conflict-free LDS row reads) -> (sum y, sum y^2) of the
+          // 64-row segment in double, rows in order (fp32 products are exact in double; the
+          // merge is a plain fixed-order sum).  Host guarantees M % 64 == 0 and n == channel;
+          // segment = (phase, m / 64).
 #pragma unroll 8
-          for (int rl = 0; rl < 64; ++rl) {
+          for (int rl = 0; rl < EPR; ++rl) {
             const double d = (double)T[rl * EP_LD + lane];
             s1 += d;
             s2 += d * d;
           }
+        }
+        if (n < g.N) {
+#pragma unroll
+          for (int s4 = 0; s4 < EPR / 4; ++s4) {
+            const int rl = 4 * s4 + (lane >> 4), m = m0 + wm + EPR * pp + rl;
+            if (m < g.M) {
+              const float4 v = *reinterpret_cast<const float4*>(T + rl * EP_LD + 4 * q);
+              float* dst = slab_out ? slab + (size_t)m * g.N + n : g.C + emoff[wm + EPR * pp + rl] + noff;
+#if RGAN_EXP_NOSTORE
+              if (v.x == 1234.5f)
+#endif
+*reinterpret_cast<float4*>(dst) = v;
+            }
+          }
+        }
+      }
+      if (bn_stats) {
+        const int mrow = m0 + wm, col = n0 + wn + lane;
+        if (mrow < g.M && col < g.N) {
           const size_t seg = (size_t)phase * (uint32_t)(g.M >> 6) + (uint32_t)(mrow >> 6);
           g.bnp[(seg * 2) * g.N + col] = s1;
           g.bnp[(seg * 2 + 1) * g.N + col] = s2;
-        }
-      }
-      const int q = lane & 15, n = n0 + wn + 4 * q;
-      if (n < g.N) {
-        float* slab = slab_out ? g.slab + (size_t)z * g.M * g.N : nullptr;
-        const long long noff = slab_out ? 0 : col_offset(g.out, n);
-#pragma unroll
-        for (int s4 = 0; s4 < 16; ++s4) {
-          const int rl = 4 * s4 + (lane >> 4), m = m0 + wm + rl;
-          if (m < g.M) {
-            const float4 v = *reinterpret_cast<const float4*>(T + rl * EP_LD + 4 * q);
-            float* dst = slab_out ? slab + (size_t)m * g.N + n : g.C + emoff[wm + rl] + noff;
-#if RGAN_EXP_NOSTORE
-            if (v.x == 1234.5f)
-#endif
-*reinterpret_cast<float4*>(dst) = v;
-          }
         }
       }
       return;
@@ -951,7 +975,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, bool AV, bool BV, bool FAST>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
+__global__ __launch_bounds__(256, RGAN_GEMM_SB ? 4 : 2) void gemm_kernel(GemmArgs g) {
   gemm_body<MODE, BM, BN, WM, WN, AV, BV, FAST, false>(g);
 }
 
