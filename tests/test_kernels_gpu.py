@@ -584,8 +584,11 @@ def test_spectral_norm(K, transposed):
 
 def test_adam_matches_torch(K):
     torch.manual_seed(5)
-    shapes = [(64, 3, 4, 4), (128,), (7, 9)]
+    # one block / several blocks with a partial last one (float4 path), scalar path (n % 4 != 0)
+    # over two blocks, a 16-B-misaligned view (scalar path), and > 48 tensors (two launches)
+    shapes = [(64, 3, 4, 4), (128,), (7, 9), (3000, 7), (4099,), (1001,)] + [(5, 4)] * 46
     params = [torch.randn(s, device=DEV) for s in shapes]
+    params[5] = torch.randn(1002, device=DEV)[1:]
     ref = [p.detach().cpu().clone().requires_grad_(True) for p in params]
     opt = torch.optim.Adam(ref, lr=1e-4, betas=(0.5, 0.999), weight_decay=0.01)
     m = [torch.zeros_like(p) for p in params]
