@@ -1545,15 +1545,17 @@ __device__ __forceinline__ void dma_lds16(int m0, int voff, i32x4 rsrc) {
                : "memory", "m0");
 }
 
-template <int CI, int WS, int ACT>  // ACT 0: identity, 1: max(v, v * neg) (ReLU / LeakyReLU, neg <= 1), 2: act_fwd
+// NI: 32-channel groups per block (4: 128-channel tiles; 1: 32-channel tiles for narrow D widths)
+template <int CI, int WS, int ACT, int NI = 4>  // ACT 0: identity, 1: max(v, v * neg) (ReLU / LeakyReLU, neg <= 1), 2: act_fwd
 __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
+  constexpr int NCH = 32 * NI;                    // output channels per block
   constexpr int K = CI * 16, NS = K / 2;          // MFMA steps (32x32x2)
   constexpr int RW = 32 / WS;                     // output rows per wave tile (1 or 2)
   constexpr int RR = 2 * RW + 2, CW = 2 * WS + 8; // window rows, columns (image cols 2 oj0 - 4 ..)
   constexpr int WCH = RR * CW;                    // window floats per channel
   constexpr int WIN = CI * WCH, NQ = WIN / 4;     // window floats, float4s
   constexpr int QPL = (NQ + 63) / 64;             // DMA pieces per lane
-  constexpr int WSTG = (128 * (K + 1) + 511) / 512 * 64;  // 1/8 of the prologue's weight staging
+  constexpr int WSTG = (NCH * (K + 1) + 511) / 512 * 64;  // 1/8 of the prologue's weight staging
   constexpr int WBUF = QPL * 256 > WSTG ? QPL * 256 : WSTG;  // one window buffer (floats)
   constexpr int RD = 4;                           // im2col read-ahead (MFMA steps)
   constexpr int OOB_OFF = 0x7ffffff0;
@@ -1561,49 +1563,49 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
   __shared__ __attribute__((aligned(16))) float win[4][2][WBUF];
   __shared__ __attribute__((aligned(16))) float stg[4][32 * 32];  // per wave [pixel][channel quad ^ swz]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, lk = lane >> 5;
-  const int n0 = blockIdx.y * 128;
+  const int n0 = blockIdx.y * NCH;
   const int HWo = a.Ho * a.Wo;
   // raw buffer descriptor of x for the DMA pieces (stride 0, num_records = byte extent)
   const i32x4 xd = {(int)(uintptr_t)a.x, (int)((uintptr_t)a.x >> 32), a.x_bytes, 0x00020000};
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, a.y_bytes, 0x00020000);
   // weights: wa[i][s] = W[n0 + 32 i + l32][2 s + lk] / sigma  (torch [Cout][CI][4][4] = [n][k])
-  // (staged through LDS by the whole block with coalesced loads: 128 x K floats, once)
+  // (staged through LDS by the whole block with coalesced loads: NCH x K floats, once)
   // (every global load of the prologue is issued before the first wait: at ~1-2 us per
   // round trip, a dependent sequence of them costs as much as several tiles)
-  constexpr int WLD = (128 * K + 255) / 256;
+  constexpr int WLD = (NCH * K + 255) / 256;
   float wtmp[WLD];
 #pragma unroll
   for (int q = 0; q < WLD; ++q) {
     const int e = tid + 256 * q;
-    wtmp[q] = e < 128 * K ? a.w[(size_t)n0 * K + e] : 0.f;
+    wtmp[q] = e < NCH * K ? a.w[(size_t)n0 * K + e] : 0.f;
   }
   const float wsc = a.wscale ? a.wscale[0] : 1.f;
-  float wb[4];  // bias column (see below)
+  float wb[NI];  // bias column (see below)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) wb[i] = (a.bias && lk == 0) ? a.bias[n0 + 32 * i + l32] : 0.f;
+  for (int i = 0; i < NI; ++i) wb[i] = (a.bias && lk == 0) ? a.bias[n0 + 32 * i + l32] : 0.f;
   {
     float* wst = &win[0][0][0];  // the window buffers are free until the first DMA
-    static_assert(4 * 2 * WBUF >= 128 * (K + 1), "weight staging fits the window buffers");
+    static_assert(4 * 2 * WBUF >= NCH * (K + 1), "weight staging fits the window buffers");
 #pragma unroll
     for (int q = 0; q < WLD; ++q) {
       const int e = tid + 256 * q, r = e / K;  // row stride K + 1: conflict-free reads below
-      if (e < 128 * K) wst[e + r] = wtmp[q];
+      if (e < NCH * K) wst[e + r] = wtmp[q];
     }
     __syncthreads();
   }
-  float wa[4][NS];
+  float wa[NI][NS];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int s = 0; s < NS; ++s) wa[i][s] = win[0][0][(32 * i + l32) * (K + 1) + 2 * s + lk];
   if (a.wscale) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int s = 0; s < NS; ++s) wa[i][s] *= wsc;
   }
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int s = 0; s < NS; ++s) asm volatile("" : "+v"(wa[i][s]));  // resident: no re-load in the loop
   // bias as one extra MFMA step per accumulator (wb: k0 = bias, k1 = 0, against a column of
@@ -1682,15 +1684,15 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
     };
 #pragma unroll
     for (int s = 0; s < RD && s < NS; ++s) read_step(s);
-    f32x16 acc[4];
+    f32x16 acc[NI];
     const f32x16 zero = {};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[i], one_k0, zero, 0, 0, 0);
+    for (int i = 0; i < NI; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(wb[i], one_k0, zero, 0, 0, 0);
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       if (s + RD < NS) read_step(s + RD);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NI; ++i)
         acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[i][s], bv[s], acc[i], 0, 0, 0);
     }
     if (more) fetch(tn, Wn);
@@ -1698,7 +1700,7 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
     tile_pos(t, b, oi0, oj0);
     const int tb4 = (int)(((long long)b * a.ysb + (long long)oi0 * a.ysh + (long long)oj0 * a.ysw) * 4);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NI; ++i) {
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int quad = 2 * g + lk;
@@ -2263,7 +2265,8 @@ static bool plan_narrow_in(Plan& p, const RganConv* d, const float* x, const flo
   const long long yext = 4 * (1 + (d->batch - 1) * d->ys[0] + (d->cout - 1) * d->ys[1] + (d->hout - 1) * d->ys[2] +
                               (d->wout - 1) * d->ys[3]);
   p.img_in = !getenv_flag("RGAN_NO_IMG_IN") && d->stride == 2 && d->pad == 1 && d->hout * 2 == d->hin &&
-             d->wout * 2 == d->win && d->cin <= 3 && d->cout % 128 == 0 && vec_nhwc(y, d->ys, d->cout) &&
+             d->wout * 2 == d->win && d->cin <= 3 && (d->cout % 128 == 0 || (d->cin == 3 && d->cout % 32 == 0)) &&
+             vec_nhwc(y, d->ys, d->cout) &&
              (d->wout == 16 || d->wout % 32 == 0) && ((long long)d->batch * d->hout * d->wout / 32) < (1LL << 31) &&
              d->xs[3] == 1 && d->xs[0] % 4 == 0 && d->xs[1] % 4 == 0 && d->xs[2] % 4 == 0 && d->xs[0] >= 0 &&
              d->xs[1] >= 0 && d->xs[2] >= 0 && ((uintptr_t)x & 15) == 0 && xext < (1LL << 31) && yext < (1LL << 31);
@@ -2620,22 +2623,28 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
     }
   } else if (p.img_in) {
     // persistent waves (two resident blocks of 4 per CU) loop over the 32-pixel wave tiles
+    // (32-channel tiles when the width is not a multiple of 128: D at h = 32, 64)
     const int tiles = a.B * a.Ho * a.Wo / 32;
-    const dim3 grid(std::min(ceil_div(tiles, 4), 512), a.Cout / 128);
+    const bool wide = a.Cout % 128 == 0;
+    const dim3 grid(std::min(ceil_div(tiles, 4), 512), a.Cout / (wide ? 128 : 32));
     const int act_kind = a.act == RGAN_ACT_NONE ? 0
                          : (a.act == RGAN_ACT_RELU || (a.act == RGAN_ACT_LRELU && a.alpha <= 1.f)) ? 1 : 2;
-#define RGAN_IMG_A(CC, WW)                                                            \
-  switch (act_kind) {                                                                 \
-    case 0: conv_img_in<CC, WW, 0><<<grid, 256, 0, s>>>(a, tiles); break;             \
-    case 1: conv_img_in<CC, WW, 1><<<grid, 256, 0, s>>>(a, tiles); break;             \
-    default: conv_img_in<CC, WW, 2><<<grid, 256, 0, s>>>(a, tiles); break;            \
+#define RGAN_IMG_A(CC, WW, NN)                                                            \
+  switch (act_kind) {                                                                     \
+    case 0: conv_img_in<CC, WW, 0, NN><<<grid, 256, 0, s>>>(a, tiles); break;             \
+    case 1: conv_img_in<CC, WW, 1, NN><<<grid, 256, 0, s>>>(a, tiles); break;             \
+    default: conv_img_in<CC, WW, 2, NN><<<grid, 256, 0, s>>>(a, tiles); break;            \
   }
-#define RGAN_IMG(CC)                                                          \
-  if (a.Wo == 16) RGAN_IMG_A(CC, 16) else RGAN_IMG_A(CC, 32)
-    switch (a.C) {
-      case 1: RGAN_IMG(1) break;
-      case 2: RGAN_IMG(2) break;
-      default: RGAN_IMG(3) break;
+#define RGAN_IMG(CC, NN)                                                          \
+  if (a.Wo == 16) RGAN_IMG_A(CC, 16, NN) else RGAN_IMG_A(CC, 32, NN)
+    if (!wide) {  // plan_narrow_in: CI == 3
+      RGAN_IMG(3, 1)
+    } else {
+      switch (a.C) {
+        case 1: RGAN_IMG(1, 4) break;
+        case 2: RGAN_IMG(2, 4) break;
+        default: RGAN_IMG(3, 4) break;
+      }
     }
 #undef RGAN_IMG
 #undef RGAN_IMG_A

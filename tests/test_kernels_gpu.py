@@ -649,18 +649,20 @@ def test_spectral_power_batch(K):
 
 @pytest.mark.parametrize("ci", [1, 3, 4])
 @pytest.mark.parametrize("hw", [(32, 32), (64, 128), (128, 64), (16, 512), (256, 256)])
-def test_conv_image_window_kernel(K, ci, hw):
-    """conv_img_in (windowed image conv: k4 s2 p1, <= 4 input channels, 128-channel tiles):
+@pytest.mark.parametrize("cout", [256, 96, 32])
+def test_conv_image_window_kernel(K, ci, hw, cout):
+    """conv_img_in (windowed image conv: k4 s2 p1, <= 4 input channels, 128-channel tiles,
+    or 32-channel tiles for 3-channel images when the width is not a multiple of 128):
     fwd with bias / LeakyReLU / wscale on NCHW and NHWC images, and the ConvTranspose2d
     image-layer dgrad that runs on it, vs torch fp64 (every tile shape: 128-wide row
     segments and 128 / Wo whole rows)."""
     H, W = hw
     B = 2 if H * W <= 128 * 128 else 1
-    torch.manual_seed(ci + H)
+    torch.manual_seed(ci + H + cout)
     gc, gt = K.ConvGeom(4, 2, 1, False), K.ConvGeom(4, 2, 1, True)
     img = torch.randn(B, ci, H, W, device=DEV)
-    w = torch.nn.Parameter(torch.randn(256, ci, 4, 4, device=DEV) * 0.1)
-    b = torch.randn(256, device=DEV)
+    w = torch.nn.Parameter(torch.randn(cout, ci, 4, 4, device=DEV) * 0.1)
+    b = torch.randn(cout, device=DEV)
     s = torch.tensor([0.7], device=DEV)
     ref = F.leaky_relu(F.conv2d(img.double().cpu(), (w * 0.7).detach().double().cpu(), b.double().cpu(), stride=2,
                                 padding=1), 0.2)
@@ -669,6 +671,8 @@ def test_conv_image_window_kernel(K, ci, hw):
             y = K.conv_fwd(x, w, gc, bias=b, act="lrelu", alpha=0.2, wscale=s, cache=cache)
             assert K.is_nhwc(y)
             assert _rel(y, ref) < 3e-6
+    if cout != 256:
+        return
     # G's image layer ConvT(256 -> ci): its input gradient is a Conv2d over the image gradient
     wt = torch.randn(256, ci, 4, 4, device=DEV) * 0.1
     gy = torch.randn(B, ci, H, W, device=DEV)
