@@ -247,13 +247,16 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   constexpr int FB_N = BN / 32;
   auto sw_q = [&](int R) { return (tid & 7) + 8 * ((tid >> 5) % (R / 32)); };
   auto sw_p = [&](int R, int i) { return ((tid >> 3) & 3) + 4 * ((tid >> 5) / (R / 32)) + (32 / (R / 32)) * i; };
-  __shared__ int ptab[2][BK];   // WGRAD FAST: im2col pixel offsets of the next tiles
+  // WGRAD FAST: im2col pixel offsets of the next tiles, per tap of the block's n tile (a
+  // tile holds one tap when Cin >= BN, else BN / Cin <= 4 whole taps of one kernel row)
+  __shared__ int ptab[2][4 * BK];
   __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g.a.p, (short)0, g.a_bytes, 0x00020000);
   __amdgpu_buffer_rsrc_t brsrc =
       MODE == MODE_WGRAD ? __builtin_amdgcn_make_buffer_rsrc((void*)g.im.p, (short)0, g.im_bytes, 0x00020000)
                          : __builtin_amdgcn_make_buffer_rsrc((void*)Bw, (short)0, g.bw_bytes, 0x00020000);
   int aoff[FAST ? FA_N : 1], boff[FAST ? FB_N : 1];
   int f_tap = 0, f_c0 = 0, f_cin = 1, w_tab = 0;
+  int w_ntap = 1, w_tq = 0, w_qb = 0;  // WGRAD FAST: taps per n tile; this thread's tap, channel byte offset
   if constexpr (FAST) {
     if constexpr (MODE != MODE_WGRAD) {
       // packed weights [N][K]: rows n = n0 + (tid>>3) + 32i, k quad tid&7 (like A)
@@ -277,6 +280,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
       w_tab = ((int)kh - g.pad) * (int)g.im.sh + ((int)kw - g.pad) * (int)g.im.sw + ci0;  // tap part
       f_tap = (int)kh;   // kept for the bounds checks below
       f_c0 = kw;
+      // column quad of this thread's B loads -> (tap within the tile, channel): with
+      // Cin >= BN every quad is in the first tap (4 q < BN <= Cin)
+      const int cin = (int)g.fC.d, c4 = 4 * sw_q(BN);
+      w_ntap = cin >= BN ? 1 : BN / cin;
+      w_tq = cin >= BN ? 0 : c4 / cin;
+      w_qb = (c4 - w_tq * cin) * 4;
     }
   }
   // CONV/CONVT2 FAST: per-row offsets for the current tap
@@ -300,7 +309,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
       }
     }
   };
-  // WGRAD FAST: one wave writes the im2col pixel offsets of tile k0 into ptab[slot]
+  // WGRAD FAST: one wave writes the im2col pixel offsets of tile k0 into ptab[slot], for
+  // each of the tile's taps (kw0 + t of kernel row kh)
   auto build_table = [&](int k0, int slot) {
     if constexpr (FAST && MODE == MODE_WGRAD) {
       const int l = tid & 63;
@@ -310,11 +320,14 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
         const uint32_t rem = p - b * g.fghw.d;
         const uint32_t oi = g.fgw.div(rem);
         const uint32_t oj = rem - oi * g.fgw.d;
-        const int ih = (int)oi * g.stride - g.pad + f_tap, iw = (int)oj * g.stride - g.pad + f_c0;
-        ptab[slot][l] = (p < kend && (unsigned)ih < (unsigned)g.im.H && (unsigned)iw < (unsigned)g.im.W)
-                            ? ((int)b * (int)g.im.sb + (int)oi * g.stride * (int)g.im.sh +
-                               (int)oj * g.stride * (int)g.im.sw + w_tab) * 4
-                            : OOB;
+        const int ih = (int)oi * g.stride - g.pad + f_tap;
+        const int pix = (int)b * (int)g.im.sb + (int)oi * g.stride * (int)g.im.sh + (int)oj * g.stride * (int)g.im.sw;
+        const bool rok = p < kend && (unsigned)ih < (unsigned)g.im.H;
+        for (int t = 0; t < w_ntap; ++t) {
+          const int iw = (int)oj * g.stride - g.pad + f_c0 + t;
+          ptab[slot][t * BK + l] =
+              (rok && (unsigned)iw < (unsigned)g.im.W) ? (pix + w_tab + t * (int)g.im.sw) * 4 : OOB;
+        }
       }
     }
   };
@@ -346,10 +359,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
         ra[4 * i + 0] = __uint_as_float(v.x); ra[4 * i + 1] = __uint_as_float(v.y);
         ra[4 * i + 2] = __uint_as_float(v.z); ra[4 * i + 3] = __uint_as_float(v.w);
       }
-      const int qb = sw_q(BN) * 16;
 #pragma unroll
       for (int i = 0; i < FB_N; ++i) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(brsrc, ptab[slot][sw_p(BN, i)] + qb, 0, 0);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(brsrc, ptab[slot][w_tq * BK + sw_p(BN, i)] + w_qb, 0, 0);
         rb[4 * i + 0] = __uint_as_float(v.x); rb[4 * i + 1] = __uint_as_float(v.y);
         rb[4 * i + 2] = __uint_as_float(v.z); rb[4 * i + 3] = __uint_as_float(v.w);
       }
@@ -2172,7 +2184,12 @@ static void set_fast(Plan& p, int batch) {
     const long long im_bytes = img_span_bytes(g.im, batch);
     if (im_bytes > FAST_MAX_BYTES) return;
     if (g.a.sh != (long long)g.a.W * g.a.sw || g.a.sb != (long long)g.a.H * g.a.sh) return;
-    if (g.im.C % bn != 0) return;
+    // a B tile is one tap's BN channels, or BN / Cin <= 4 whole taps of one kernel row
+    const int cin = g.im.C;
+    static const bool multitap = !getenv_flag("RGAN_NO_MULTITAP");  // A/B switch
+    if (cin % bn != 0 &&
+        !(multitap && bn % cin == 0 && cin % 4 == 0 && bn / cin <= 4 && g.KW % (bn / cin) == 0))
+      return;
     g.a_bytes = (int)a_bytes;
     g.im_bytes = (int)im_bytes;
   }

@@ -52,6 +52,9 @@ SMALL = [
     (2, 64, 128, 8, 4, 2, 1, False),
     (2, 128, 64, 4, 4, 2, 1, True),
     (7, 20, 36, 10, 4, 2, 1, False),    # ragged sizes
+    (2, 32, 64, 16, 4, 2, 1, False),    # FAST WGRAD, Cin = 32: four taps per 128-wide n tile
+    (2, 64, 32, 16, 4, 2, 1, True),     # ConvT WGRAD over a 32-channel dy: four taps per tile
+    (3, 64, 128, 16, 4, 2, 1, False),   # two taps per tile
 ]
 
 
