@@ -32,6 +32,9 @@
 #ifndef RGAN_SB_NARROW
 #define RGAN_SB_NARROW 1
 #endif
+#ifndef RGAN_SB_M  // single-buffered 128x64 tile (27.6 KB per block)
+#define RGAN_SB_M 1
+#endif
 
 namespace rgan {
 
@@ -157,8 +160,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   // RGAN_GEMM_SB (experiment): single-buffered LDS stage (two barriers per k tile) and the
   // vector epilogue in two 32-row passes -- ~37 KB per block, four resident blocks per CU
   // The 256x32 narrow-N tile (CFG_N) is single-buffered by default: its two stages (83 KB)
-  // left one resident block per CU; one stage (41.5 KB) gives three
-  constexpr bool GEMM_SB = !EMU && (RGAN_GEMM_SB || (RGAN_SB_NARROW && BM == 256 && BN == 32));
+  // left one resident block per CU; one stage (41.5 KB) gives three.  The 128x64 tile
+  // (CFG_M) likewise (two -> five blocks; C3h32 -1.6 %, C1 / C4 unchanged)
+  constexpr bool GEMM_SB = !EMU && (RGAN_GEMM_SB || (RGAN_SB_NARROW && BM == 256 && BN == 32) ||
+                                    (RGAN_SB_M && BM == 128 && BN == 64));
   constexpr int EPI_SZ = KROW ? 4 * (GEMM_SB ? 32 : 64) * 72 : 0;  // vector epilogue staging (4 waves x rows x 72)
   // EMU: one (single-buffered) stage of six bf16 planes (A hi/mid/lo, B hi/mid/lo), rows of
   // 32 bf16 = 16 dwords at a 20-dword stride (16 lanes' ds_read_b128 on 16 distinct quads)
