@@ -60,6 +60,11 @@ size_t rgan_conv_workspace(const RganConv* d, int which, int prepacked);
  * rgan_conv_workspace reports separately (0). */
 size_t rgan_conv_pack_floats(const RganConv* d, int which);
 int rgan_conv_pack(const RganConv* d, int which, const float* w, float* packed, void* stream);
+/* n packs at once (the stale layouts of a net after its optimizer step, torch.optim's
+ * step at GLI:659/712 being what moved them): entry i = rgan_conv_pack(d[i], which[i], w[i],
+ * packed[i]); the tiled layouts share one launch per 16, others get their own. */
+int rgan_conv_pack_batch(int n, const RganConv* const* d, const int* which, const float* const* w,
+                         float* const* packed, void* stream);
 
 /* y = act(conv(x, w) * (*wscale) + bias).  Replaces Conv2d/ConvTranspose2d.forward
  * (GLI:336,361,387,410,428,448; arch 1 GLI:202-223,260-302) fused with the

@@ -35,6 +35,7 @@ _SIGS = {
     "rgan_conv_workspace": (c_sz, [ctypes.POINTER(RganConv), c_int, c_int]),
     "rgan_conv_pack_floats": (c_sz, [ctypes.POINTER(RganConv), c_int]),
     "rgan_conv_pack": (c_int, [ctypes.POINTER(RganConv), c_int, c_vp, c_vp, c_vp]),
+    "rgan_conv_pack_batch": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rgan_conv_fwd": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_f, c_vp, c_sz,
                               c_vp]),
     "rgan_conv_bn_segments": (c_ll, [ctypes.POINTER(RganConv), c_int]),

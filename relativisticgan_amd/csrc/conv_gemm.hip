@@ -1987,11 +1987,10 @@ __global__ void pack_narrow(const float* __restrict__ W, float* __restrict__ out
 // order (taps, then the smaller-stride index: 512 or 128 contiguous floats) and writing
 // whole 128-B lines (32-float k runs) of the [N][K] image.
 constexpr int PK_I = 32, PK_O = 8, PK_LD = PK_O * 17 + 1;  // odd row stride: conflict-free reads
-__global__ __launch_bounds__(256) void pack_tiled(PackArgs a) {
-  __shared__ float t[PK_I * PK_LD];  // [in][out][tap]
+__device__ __forceinline__ void pack_tiled_body(const PackArgs& a, int bx, int by, float* t) {  // t: [in][out][tap]
   const int KK = a.KH * a.KW;
   const int Nin = (int)a.fpci.d, Nout = a.N;
-  const int i0 = blockIdx.x * PK_I, o0 = blockIdx.y * PK_O;
+  const int i0 = bx * PK_I, o0 = by * PK_O;
   const bool in_fast = a.s_in < a.s_out;
   for (int e = threadIdx.x; e < PK_I * PK_O * 16; e += 256) {
     const int tap = e & 15;
@@ -2019,15 +2018,19 @@ __global__ __launch_bounds__(256) void pack_tiled(PackArgs a) {
   }
 }
 
+__global__ __launch_bounds__(256) void pack_tiled(PackArgs a) {
+  __shared__ float t[PK_I * PK_LD];
+  pack_tiled_body(a, blockIdx.x, blockIdx.y, t);
+}
+
 // 4x4 taps, Nin % 32 == 0, Nout % 8 == 0 (every C2 pack): the same brick moved with
 // float4s -- 4 taps per load (taps are the weight's contiguous index), 4 in-indices per
 // store (the packed row's contiguous index) -- 4 loads + 4 stores per thread, all issued
 // before their first use.
 constexpr int P4_LD = PK_O * 16 + 4;  // [in][out][16 taps], 16-B aligned rows
-__global__ __launch_bounds__(256) void pack_tiled16(PackArgs a) {
-  __shared__ __attribute__((aligned(16))) float t[PK_I * P4_LD];
+__device__ __forceinline__ void pack_tiled16_body(const PackArgs& a, int bx, int by, float* t) {
   const int Nin = (int)a.fpci.d, Nout = a.N, K = a.K;
-  const int i0 = blockIdx.x * PK_I, o0 = blockIdx.y * PK_O;
+  const int i0 = bx * PK_I, o0 = by * PK_O;
   const bool in_fast = a.s_in < a.s_out;
   float4 v[4];
 #pragma unroll
@@ -2064,6 +2067,32 @@ __global__ __launch_bounds__(256) void pack_tiled16(PackArgs a) {
     *reinterpret_cast<float4*>(a.out + ((size_t)phase * Nout + o0 + o) * K + (size_t)kt * Nin + i0 + 4 * iq) =
         make_float4(src[0], src[P4_LD], src[2 * P4_LD], src[3 * P4_LD]);
   }
+}
+
+__global__ __launch_bounds__(256) void pack_tiled16(PackArgs a) {
+  __shared__ __attribute__((aligned(16))) float t[PK_I * P4_LD];
+  pack_tiled16_body(a, blockIdx.x, blockIdx.y, t);
+}
+
+// Every stale weight layout of a net after its optimizer step in one launch (the repacks
+// of a small model are ~10 us launches of ~1 us of work each): entry j owns blocks
+// [first[j], first[j+1]) of a 1-D grid, its own (bx, by) brick grid and kernel body.
+constexpr int PACK_BATCH = 16;
+struct PackBatch {
+  PackArgs a[PACK_BATCH];
+  int kind[PACK_BATCH];  // 0: pack_tiled16, 1: pack_tiled
+  int gx[PACK_BATCH];
+  int first[PACK_BATCH + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void pack_multi(PackBatch b) {
+  __shared__ __attribute__((aligned(16))) float t[PK_I * (P4_LD > PK_LD ? P4_LD : PK_LD)];
+  int j = 0;
+  while (j + 1 < b.n && (int)blockIdx.x >= b.first[j + 1]) ++j;
+  const int local = (int)blockIdx.x - b.first[j], bx = local % b.gx[j], by = local / b.gx[j];
+  if (b.kind[j] == 0) pack_tiled16_body(b.a[j], bx, by, t);
+  else pack_tiled_body(b.a[j], bx, by, t);
 }
 
 // ---------------------------------------------------------------- host planning
@@ -2511,15 +2540,33 @@ static size_t plan_ws_bytes(const Plan& p) {
   return pack + align_up(p.slab_floats * 4, 256) + align_up(p.tap_floats * 4, 256);
 }
 
-static void launch_pack(const PackArgs& a, hipStream_t s) {
+// pack kernel of a layout: 0 pack_tiled16, 1 pack_tiled (grid gx x gy), -1 pack_weights
+static int pack_kind(const PackArgs& a, int& gx, int& gy) {
   // tiled when n is one weight index and the taps are contiguous in W
   if (a.fnco.d == (uint32_t)a.N && a.fnkw.d == 1 && a.s_kw == 1 && a.s_kh == a.KW && a.KH * a.KW <= 16 &&
       (!a.convt2 || (a.KH == 4 && a.KW == 4))) {
     if (a.KH == 4 && a.KW == 4 && a.fpci.d % PK_I == 0 && a.N % PK_O == 0 && a.s_in % 4 == 0 && a.s_out % 4 == 0 &&
-        aligned16(a.W) && aligned16(a.out))
-      pack_tiled16<<<dim3((int)a.fpci.d / PK_I, a.N / PK_O), 256, 0, s>>>(a);
-    else
-      pack_tiled<<<dim3(ceil_div((int)a.fpci.d, PK_I), ceil_div(a.N, PK_O)), 256, 0, s>>>(a);
+        aligned16(a.W) && aligned16(a.out)) {
+      gx = (int)a.fpci.d / PK_I;
+      gy = a.N / PK_O;
+      return 0;
+    }
+    gx = ceil_div((int)a.fpci.d, PK_I);
+    gy = ceil_div(a.N, PK_O);
+    return 1;
+  }
+  return -1;
+}
+
+static void launch_pack(const PackArgs& a, hipStream_t s) {
+  int gx, gy;
+  const int kind = pack_kind(a, gx, gy);
+  if (kind == 0) {
+    pack_tiled16<<<dim3(gx, gy), 256, 0, s>>>(a);
+    return;
+  }
+  if (kind == 1) {
+    pack_tiled<<<dim3(gx, gy), 256, 0, s>>>(a);
     return;
   }
   const int ny = std::min(a.N, 8192);
@@ -2920,6 +2967,47 @@ extern "C" int rgan_conv_pack(const RganConv* d, int which, const float* w, floa
   if (rc) return rc;
   if (!p.pack) return RGAN_EINVAL;
   launch_pack_plan(p, packed, (hipStream_t)stream);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int rgan_conv_pack_batch(int n, const RganConv* const* d, const int* which, const float* const* w,
+                                    float* const* packed, void* stream) {
+  if (n < 0 || (n > 0 && (!d || !which || !w || !packed))) return RGAN_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  alignas(16) static const float dummy[4] = {0, 0, 0, 0};
+  PackBatch b{};
+  long long blocks = 0;
+  auto flush = [&]() {
+    if (b.n == 0) return;
+    b.first[b.n] = (int)blocks;
+    pack_multi<<<(unsigned)blocks, 256, 0, s>>>(b);
+    b = PackBatch{};
+    blocks = 0;
+  };
+  for (int i = 0; i < n; ++i) {
+    if (!w[i] || !packed[i] || which[i] < 0 || which[i] > 1) return RGAN_EINVAL;
+    Plan p;
+    const int rc = which[i] == 0 ? plan_fwd(d[i], dummy, w[i], nullptr, nullptr, (float*)dummy, 0, 0.f, p)
+                                 : plan_dgrad(d[i], dummy, w[i], nullptr, (float*)dummy, p);
+    if (rc) return rc;
+    if (!p.pack) return RGAN_EINVAL;
+    int gx = 0, gy = 0;
+    const int kind = p.mode == MODE_NARROW_T ? -1 : (p.pk.out = packed[i], pack_kind(p.pk, gx, gy));
+    if (kind < 0) {  // narrow / generic layouts: their own launch
+      launch_pack_plan(p, packed[i], s);
+      RGAN_CHECK_LAUNCH();
+      continue;
+    }
+    if (b.n == PACK_BATCH || blocks + (long long)gx * gy >= (1LL << 30)) flush();
+    b.a[b.n] = p.pk;
+    b.kind[b.n] = kind;
+    b.gx[b.n] = gx;
+    b.first[b.n] = (int)blocks;
+    blocks += (long long)gx * gy;
+    ++b.n;
+  }
+  flush();
   RGAN_CHECK_LAUNCH();
   return 0;
 }

@@ -107,8 +107,35 @@ class _PackCache:
         reuse = ent is not None and ent[0]() is base and ent[2].numel() == n
         buf = ent[2] if reuse else torch.empty(n, dtype=torch.float32, device=w.device)
         L.check(lib.rgan_conv_pack(ctypes.byref(d), which, L.ptr(w), L.ptr(buf), L.stream()), "rgan_conv_pack")
-        self.entries[key] = (weakref.ref(base, self._drop(key)), ver, buf, w.data_ptr())
+        # (the descriptor, layout and a weak reference to w itself let refresh() repack it)
+        self.entries[key] = (weakref.ref(base, self._drop(key)), ver, buf, w.data_ptr(), d, which, weakref.ref(w))
         return buf
+
+    def refresh(self, params):
+        """Repack, in one batched launch, every cached layout of ``params`` whose weight
+        moved (called right after an optimizer step): the next convolutions find them
+        current instead of packing one launch at a time."""
+        ids = {id(p) for p in params}
+        todo = []
+        for key, ent in self.entries.items():
+            base, w = ent[0](), ent[6]()
+            if base is None or w is None or id(base) not in ids:
+                continue
+            if ent[1] == w._version and ent[3] == w.data_ptr():
+                continue
+            todo.append((key, ent, w))
+        if not todo:
+            return
+        n = len(todo)
+        descs = (ctypes.POINTER(L.RganConv) * n)(*[ctypes.pointer(e[4]) for _, e, _ in todo])
+        which = (ctypes.c_int * n)(*[e[5] for _, e, _ in todo])
+        ws = (ctypes.c_void_p * n)(*[w.data_ptr() for _, _, w in todo])
+        outs = (ctypes.c_void_p * n)(*[e[2].data_ptr() for _, e, _ in todo])
+        L.check(L.lib().rgan_conv_pack_batch(n, ctypes.cast(descs, ctypes.c_void_p), ctypes.cast(which, ctypes.c_void_p),
+                                             ctypes.cast(ws, ctypes.c_void_p), ctypes.cast(outs, ctypes.c_void_p),
+                                             L.stream()), "rgan_conv_pack_batch")
+        for key, ent, w in todo:
+            self.entries[key] = (ent[0], w._version, ent[2], w.data_ptr()) + ent[4:]
 
     def _drop(self, key):
         def cb(_ref):

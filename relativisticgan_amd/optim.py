@@ -4,15 +4,21 @@ A drop-in for ``torch.optim.Adam(params, lr, betas, weight_decay)`` as the refer
 uses it: the same param_groups and per-parameter state layout
 (``state[p] = {step, exp_avg, exp_avg_sq}``), so ``state_dict()`` / ``load_state_dict()``
 and ``torch.optim.lr_scheduler.ExponentialLR`` (GLI:533-534, 713-714) work unchanged.
-One launch updates every tensor of a param group (multi-tensor, one element per
-thread per iteration, 28 B/element of HBM traffic).  Hyper-parameters live in a
+One launch updates every tensor of a param group (multi-tensor, a size-proportional
+grid of 4096-element blocks, float4 loads, 28 B/element of HBM traffic); the cached GEMM
+layouts of the updated weights are then repacked in one batched launch.  Hyper-parameters live in a
 device buffer (doubles, as torch keeps them in Python floats), refreshed only when a
 group's values change; the step counter is a device scalar incremented by the kernel.
 """
+import os
+
 import torch
 from torch.autograd.graph import increment_version
 
 from . import kernels as K
+
+# RGAN_REFRESH_PACKS=0: leave repacking to the next convolution of each weight (A/B switch)
+REFRESH_PACKS = os.environ.get("RGAN_REFRESH_PACKS", "1") != "0"
 
 
 class Adam(torch.optim.Optimizer):
@@ -86,6 +92,8 @@ class Adam(torch.optim.Optimizer):
             for p in ps:
                 self.state[p]["step"] += 1  # host mirror of state['step'] (torch Adam's state_dict layout)
                 increment_version(p)        # the kernel wrote p: invalidate cached packed layouts
+            if REFRESH_PACKS:
+                K.PACKS.refresh(ps)  # ... and repack the ones in use, in one batched launch
         return loss
 
     def load_state_dict(self, state_dict):

@@ -683,3 +683,43 @@ def test_conv_image_window_kernel(K, ci, hw, cout):
     F.conv_transpose2d(x64, wt.double().cpu(), stride=2, padding=1).backward(gy.double().cpu())
     dx = K.conv_dgrad(gy, wt, gt, (B, 256, H // 2, W // 2))
     assert _rel(dx, x64.grad) < 3e-6
+
+
+def test_pack_batch_refresh(K):
+    """PACKS.refresh (one rgan_conv_pack_batch launch after an optimizer step) leaves every
+    cached layout bitwise equal to a fresh single pack: 4x4 tiled16 (fwd, ConvT phases),
+    3x3 tiled, the narrow-ConvT pack and > 16 layouts (two batches)."""
+    import ctypes
+    from relativisticgan_amd import _lib as L
+    torch.manual_seed(13)
+    g4, gt, g3 = K.ConvGeom(4, 2, 1, False), K.ConvGeom(4, 2, 1, True), K.ConvGeom(3, 1, 1, False)
+    ws, runs = [], []
+    for i in range(7):
+        w = torch.nn.Parameter(torch.randn(64, 32, 4, 4, device=DEV) * 0.1)
+        x = _nhwc(torch.randn(2, 32, 8, 8, device=DEV))
+        y = K.conv_fwd(x, w, g4, cache=True)
+        K.conv_dgrad(y, w, g4, x.shape, like=x, cache=True)
+        ws.append(w)
+    wt = torch.nn.Parameter(torch.randn(32, 64, 4, 4, device=DEV) * 0.1)
+    K.conv_fwd(_nhwc(torch.randn(2, 32, 8, 8, device=DEV)), wt, gt, cache=True)
+    w3 = torch.nn.Parameter(torch.randn(24, 20, 3, 3, device=DEV) * 0.1)
+    K.conv_fwd(_nhwc(torch.randn(2, 20, 8, 8, device=DEV)), w3, g3, cache=True)
+    wn = torch.nn.Parameter(torch.randn(32, 3, 4, 4, device=DEV) * 0.1)
+    K.conv_fwd(_nhwc(torch.randn(2, 32, 8, 8, device=DEV)), wn, gt, cache=True)
+    params = ws + [wt, w3, wn]
+    with torch.no_grad():
+        for p in params:
+            p.mul_(1.5).add_(0.25)  # an optimizer step: new values, new version
+    K.PACKS.refresh(params)
+    ids = {id(p) for p in params}
+    checked = 0
+    for ent in list(K.PACKS.entries.values()):
+        base, w = ent[0](), ent[6]()
+        if base is None or id(base) not in ids:
+            continue
+        assert ent[1] == w._version
+        fresh = torch.empty_like(ent[2])
+        L.check(L.lib().rgan_conv_pack(ctypes.byref(ent[4]), ent[5], L.ptr(w), L.ptr(fresh), L.stream()), "pack")
+        assert torch.equal(fresh, ent[2])
+        checked += 1
+    assert checked >= 17
