@@ -32,6 +32,9 @@ from . import kernels as K
 # bound by writing the 128-channel side).  False = narrow kernels / implicit GEMM throughout.
 PATCH_IMAGE_LAYERS = os.environ.get("RGAN_PATCH_IMAGE", "1") != "0"
 
+# RGAN_ACC_EPILOGUE=0: leave repeated weight-gradient contributions to autograd's add (A/B)
+ACCUMULATE_IN_EPILOGUE = os.environ.get("RGAN_ACC_EPILOGUE", "1") != "0"
+
 ACT_TRACE = None
 ACT_TAGS = []      # per ACT_TRACE entry: the net that produced it ("G" / "D", set by nets._Net)
 ACT_LAYERS = []    # per ACT_TRACE entry: the layer's index in the net's plan
@@ -288,6 +291,18 @@ class ConvLayerFn(torch.autograd.Function):
         else:
             dx = K.conv_dgrad(dy, w, spec.geom, tuple(x.shape), wscale=wscale, like=x, cache=True) if nx else None
             dw = db = None
+            if nw and not nb and spec.geom.upsample == 1 and ConvLayerFn._accumulate_into_grad(w, bias):
+                # a second call of the net in this backward (spectral D's D(x) and D(G(z)),
+                # heads 1-4 of the reference's two backwards): add into the .grad the first
+                # one left, in the GEMM epilogue / sigma correction, instead of autograd's add
+                # pass (same values: grad + dw, one rounding); no gradient is returned
+                if spec.spectral:
+                    u, v, inv_sigma = sn
+                    dwe, _ = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape))
+                    K.spectral_backward(w, dwe, u, v, inv_sigma, spec.geom.transposed, out=w.grad)
+                else:
+                    K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), out=w.grad)
+                return dx, None, None, dgamma, dbeta, None, None, None, None, None
             if nw or nb:
                 dw, db = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), with_bias=bias is not None and nb)
         if nw or nb:
@@ -297,6 +312,16 @@ class ConvLayerFn(torch.autograd.Function):
             if not nw:
                 dw = None
         return dx, dw, db, dgamma, dbeta, None, None, None, None, None
+
+    @staticmethod
+    def _accumulate_into_grad(w, bias):
+        """w.grad can take this call's weight gradient in place of autograd's add: one
+        process (no gradient-bucket hooks waiting on AccumulateGrad), a plain contiguous
+        fp32 .grad of w's shape, and no bias gradient to accumulate alongside."""
+        g = w.grad
+        return (ACCUMULATE_IN_EPILOGUE and not dp.active() and g is not None and bias is None
+                and g.shape == w.shape and g.dtype == torch.float32 and g.is_contiguous()
+                and not g.requires_grad and g.device == w.device)
 
     @staticmethod
     def _patch_conv(spec, x):
