@@ -548,22 +548,9 @@ __global__ __launch_bounds__(256) void sn_batch_u(SnBatch b) {
   const SnView& w = b.w[l];
   const int tid = threadIdx.x;
   const float* t = b.t[l];
-  // ||t|| from V2's per-block sums (the same fixed order in every block)
-  const float tsq = snb_sum_parts(b.sq[l], b.nt[l]);
-  if (tid == 0) den_s = fmaxf(sqrtf(tsq), b.eps);
-  __syncthreads();
-  const float den = den_s;
-  // this block's slice of v = t / max(||t||, eps)
-  {
-    const int per = (w.cols + nblk - 1) / nblk, c0 = row * per, c1 = min(w.cols, c0 + per);
-    float* v2 = b.v2[l];
-    for (int c = c0 + tid; c < c1; c += blockDim.x) {
-      const float x = t[c] / den;
-      b.v[l][c] = x;
-      if (v2) v2[c] = x;
-    }
-  }
-  // w[row] = (W t)[row] / ||t||: the block's 256 threads split the row, 8 float4 in flight each
+  // w[row] = (W t)[row] / ||t||: the block's 256 threads split the row, 8 float4 in flight
+  // each.  The row loads go out first: ||t|| (a sum of V2's partials) and the v slice only
+  // scale the result, so their round trips overlap the row's instead of preceding it.
   float s = 0.f;
   if (b.vec[l] && w.lo < w.cols && w.lo == 16) {
     // dim-1 (ConvTranspose) view: runs of 16 contiguous columns at row * rs + ch * hs
@@ -599,8 +586,22 @@ __global__ __launch_bounds__(256) void sn_batch_u(SnBatch b) {
   } else {
     for (int c = tid; c < w.cols; c += 256) s += w.W[w.off(row, c)] * t[c];
   }
-  s = block_sum(s, red) / den;  // (W t) / ||t|| = W v
-  if (tid == 0) b.wv[l][row] = s;
+  // ||t|| from V2's per-block sums (the same fixed order in every block)
+  const float tsq = snb_sum_parts(b.sq[l], b.nt[l]);
+  if (tid == 0) den_s = fmaxf(sqrtf(tsq), b.eps);
+  s = block_sum(s, red);  // (its barriers also publish den_s)
+  const float den = den_s;
+  // this block's slice of v = t / max(||t||, eps)
+  {
+    const int per = (w.cols + nblk - 1) / nblk, c0 = row * per, c1 = min(w.cols, c0 + per);
+    float* v2 = b.v2[l];
+    for (int c = c0 + tid; c < c1; c += blockDim.x) {
+      const float x = t[c] / den;
+      b.v[l][c] = x;
+      if (v2) v2[c] = x;
+    }
+  }
+  if (tid == 0) b.wv[l][row] = s / den;  // (W t) / ||t|| = W v
 }
 
 // one block per layer: u = w / max(||w||, eps), sigma = u . w (fixed-order sums).  A launch
