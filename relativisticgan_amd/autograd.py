@@ -35,6 +35,20 @@ PATCH_IMAGE_LAYERS = os.environ.get("RGAN_PATCH_IMAGE", "1") != "0"
 # RGAN_ACC_EPILOGUE=0: leave repeated weight-gradient contributions to autograd's add (A/B)
 ACCUMULATE_IN_EPILOGUE = os.environ.get("RGAN_ACC_EPILOGUE", "1") != "0"
 
+
+class owning_grads:
+    """Context of a ``loss.backward()`` whose weight gradients the layers may write into
+    ``.grad`` themselves (train.Trainer wraps its backwards in it).  Outside it -- e.g. a
+    ``torch.autograd.grad`` call, which must not touch ``.grad`` -- autograd's own
+    accumulation is used."""
+    active = False
+
+    def __enter__(self):
+        self.prev, owning_grads.active = owning_grads.active, True
+
+    def __exit__(self, *exc):
+        owning_grads.active = self.prev
+
 ACT_TRACE = None
 ACT_TAGS = []      # per ACT_TRACE entry: the net that produced it ("G" / "D", set by nets._Net)
 ACT_LAYERS = []    # per ACT_TRACE entry: the layer's index in the net's plan
@@ -291,17 +305,22 @@ class ConvLayerFn(torch.autograd.Function):
         else:
             dx = K.conv_dgrad(dy, w, spec.geom, tuple(x.shape), wscale=wscale, like=x, cache=True) if nx else None
             dw = db = None
-            if nw and not nb and spec.geom.upsample == 1 and ConvLayerFn._accumulate_into_grad(w, bias):
-                # a second call of the net in this backward (spectral D's D(x) and D(G(z)),
-                # heads 1-4 of the reference's two backwards): add into the .grad the first
-                # one left, in the GEMM epilogue / sigma correction, instead of autograd's add
-                # pass (same values: grad + dw, one rounding); no gradient is returned
+            if nw and not nb and spec.geom.upsample == 1 and ConvLayerFn._own_grad(w, bias):
+                # The weight gradient goes straight into w.grad: set when it is empty (what
+                # AccumulateGrad would do), added in the GEMM epilogue / sigma correction when
+                # an earlier call of the net left one (spectral D's separate D(x) / D(G(z))
+                # calls, heads 1-4's two backwards) -- instead of autograd summing the calls'
+                # gradients with an add kernel (same values: grad + dw, one rounding).  No
+                # gradient is returned for w.
+                acc = w.grad
                 if spec.spectral:
                     u, v, inv_sigma = sn
                     dwe, _ = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape))
-                    K.spectral_backward(w, dwe, u, v, inv_sigma, spec.geom.transposed, out=w.grad)
+                    g = K.spectral_backward(w, dwe, u, v, inv_sigma, spec.geom.transposed, out=acc)
                 else:
-                    K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), out=w.grad)
+                    g, _ = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), out=acc)
+                if acc is None:
+                    w.grad = g
                 return dx, None, None, dgamma, dbeta, None, None, None, None, None
             if nw or nb:
                 dw, db = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), with_bias=bias is not None and nb)
@@ -314,14 +333,15 @@ class ConvLayerFn(torch.autograd.Function):
         return dx, dw, db, dgamma, dbeta, None, None, None, None, None
 
     @staticmethod
-    def _accumulate_into_grad(w, bias):
-        """w.grad can take this call's weight gradient in place of autograd's add: one
-        process (no gradient-bucket hooks waiting on AccumulateGrad), a plain contiguous
-        fp32 .grad of w's shape, and no bias gradient to accumulate alongside."""
+    def _own_grad(w, bias):
+        """This call may write its weight gradient into w.grad itself: one process (no
+        gradient-bucket hooks waiting on AccumulateGrad), w a leaf, no bias gradient to
+        accumulate alongside, and .grad empty or a plain contiguous fp32 tensor of w's shape."""
+        if not (ACCUMULATE_IN_EPILOGUE and owning_grads.active and not dp.active() and w.is_leaf and bias is None):
+            return False
         g = w.grad
-        return (ACCUMULATE_IN_EPILOGUE and not dp.active() and g is not None and bias is None
-                and g.shape == w.shape and g.dtype == torch.float32 and g.is_contiguous()
-                and not g.requires_grad and g.device == w.device)
+        return g is None or (g.shape == w.shape and g.dtype == torch.float32 and g.is_contiguous()
+                             and not g.requires_grad and g.device == w.device)
 
     @staticmethod
     def _patch_conv(spec, x):

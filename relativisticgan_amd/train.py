@@ -18,7 +18,7 @@ import time
 import numpy
 import torch
 
-from . import dp
+from . import autograd, dp
 from .config import TITLES, parse
 from .losses import gradient_penalty, loss_D, loss_D_cat, loss_D_fake, loss_D_real, loss_G
 from .nets import DCGAN_D, DCGAN_G, weights_init
@@ -164,7 +164,8 @@ class Trainer:
         one = self._one
         if one is None or one.device != loss.device:
             one = self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
-        loss.backward(one)
+        with autograd.owning_grads():  # the fused layers write their weight .grad directly
+            loss.backward(one)
 
     def _set_D_grad(self, flag):
         for q in self.D.parameters():
