@@ -351,6 +351,17 @@ int rgan_set_gemm_emulation(int on);
 /* Library self-description: number of exported compute entry points, version string. */
 const char* rgan_version(void);
 
+/* Device sampling (--rgan_rng device; replaces the draws of GLI:176,608,630,648-649,674):
+ * Philox-4x32-10 keyed by `seed` at the device counter *counter, which the call advances
+ * on the stream by the numbers it used (graph-replay safe).
+ * rgan_rng_fill: out[0..n) ~ N(0, 1) (kind 0, Box-Muller) or U[0, 1) (kind 1).
+ * rgan_rng_choice: n <= 4096 distinct indices of [0, N) (numpy.random.choice(N, n,
+ * replace=False)'s distribution; Floyd's algorithm on one wave), int64. */
+int rgan_rng_fill(float* out, long long n, int kind, unsigned long long seed, unsigned long long* counter,
+                  void* stream);
+int rgan_rng_choice(long long* out, int N, int n, unsigned long long seed, unsigned long long* counter,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

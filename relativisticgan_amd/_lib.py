@@ -96,6 +96,8 @@ _SIGS = {
     "rgan_adam": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "rgan_lr_decay": (c_int, [c_vp, c_d, c_vp]),
     "rgan_gather_images": (c_int, [c_vp, c_vp, c_int, c_ll, c_vp, c_vp]),
+    "rgan_rng_fill": (c_int, [c_vp, c_ll, c_int, ctypes.c_ulonglong, c_vp, c_vp]),
+    "rgan_rng_choice": (c_int, [c_vp, c_int, c_int, ctypes.c_ulonglong, c_vp, c_vp]),
     "rgan_set_gemm_emulation": (c_int, [c_int]),
     "rgan_profile_begin": (c_int, [c_int]),
     "rgan_profile_end": (c_int, [c_vp, c_vp, c_vp]),

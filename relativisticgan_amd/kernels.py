@@ -746,6 +746,35 @@ def spectral_backward(w, dw_eff, u, v, inv_sigma, transposed, out=None):
     return dw
 
 
+# ------------------------------------------------------------------ device sampling
+class DeviceRNG:
+    """Counter-based device draws for --rgan_rng device (rgan_rng_fill / rgan_rng_choice):
+    the counter is a device int64 the kernels advance, so graph replays draw fresh values."""
+
+    def __init__(self, seed, device):
+        self.seed = (int(seed) * 0x9E3779B97F4A7C15 + 0x632BE59BD9B4E019) & ((1 << 64) - 1)
+        self.counter = torch.zeros(1, dtype=torch.int64, device=device)
+
+    def normal(self, shape):
+        out = torch.empty(shape, dtype=torch.float32, device=self.counter.device)
+        L.check(L.lib().rgan_rng_fill(L.ptr(out), out.numel(), 0, self.seed, L.ptr(self.counter), L.stream()),
+                "rgan_rng_fill")
+        return out
+
+    def uniform(self, shape):
+        out = torch.empty(shape, dtype=torch.float32, device=self.counter.device)
+        L.check(L.lib().rgan_rng_fill(L.ptr(out), out.numel(), 1, self.seed, L.ptr(self.counter), L.stream()),
+                "rgan_rng_fill")
+        return out
+
+    def choice(self, N, n):
+        """n distinct indices of [0, N) (numpy.random.choice(N, n, replace=False))."""
+        out = torch.empty(n, dtype=torch.int64, device=self.counter.device)
+        L.check(L.lib().rgan_rng_choice(L.ptr(out), int(N), int(n), self.seed, L.ptr(self.counter), L.stream()),
+                "rgan_rng_choice")
+        return out
+
+
 # ------------------------------------------------------------------ Adam / data
 def adam(params, grads, exp_avgs, exp_avg_sqs, hyper, step):
     n = len(params)

@@ -20,6 +20,7 @@ import torch
 
 from . import autograd, dp
 from .config import TITLES, parse
+from .kernels import DeviceRNG
 from .losses import gradient_penalty, loss_D, loss_D_cat, loss_D_fake, loss_D_real, loss_G
 from .nets import DCGAN_D, DCGAN_G, weights_init
 from .optim import Adam
@@ -83,6 +84,9 @@ class Trainer:
         self.redG = dp.GradReducer(self.G.parameters()) if self.world > 1 else None
         self._pending_G, self._pending_decay_G = None, False
         self.host_rng = getattr(p, "rgan_rng", "host") == "host"
+        # --rgan_rng device: counter-based draws in HIP kernels (same seed on every rank)
+        self.dev_rng = (None if self.host_rng or self.device.type != "cuda" else
+                        DeviceRNG(p.seed if p.seed is not None else torch.initial_seed(), self.device))
         self.pac = getattr(p, "pac", 1)  # 2: code/GAN_losses_iter_PAC.py
         # one batched D pass per D step where the nets allow it (--rgan_batch_D).  Default
         # (auto): single process only -- under DP the separate D(x) forward is what hides
@@ -123,7 +127,7 @@ class Trainer:
             idx = numpy.random.choice(self.images.shape[0], size=n, replace=False)
             idx = self._shard_pac(torch.from_numpy(idx.astype(numpy.int64))).to(self.device, non_blocking=True)
         else:
-            idx = self._shard_pac(torch.randperm(self.images.shape[0], device=self.device)[:n])
+            idx = self._shard_pac(self.dev_rng.choice(self.images.shape[0], n))
         return self._pack(gather_images(self.images, idx, out=out if self.pac == 1 else None))
 
     def _normal(self, feed, key, shape):
@@ -133,14 +137,14 @@ class Trainer:
             return self._shard_pac(torch.empty(shape).normal_(0, 1)).to(self.device, non_blocking=True)
         # every rank draws the global batch from the same device generator and keeps its
         # shard: ranks see different z, and the union is the 1-process draw
-        return self._shard_pac(torch.randn(shape, device=self.device))
+        return self._shard_pac(self.dev_rng.normal(shape))
 
     def _uniform(self, feed, key, shape):
         if feed is not None and key in feed:
             return feed[key]
         if self.host_rng:
             return self._shard(torch.empty(shape).uniform_(0, 1)).to(self.device, non_blocking=True)
-        return self._shard(torch.rand(shape, device=self.device))
+        return self._shard(self.dev_rng.uniform(shape))
 
     def _generate_D(self, z, out=None):
         """The D step's fake batch.  Single samples: G(z) without a graph (GLI copies it into

@@ -723,3 +723,34 @@ def test_pack_batch_refresh(K):
         assert torch.equal(fresh, ent[2])
         checked += 1
     assert checked >= 17
+
+
+def test_device_rng(K):
+    """--rgan_rng device draws: N(0,1) / U[0,1) moments, distinct in-range batch indices, the
+    device counter advancing (fresh draws per call, the same sequence for the same seed --
+    every data-parallel rank draws the global batch), and fresh draws per HIP-graph replay."""
+    a, b = K.DeviceRNG(7, DEV), K.DeviceRNG(7, DEV)
+    z = a.normal((400, 1000))
+    assert abs(z.mean().item()) < 0.01 and abs(z.std().item() - 1) < 0.01 and torch.isfinite(z).all()
+    u = a.uniform((1000, 1001))
+    assert u.min().item() >= 0 and u.max().item() < 1 and abs(u.mean().item() - 0.5) < 0.01
+    idx = a.choice(1000, 64)
+    assert idx.unique().numel() == 64 and idx.min().item() >= 0 and idx.max().item() < 1000
+    full = a.choice(50, 50)
+    assert sorted(full.tolist()) == list(range(50))
+    assert torch.equal(b.normal((400, 1000)), z)  # same seed, same counter: same draws
+    assert not torch.equal(b.normal((400, 1000)), z)  # the counter moved
+    counts = torch.zeros(20, device=DEV)
+    for _ in range(200):
+        counts.index_add_(0, a.choice(20, 5), torch.ones(5, device=DEV))
+    assert counts.min().item() > 20 and counts.max().item() < 80  # ~50 each
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            zz = a.normal((16,))
+    g.replay()
+    first = zz.clone()
+    g.replay()
+    assert not torch.equal(first, zz)
