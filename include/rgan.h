@@ -161,6 +161,15 @@ int rgan_bn_stats(const float* y, long long P, int C, long long sp, long long sc
 int rgan_bn_segment_stats(const double* part, long long s0, long long s1, int C, int seg_rows,
                           float eps, float momentum, float* running_mean, float* running_var,
                           long long* num_batches_tracked, float* stats, double* moments, void* stream);
+/* The batched D pass's two calls (GLI:580-605 run D(x) then D(x_fake)) in one launch each:
+ * segment stats of the nseg (1 or 2) equal halves of segments [s0, s1) -> stats[nseg][2C],
+ * running statistics updated in call order; and the normalisation + activation of y's nseg
+ * equal row ranges with their stats rows (dense NHWC y and a, P % nseg == 0). */
+int rgan_bn_segment_stats_n(const double* part, long long s0, long long s1, int nseg, int C, int seg_rows,
+                            float eps, float momentum, float* running_mean, float* running_var,
+                            long long* num_batches_tracked, float* stats, void* stream);
+int rgan_bn_apply_segments(const float* y, long long P, int C, int nseg, const float* stats, const float* gamma,
+                           const float* beta, int act, float act_alpha, float* a, void* stream);
 /* a = act(gamma * (y - mean) * invstd + beta)  (torch's alpha/beta form) */
 int rgan_bn_apply(const float* y, long long P, int C, long long sp, long long sc,
                   const float* stats, const float* gamma, const float* beta,

@@ -41,6 +41,9 @@ _SIGS = {
     "rgan_conv_bn_segments": (c_ll, [ctypes.POINTER(RganConv), c_int]),
     "rgan_conv_fwd_bn": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp,
                                  c_ll, c_int, ctypes.POINTER(c_int), c_vp]),
+    "rgan_bn_segment_stats_n": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_f, c_f, c_vp, c_vp, c_vp, c_vp,
+                                        c_vp]),
+    "rgan_bn_apply_segments": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_f, c_vp, c_vp]),
     "rgan_bn_segment_stats": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp]),
     "rgan_conv_dgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),

@@ -36,6 +36,10 @@ PATCH_IMAGE_LAYERS = os.environ.get("RGAN_PATCH_IMAGE", "1") != "0"
 ACCUMULATE_IN_EPILOGUE = os.environ.get("RGAN_ACC_EPILOGUE", "1") != "0"
 
 
+# RGAN_SEG_FUSED=0: the batched pass's per-call BatchNorm one call at a time (A/B switch)
+SEG_FUSED = os.environ.get("RGAN_SEG_FUSED", "1") != "0"
+
+
 class owning_grads:
     """Context of a ``loss.backward()`` whose weight gradients the layers may write into
     ``.grad`` themselves (train.Trainer wraps its backwards in it).  Outside it -- e.g. a
@@ -217,11 +221,18 @@ class ConvLayerFn(torch.autograd.Function):
                 Bs = y.shape[0] // segs
                 a = torch.empty_like(y) if out is None else out
                 stats = torch.empty((segs, 2 * C), dtype=torch.float32, device=y.device)
-                for s_ in range(segs):
-                    sl = slice(s_ * Bs, (s_ + 1) * Bs)
-                    seg = (part, s_ * S // segs, (s_ + 1) * S // segs) if part is not None else None
-                    _train_stats(y[sl], spec, rm, rv, nbt, seg, out=stats[s_])
-                    K.bn_apply(y[sl], stats[s_], gamma, beta, spec.act, spec.alpha, out=a[sl])
+                if (SEG_FUSED and part is not None and segs == 2 and S % 2 == 0 and not dp.sync_bn() and K.is_nhwc(y)
+                        and K.is_nhwc(a) and y.data_ptr() % 16 == 0 and a.data_ptr() % 16 == 0 and C % 4 == 0):
+                    # both calls' statistics (running stats in call order) and normalisation,
+                    # one launch each
+                    K.bn_segment_stats_n(part, S, 2, C, spec.eps, spec.momentum, rm, rv, nbt, out=stats)
+                    K.bn_apply_segments(y, stats, gamma, beta, spec.act, spec.alpha, out=a)
+                else:
+                    for s_ in range(segs):
+                        sl = slice(s_ * Bs, (s_ + 1) * Bs)
+                        seg = (part, s_ * S // segs, (s_ + 1) * S // segs) if part is not None else None
+                        _train_stats(y[sl], spec, rm, rv, nbt, seg, out=stats[s_])
+                        K.bn_apply(y[sl], stats[s_], gamma, beta, spec.act, spec.alpha, out=a[sl])
             else:
                 if training:
                     stats = _train_stats(y, spec, rm, rv, nbt, (part, 0, S) if part is not None else None)

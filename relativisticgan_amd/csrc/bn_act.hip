@@ -218,14 +218,21 @@ __global__ __launch_bounds__(1024) void bn_merge(const double* __restrict__ part
 //   FIN 2: (mean, invstd) stats + running-stat update, as bn_merge<2>
 constexpr int SEG_CPB = 4, SEG_LANES = 256;
 
-template <int FIN>
-__global__ __launch_bounds__(1024) void bn_seg_merge(const double* __restrict__ part, long long s0, long long s1,
-                                                     int C, double seg_n, double* __restrict__ out, float eps,
-                                                     float momentum, float* running_mean, float* running_var,
-                                                     long long* nbt, float* stats) {
+// NSEG > 1 (FIN 2): the batch segments [s0 + k L, s0 + (k+1) L), L = (s1 - s0) / NSEG, of
+// the batched D pass, one after the other in one launch: stats[k][2C], running statistics
+// updated in segment order (as NSEG separate calls would).
+template <int FIN, int NSEG = 1>
+__global__ __launch_bounds__(1024) void bn_seg_merge(const double* __restrict__ part, long long s0_all,
+                                                     long long s1_all, int C, double seg_n, double* __restrict__ out,
+                                                     float eps, float momentum, float* running_mean,
+                                                     float* running_var, long long* nbt, float* stats) {
   __shared__ double sh[2][SEG_LANES][SEG_CPB];
   const int cl = threadIdx.x % SEG_CPB, r = threadIdx.x / SEG_CPB;
   const int c = blockIdx.x * SEG_CPB + cl;
+  const long long seg_len = (s1_all - s0_all) / NSEG;
+  for (int sg = 0; sg < NSEG; ++sg) {
+  const long long s0 = s0_all + sg * seg_len, s1 = s0 + seg_len;
+  if (sg > 0) __syncthreads();  // the previous segment's tree reads are done
   double a1 = 0.0, a2 = 0.0;
   if (c < C) {
     long long k = s0 + r;
@@ -257,23 +264,43 @@ __global__ __launch_bounds__(1024) void bn_seg_merge(const double* __restrict__ 
   if constexpr (FIN == 2) {
     if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) nbt[0] += 1;
   }
-  if (r != 0 || c >= C) return;
-  const double n = seg_n * (double)(s1 - s0), S1 = sh[0][0][cl], S2 = sh[1][0][cl];
-  const double mean = S1 / n, m2 = fmax(S2 - S1 * mean, 0.0);
-  if constexpr (FIN == 1) {
-    out[c] = n;
-    out[C + c] = mean;
-    out[2 * C + c] = m2;
-  } else {
-    const double var = m2 / n;
-    stats[c] = (float)mean;
-    stats[C + c] = (float)(1.0 / sqrt(var + (double)eps));
-    if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
-    if (running_var) {
-      const float unb = n > 1.0 ? (float)(m2 / (n - 1.0)) : (float)var;
-      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+  if (r == 0 && c < C) {
+    const double n = seg_n * (double)(s1 - s0), S1 = sh[0][0][cl], S2 = sh[1][0][cl];
+    const double mean = S1 / n, m2 = fmax(S2 - S1 * mean, 0.0);
+    if constexpr (FIN == 1) {
+      out[c] = n;
+      out[C + c] = mean;
+      out[2 * C + c] = m2;
+    } else {
+      const double var = m2 / n;
+      float* st = stats + (size_t)sg * 2 * C;
+      st[c] = (float)mean;
+      st[C + c] = (float)(1.0 / sqrt(var + (double)eps));
+      if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+      if (running_var) {
+        const float unb = n > 1.0 ? (float)(m2 / (n - 1.0)) : (float)var;
+        running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+      }
     }
   }
+  }  // segments
+}
+
+extern "C" int rgan_bn_segment_stats_n(const double* part, long long s0, long long s1, int nseg, int C, int seg_rows,
+                                       float eps, float momentum, float* running_mean, float* running_var,
+                                       long long* num_batches_tracked, float* stats, void* stream) {
+  RGAN_REQUIRE(part && s1 > s0 && s0 >= 0 && C > 0 && seg_rows > 0 && stats && (nseg == 1 || nseg == 2) &&
+               (s1 - s0) % nseg == 0);
+  const hipStream_t s = (hipStream_t)stream;
+  const int blocks = ceil_div(C, SEG_CPB);
+  if (nseg == 1)
+    bn_seg_merge<2, 1><<<blocks, 1024, 0, s>>>(part, s0, s1, C, (double)seg_rows, nullptr, eps, momentum,
+                                               running_mean, running_var, num_batches_tracked, stats);
+  else
+    bn_seg_merge<2, 2><<<blocks, 1024, 0, s>>>(part, s0, s1, C, (double)seg_rows, nullptr, eps, momentum,
+                                               running_mean, running_var, num_batches_tracked, stats);
+  RGAN_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int rgan_bn_segment_stats(const double* part, long long s0, long long s1, int C, int seg_rows,
@@ -362,27 +389,33 @@ extern "C" int rgan_bn_stats(const float* y, long long P, int C, long long sp, l
 
 // ------------------------------------------------------------------ apply
 // per-thread fixed channel quad (blockIdx.x = channel group); pixels strided over blockIdx.y
-template <int Q>
+// NSEG 2: rows [0, seg_rows) normalised with stats[0], the rest with stats[1] ([2][2C]: the
+// batched D pass's two calls in one launch)
+template <int Q, int NSEG = 1>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__ y, long long P, int C,
                                                        long long sp, long long sc, const float* __restrict__ stats,
                                                        const float* __restrict__ gamma,
                                                        const float* __restrict__ beta, int act, float alpha,
                                                        float* __restrict__ a, long long asp, long long asc,
-                                                       int tpr) {
+                                                       int tpr, long long seg_rows = 0) {
   const int tid = threadIdx.x, lc = tid % tpr, rl = tid / tpr, rp = blockDim.x / tpr;
   const int c0 = (blockIdx.x * tpr + lc) * Q;
   if (c0 >= C) return;
-  float al[Q], be[Q];
+  float al_s[NSEG][Q], be_s[NSEG][Q];
 #pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int c = min(c0 + q, C - 1);
-    al[q] = (gamma ? gamma[c] : 1.f) * stats[C + c];
-    be[q] = (beta ? beta[c] : 0.f) - stats[c] * al[q];
-  }
+  for (int sg = 0; sg < NSEG; ++sg)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int c = min(c0 + q, C - 1);
+      const float* st = stats + (size_t)sg * 2 * C;
+      al_s[sg][q] = (gamma ? gamma[c] : 1.f) * st[C + c];
+      be_s[sg][q] = (beta ? beta[c] : 0.f) - st[c] * al_s[sg][q];
+    }
   const long long step = (long long)gridDim.y * rp;
   auto out = [&](long long p, float (&v)[Q]) {
+    const int sg = NSEG > 1 && p >= seg_rows ? 1 : 0;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) v[q] = act_fwd(v[q] * al[q] + be[q], act, alpha);
+    for (int q = 0; q < Q; ++q) v[q] = act_fwd(v[q] * al_s[sg][q] + be_s[sg][q], act, alpha);
     if constexpr (Q == 4) {
       *reinterpret_cast<float4*>(a + p * asp + c0) = make_float4(v[0], v[1], v[2], v[3]);
     } else {
@@ -416,6 +449,24 @@ static dim3 apply_grid(const BnGeo& g, long long P) {
   const long long rb = std::max<long long>(
       1, std::min<long long>((P + g.rp * min_iter - 1) / (g.rp * min_iter), std::max<long long>(1, blocks / g.cgroups)));
   return dim3(g.cgroups, (unsigned)rb);
+}
+
+extern "C" int rgan_bn_apply_segments(const float* y, long long P, int C, int nseg, const float* stats,
+                                      const float* gamma, const float* beta, int act, float act_alpha, float* a,
+                                      void* stream) {
+  // dense NHWC y and a, P % nseg == 0; stats [nseg][2C]
+  RGAN_REQUIRE(y && stats && a && P > 0 && C > 0 && (nseg == 1 || nseg == 2) && P % nseg == 0);
+  hipStream_t s = (hipStream_t)stream;
+  BnGeo g = bn_geo(P, C, C, 1);
+  RGAN_REQUIRE(g.vec && ((uintptr_t)y & 15) == 0 && ((uintptr_t)a & 15) == 0);
+  if (nseg == 1)
+    bn_apply_kernel<4, 1><<<apply_grid(g, P), 256, 0, s>>>(y, P, C, C, 1, stats, gamma, beta, act, act_alpha, a, C,
+                                                          1, g.tpr, 0);
+  else
+    bn_apply_kernel<4, 2><<<apply_grid(g, P), 256, 0, s>>>(y, P, C, C, 1, stats, gamma, beta, act, act_alpha, a, C,
+                                                          1, g.tpr, P / 2);
+  RGAN_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int rgan_bn_apply(const float* y, long long P, int C, long long sp, long long sc,

@@ -468,6 +468,25 @@ def bn_backward_apply(da, y, stats, gamma, beta, act, alpha, sums, P_global, nee
     return dy, dgamma, dbeta
 
 
+def bn_segment_stats_n(part, S, nseg, C, eps, momentum, running_mean, running_var, num_batches_tracked, out):
+    """bn_segment_stats of the nseg equal batch segments of [0, S) in one launch: out[nseg][2C],
+    running statistics updated in segment order."""
+    L.check(L.lib().rgan_bn_segment_stats_n(L.ptr(part), 0, int(S), int(nseg), C, 64, float(eps), float(momentum),
+                                            L.ptr(running_mean), L.ptr(running_var), L.ptr(num_batches_tracked),
+                                            L.ptr(out), L.stream()), "rgan_bn_segment_stats_n")
+    return out
+
+
+def bn_apply_segments(y, stats, gamma, beta, act, alpha, out):
+    """bn_apply of y's nseg = stats.shape[0] equal batch segments, each with its stats row,
+    in one launch (dense NHWC y and out)."""
+    P, C, _, _ = _pc(y)
+    L.check(L.lib().rgan_bn_apply_segments(L.ptr(y), P, C, stats.shape[0], L.ptr(stats), L.ptr(gamma), L.ptr(beta),
+                                           L.ACT[act], float(alpha), L.ptr(out), L.stream()),
+            "rgan_bn_apply_segments")
+    return out
+
+
 def bn_apply(y, stats, gamma, beta, act="none", alpha=0.0, out=None):
     P, C, sp, sc = _pc(y)
     if out is None:

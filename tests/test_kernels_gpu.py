@@ -754,3 +754,30 @@ def test_device_rng(K):
     first = zz.clone()
     g.replay()
     assert not torch.equal(first, zz)
+
+
+def test_bn_two_segments_one_launch(K):
+    """rgan_bn_segment_stats_n + rgan_bn_apply_segments (the batched D pass's two calls in
+    one launch each) == the two calls one at a time, bitwise, incl. the running statistics."""
+    from relativisticgan_amd.kernels import ConvGeom
+    torch.manual_seed(17)
+    g = ConvGeom(4, 2, 1, False)
+    x = _nhwc(torch.randn(16, 32, 32, 32, device=DEV))
+    w = torch.randn(128, 32, 4, 4, device=DEV) * 0.05
+    y, part, S = K.conv_fwd_bn(x, w, g, segs=2)
+    assert part is not None
+    C = 128
+    gamma, beta = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    rm1, rv1, n1 = torch.randn(C, device=DEV), torch.rand(C, device=DEV) + 0.5, torch.zeros((), dtype=torch.long, device=DEV)
+    rm2, rv2, n2 = rm1.clone(), rv1.clone(), n1.clone()
+    st1 = torch.empty(2, 2 * C, device=DEV)
+    a1 = torch.empty_like(y)
+    for k in range(2):
+        sl = slice(8 * k, 8 * (k + 1))
+        K.bn_segment_stats(part, k * S // 2, (k + 1) * S // 2, C, 1e-5, 0.1, rm1, rv1, n1, out=st1[k])
+        K.bn_apply(y[sl], st1[k], gamma, beta, "lrelu", 0.2, out=a1[sl])
+    st2 = torch.empty(2, 2 * C, device=DEV)
+    K.bn_segment_stats_n(part, S, 2, C, 1e-5, 0.1, rm2, rv2, n2, out=st2)
+    a2 = K.bn_apply_segments(y, st2, gamma, beta, "lrelu", 0.2, out=torch.empty_like(y))
+    assert torch.equal(st1, st2) and torch.equal(a1, a2)
+    assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2) and int(n2.item()) == 2
