@@ -1365,6 +1365,32 @@ __global__ __launch_bounds__(256) void pack_weights(PackArgs a) {
   }
 }
 
+// G's 1x1 -> KH x KW first layer (a plain GEMM over z): W[ci][co][tap] contiguous ->
+// out[tap * Cout + co][ci] -- a 2-D transpose of [K][N] with the (co, tap) -> (tap, co)
+// column permutation.  pack_weights reads that layout a float per 128-B line (one column
+// of a K x N matrix per block); here a block moves a 32 (ci) x 128 (co, tap) brick through
+// LDS, loaded as float4 rows, stored as 128-B ci runs.
+constexpr int PT_K = 32, PT_N = 128;
+__global__ __launch_bounds__(256) void pack_t2d(PackArgs a) {
+  __shared__ float t[PT_K][PT_N + 1];
+  const int T = a.KH * a.KW, Cout = (int)a.fnco.d;
+  const int k0 = blockIdx.y * PT_K, j0 = blockIdx.x * PT_N;
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (tid >> 5) + 8 * i, c = 4 * (tid & 31);
+    const float4 v = *reinterpret_cast<const float4*>(a.W + (size_t)(k0 + r) * a.N + j0 + c);
+    t[r][c] = v.x; t[r][c + 1] = v.y; t[r][c + 2] = v.z; t[r][c + 3] = v.w;
+  }
+  __syncthreads();
+  const int jl = tid >> 1, h = tid & 1, j = j0 + jl;
+  const int co = j / T, tap = j - co * T;
+  float* dst = a.out + (size_t)(tap * Cout + co) * a.K + k0 + 16 * h;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    *reinterpret_cast<float4*>(dst + 4 * q) = make_float4(t[16 * h + 4 * q][jl], t[16 * h + 4 * q + 1][jl],
+                                                          t[16 * h + 4 * q + 2][jl], t[16 * h + 4 * q + 3][jl]);
+}
 
 // ---------------------------------------------------------------- narrow convolutions
 // The image layers do not fit the pipelined GEMM: N <= 4 wastes >= 88% of a 32-wide MFMA
@@ -2558,7 +2584,19 @@ static int pack_kind(const PackArgs& a, int& gx, int& gy) {
   return -1;
 }
 
+// pack_t2d applies: k = ci alone, n = (tap, co) over a [K][Cout][KH][KW]-contiguous W
+static bool pack_t2d_ok(const PackArgs& a) {
+  const int T = a.KH * a.KW;
+  return !a.convt2 && !a.flip && a.phases == 1 && a.fpci.d == (uint32_t)a.K && a.fnco.d * T == (uint32_t)a.N &&
+         a.fnkw.d == (uint32_t)a.KW && a.s_kw == 1 && a.s_kh == a.KW && a.s_out == T && a.s_in == a.N &&
+         a.K % PT_K == 0 && a.N % PT_N == 0 && aligned16(a.W) && aligned16(a.out);
+}
+
 static void launch_pack(const PackArgs& a, hipStream_t s) {
+  if (pack_t2d_ok(a)) {
+    pack_t2d<<<dim3(a.N / PT_N, a.K / PT_K), 256, 0, s>>>(a);
+    return;
+  }
   int gx, gy;
   const int kind = pack_kind(a, gx, gy);
   if (kind == 0) {
