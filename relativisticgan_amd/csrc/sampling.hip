@@ -3,7 +3,8 @@
 // numpy.random.choice(N, B, replace=False)), as counter-based draws on the GPU.
 //
 // Philox-4x32-10 keyed by the run's seed; the 64-bit counter lives on the device and every
-// call advances it by the numbers it consumed in a trailing one-thread launch, so a call
+// call advances it by the numbers it consumed (a trailing one-thread launch after a fill,
+// the sampling wave itself for the indices), so a call
 // captured in a HIP graph draws fresh numbers at every replay with no host involvement.
 // Every rank of a data-parallel run holds the same seed and counter and draws the global
 // batch (each keeps its shard), like torch's device generator did here before.
@@ -59,12 +60,33 @@ __global__ __launch_bounds__(256) void rng_fill(float* out, long long n, int kin
 __global__ void rng_advance(unsigned long long* counter, unsigned long long by) { counter[0] += by; }
 
 // n distinct indices of [0, N) (Floyd's algorithm: for j = N-n .. N-1 take t uniform in
-// [0, j], or j itself when t is already taken), one wave: the membership test of each step
-// is a ballot over the taken set in LDS.  Output in draw order.
+// [0, j], or j itself when t is already taken), one wave, output in draw order; the wave
+// advances the counter itself (every lane read it before lane 0 writes).
+//   n <= 64: lane s draws step s and keeps its pick in a register; each step broadcasts its
+//            t, the lanes holding earlier picks compare, a ballot decides (no LDS, no barrier);
+//   else:    the taken set in LDS, the membership test a ballot over it.
 constexpr int CHOICE_MAX = 4096;
 
+__global__ __launch_bounds__(64) void rng_choice_small(long long* out, int N, int n, unsigned long long seed,
+                                                       unsigned long long* counter) {
+  const unsigned long long base = counter[0];
+  const int lane = threadIdx.x;
+  int t_own = 0, pick = -1;  // -1: no pick yet (never equal to a draw)
+  if (lane < n) {
+    const u32x4s r = philox(base + (unsigned long long)lane, seed);
+    t_own = (int)(((unsigned long long)r.x * (unsigned long long)(N - n + lane + 1)) >> 32);
+  }
+  for (int s = 0; s < n; ++s) {
+    const int t = __shfl(t_own, s);
+    const bool any = __ballot(pick == t) != 0;
+    if (lane == s) pick = any ? N - n + s : t;
+  }
+  if (lane < n) out[lane] = pick;
+  if (lane == 0) counter[0] = base + (unsigned long long)n;
+}
+
 __global__ __launch_bounds__(64) void rng_choice(long long* out, int N, int n, unsigned long long seed,
-                                                 const unsigned long long* counter) {
+                                                 unsigned long long* counter) {
   __shared__ int taken[CHOICE_MAX];
   const unsigned long long base = counter[0];
   const int lane = threadIdx.x;
@@ -82,6 +104,7 @@ __global__ __launch_bounds__(64) void rng_choice(long long* out, int N, int n, u
     }
     __syncthreads();
   }
+  if (lane == 0) counter[0] = base + (unsigned long long)n;
 }
 
 }  // namespace rgan
@@ -106,9 +129,8 @@ extern "C" int rgan_rng_choice(long long* out, int N, int n, unsigned long long 
   RGAN_REQUIRE(out && counter && N > 0 && n >= 0 && n <= N && n <= CHOICE_MAX);
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
-  rng_choice<<<1, 64, 0, s>>>(out, N, n, seed, counter);
-  RGAN_CHECK_LAUNCH();
-  rng_advance<<<1, 1, 0, s>>>(counter, (unsigned long long)n);
+  if (n <= 64) rng_choice_small<<<1, 64, 0, s>>>(out, N, n, seed, counter);
+  else rng_choice<<<1, 64, 0, s>>>(out, N, n, seed, counter);
   RGAN_CHECK_LAUNCH();
   return 0;
 }

@@ -738,6 +738,8 @@ def test_device_rng(K):
     assert idx.unique().numel() == 64 and idx.min().item() >= 0 and idx.max().item() < 1000
     full = a.choice(50, 50)
     assert sorted(full.tolist()) == list(range(50))
+    big = a.choice(5000, 300)  # > 64: the LDS path
+    assert big.unique().numel() == 300 and big.min().item() >= 0 and big.max().item() < 5000
     assert torch.equal(b.normal((400, 1000)), z)  # same seed, same counter: same draws
     assert not torch.equal(b.normal((400, 1000)), z)  # the counter moved
     counts = torch.zeros(20, device=DEV)
