@@ -182,6 +182,13 @@ int rgan_bn_moments(const float* y, long long P, int C, long long sp, long long 
 int rgan_bn_finalize(const double* moments, int nranks, int C, float eps, float momentum,
                      float* running_mean, float* running_var, long long* num_batches_tracked,
                      float* stats, void* stream);
+/* The batched D pass's two calls' BatchNorm backward (GLI:605/624/644 through each call's
+ * BatchNorm) in three launches instead of six: dy of y's nseg (1 or 2) equal row ranges, each
+ * with its stats row [nseg][2C] and its own sums; dgamma / dbeta = the segments' sum.  Dense
+ * NHWC da, y, dy; partial >= nseg * rgan_bn_partial_bytes(P / nseg, C). */
+int rgan_bn_backward_segments(const float* da, const float* y, long long P, int C, int nseg, const float* stats,
+                              const float* gamma, const float* beta, int act, float act_alpha, float* dy,
+                              float* dgamma, float* dbeta, void* partial, void* stream);
 /* Backward through act(BN(y)): given da, produce dy, dgamma, dbeta. */
 int rgan_bn_backward(const float* da, long long dsp, long long dsc,
                      const float* y, long long P, int C, long long sp, long long sc,

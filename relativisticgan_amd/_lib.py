@@ -43,6 +43,8 @@ _SIGS = {
                                  c_ll, c_int, ctypes.POINTER(c_int), c_vp]),
     "rgan_bn_segment_stats_n": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_f, c_f, c_vp, c_vp, c_vp, c_vp,
                                         c_vp]),
+    "rgan_bn_backward_segments": (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_f, c_vp, c_vp,
+                                          c_vp, c_vp, c_vp]),
     "rgan_bn_apply_segments": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_f, c_vp, c_vp]),
     "rgan_bn_segment_stats": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp]),

@@ -374,6 +374,10 @@ class ConvLayerFn(torch.autograd.Function):
         P = Bs * y.shape[2] * y.shape[3]
         C = y.shape[1]
         dgamma = dbeta = None
+        if (SEG_FUSED and ctx.segs == 2 and not dp.sync_bn() and K.is_nhwc(y) and C % 4 == 0
+                and y.data_ptr() % 16 == 0 and da.data_ptr() % 16 == 0 and dy.data_ptr() % 16 == 0):
+            # both calls' BatchNorm backward in one set of launches (affine gradients summed)
+            return K.bn_backward_segments(da, y, stats, gamma, beta, spec.act, spec.alpha, ng, nbeta, dy)
         for s_ in range(ctx.segs):
             sl = slice(s_ * Bs, (s_ + 1) * Bs)
             if dp.sync_bn():

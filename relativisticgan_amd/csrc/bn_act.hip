@@ -168,6 +168,10 @@ __global__ __launch_bounds__(1024) void bn_merge(const double* __restrict__ part
                                                  long long sc, float eps, float momentum, float* running_mean,
                                                  float* running_var, long long* nbt, float* stats) {
   __shared__ double sh[2][MERGE_ROWS][MERGE_CPB];
+  if constexpr (FIN == 0) {  // gridDim.y segments: [seg][chunks][2][C] -> [seg][2][C]
+    part += (size_t)blockIdx.y * chunks * 2 * C;
+    out += (size_t)blockIdx.y * 2 * C;
+  }
   const int cl = threadIdx.x % MERGE_CPB, r = threadIdx.x / MERGE_CPB;
   const int c = blockIdx.x * MERGE_CPB + cl;
   double a1 = 0.0, a2 = 0.0;
@@ -489,17 +493,23 @@ extern "C" int rgan_bn_apply(const float* y, long long P, int C, long long sp, l
 
 // ------------------------------------------------------------------ backward
 // partial [chunk][2][C] doubles: sum g, sum g*(y-mean);  g = da * act'(y*al + be)
-template <int Q>
+// NSEG 2: the batched D pass's two calls in one launch -- chunk x of segment x / chunks_seg
+// covers rows of that segment only, with its stats row (partials [seg][chunk][2][C])
+template <int Q, int NSEG = 1>
 __global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ da, long long dsp, long long dsc,
                                                       const float* __restrict__ y, long long P, int C, long long sp,
-                                                      long long sc, const float* __restrict__ stats,
+                                                      long long sc, const float* __restrict__ stats_all,
                                                       const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, int act, float alpha, int tpr,
-                                                      long long rows, double* __restrict__ part) {
+                                                      long long rows, double* __restrict__ part, int chunks_seg = 1) {
   __shared__ double sh[2][256][Q];
   const int tid = threadIdx.x, lc = tid % tpr, rl = tid / tpr, rp = blockDim.x / tpr;
   const int c0 = (blockIdx.y * tpr + lc) * Q;
-  const long long p0 = blockIdx.x * rows, p1 = min(P, p0 + rows);
+  const int seg = NSEG > 1 ? (int)blockIdx.x / chunks_seg : 0;
+  const int chunk = NSEG > 1 ? (int)blockIdx.x - seg * chunks_seg : (int)blockIdx.x;
+  const float* stats = stats_all + (size_t)seg * 2 * C;
+  const long long pb = (long long)seg * P;  // NSEG > 1: P = rows per segment
+  const long long p0 = pb + chunk * rows, p1 = min(pb + P, p0 + rows);
   double s1[Q], s2[Q];
   float mean[Q], al[Q], be[Q];
 #pragma unroll
@@ -554,7 +564,9 @@ __global__ __launch_bounds__(256) void bn_bwd_partial(const float* __restrict__ 
 }
 
 // dy = al*(g - sum_g/Pg - (y-mean)*invstd^2*sum_gx/Pg); dgamma = invstd*sum_gx, dbeta = sum_g
-template <int Q>
+// NSEG 2: rows [0, seg_rows) with stats / sums row 0, the rest with row 1 (the batched
+// pass's two calls); the affine gradients are the segments' sum (segment order)
+template <int Q, int NSEG = 1>
 __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ da, long long dsp, long long dsc,
                                                     const float* __restrict__ y, long long P, int C, long long sp,
                                                     long long sc, const float* __restrict__ stats,
@@ -563,28 +575,43 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ da
                                                     const double* __restrict__ sums, double inv_pg,
                                                     float* __restrict__ dy, long long ysp, long long ysc,
                                                     float* dgamma, float* dbeta, int tpr,
-                                                    const float* __restrict__ add, int accum_affine) {
+                                                    const float* __restrict__ add, int accum_affine,
+                                                    long long seg_rows = 0) {
   const int tid = threadIdx.x, lc = tid % tpr, rl = tid / tpr, rp = blockDim.x / tpr;
   const int c0 = (blockIdx.x * tpr + lc) * Q;
   if (c0 >= C) return;
-  float mean[Q], al[Q], be[Q], k1[Q], k2[Q];
+  float mean_s[NSEG][Q], al_s[NSEG][Q], be_s[NSEG][Q], k1_s[NSEG][Q], k2_s[NSEG][Q];
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     const int c = min(c0 + q, C - 1);
-    const float inv = stats[C + c];
-    mean[q] = stats[c];
-    al[q] = (gamma ? gamma[c] : 1.f) * inv;
-    be[q] = (beta ? beta[c] : 0.f) - mean[q] * al[q];
-    k1[q] = (float)(sums[c] * inv_pg);
-    k2[q] = (float)(sums[C + c] * (double)inv * (double)inv * inv_pg);
+    float db = 0.f, dg = 0.f;
+#pragma unroll
+    for (int sg = 0; sg < NSEG; ++sg) {
+      const float* st = stats + (size_t)sg * 2 * C;
+      const double* su = sums + (size_t)sg * 2 * C;
+      const float inv = st[C + c];
+      mean_s[sg][q] = st[c];
+      al_s[sg][q] = (gamma ? gamma[c] : 1.f) * inv;
+      be_s[sg][q] = (beta ? beta[c] : 0.f) - mean_s[sg][q] * al_s[sg][q];
+      k1_s[sg][q] = (float)(su[c] * inv_pg);
+      k2_s[sg][q] = (float)(su[C + c] * (double)inv * (double)inv * inv_pg);
+      const float dbs = (float)su[c], dgs = (float)(su[C + c] * (double)inv);
+      db = sg == 0 ? dbs : db + dbs;
+      dg = sg == 0 ? dgs : dg + dgs;
+    }
     if (blockIdx.y == 0 && rl == 0 && c0 + q < C) {
-      const float db = (float)sums[c], dg = (float)(sums[C + c] * (double)inv);
       if (dbeta) dbeta[c] = accum_affine ? dbeta[c] + db : db;
       if (dgamma) dgamma[c] = accum_affine ? dgamma[c] + dg : dg;
     }
   }
   const long long step = (long long)gridDim.y * rp;
   auto out = [&](long long p, float (&v)[Q], const float (&g)[Q]) {
+    const int sg = NSEG > 1 && p >= seg_rows ? 1 : 0;
+    const float(&mean)[Q] = mean_s[sg];
+    const float(&al)[Q] = al_s[sg];
+    const float(&be)[Q] = be_s[sg];
+    const float(&k1)[Q] = k1_s[sg];
+    const float(&k2)[Q] = k2_s[sg];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       const float gz = g[q] * act_grad_from_in(v[q] * al[q] + be[q], act, alpha);
@@ -681,6 +708,41 @@ extern "C" int rgan_bn_backward_apply(const float* da, long long dsp, long long 
                                       float* dbeta, void* stream) {
   return rgan_bn_backward_apply_ex(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, sums,
                                    P_global, nullptr, dy, ysp, ysc, dgamma, dbeta, 0, stream);
+}
+
+extern "C" int rgan_bn_backward_segments(const float* da, const float* y, long long P, int C, int nseg,
+                                         const float* stats, const float* gamma, const float* beta, int act,
+                                         float act_alpha, float* dy, float* dgamma, float* dbeta, void* partial,
+                                         void* stream) {
+  // dense NHWC da, y, dy; P % nseg == 0; stats [nseg][2C]; partial: nseg * rgan_bn_partial_bytes(P / nseg, C)
+  RGAN_REQUIRE(da && y && stats && dy && partial && P > 0 && C > 0 && (nseg == 1 || nseg == 2) && P % nseg == 0);
+  hipStream_t s = (hipStream_t)stream;
+  const long long Ps = P / nseg;
+  BnGeo g = bn_geo(Ps, C, C, 1);
+  RGAN_REQUIRE(g.vec && dense_nhwc(C, 1, C, y) && dense_nhwc(C, 1, C, da) && dense_nhwc(C, 1, C, dy));
+  double* part = (double*)partial;
+  double* sums = part + (size_t)nseg * g.chunks * 2 * C;
+  const dim3 pgrid(nseg * g.chunks, g.cgroups);
+  if (nseg == 1)
+    bn_bwd_partial<4, 1><<<pgrid, 256, 0, s>>>(da, C, 1, y, Ps, C, C, 1, stats, gamma, beta, act, act_alpha, g.tpr,
+                                               g.rows, part, g.chunks);
+  else
+    bn_bwd_partial<4, 2><<<pgrid, 256, 0, s>>>(da, C, 1, y, Ps, C, C, 1, stats, gamma, beta, act, act_alpha, g.tpr,
+                                               g.rows, part, g.chunks);
+  RGAN_CHECK_LAUNCH();
+  bn_merge<0><<<dim3(ceil_div(C, MERGE_CPB), nseg), 1024, 0, s>>>(part, g.chunks, C, sums, nullptr, 0, 0, 0.f, 0.f,
+                                                                  nullptr, nullptr, nullptr, nullptr);
+  RGAN_CHECK_LAUNCH();
+  const BnGeo ga = bn_geo(P, C, C, 1);
+  const double inv_pg = 1.0 / (double)Ps;
+  if (nseg == 1)
+    bn_bwd_apply<4, 1><<<apply_grid(ga, P), 256, 0, s>>>(da, C, 1, y, P, C, C, 1, stats, gamma, beta, act, act_alpha,
+                                                        sums, inv_pg, dy, C, 1, dgamma, dbeta, ga.tpr, nullptr, 0, 0);
+  else
+    bn_bwd_apply<4, 2><<<apply_grid(ga, P), 256, 0, s>>>(da, C, 1, y, P, C, C, 1, stats, gamma, beta, act, act_alpha,
+                                                        sums, inv_pg, dy, C, 1, dgamma, dbeta, ga.tpr, nullptr, 0, Ps);
+  RGAN_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int rgan_bn_backward(const float* da, long long dsp, long long dsc, const float* y, long long P,

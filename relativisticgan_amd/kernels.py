@@ -487,6 +487,21 @@ def bn_apply_segments(y, stats, gamma, beta, act, alpha, out):
     return out
 
 
+def bn_backward_segments(da, y, stats, gamma, beta, act, alpha, need_gamma, need_beta, out):
+    """bn_backward of y's nseg = stats.shape[0] equal batch segments in one set of launches
+    (dense NHWC da, y, out); dgamma / dbeta summed over the segments."""
+    P, C, _, _ = _pc(y)
+    nseg = stats.shape[0]
+    dgamma = torch.empty(C, dtype=torch.float32, device=y.device) if need_gamma and gamma is not None else None
+    dbeta = torch.empty(C, dtype=torch.float32, device=y.device) if need_beta and beta is not None else None
+    lib = L.lib()
+    ws = L.workspace(nseg * lib.rgan_bn_partial_bytes(P // nseg, C), y.device)
+    L.check(lib.rgan_bn_backward_segments(L.ptr(da), L.ptr(y), P, C, nseg, L.ptr(stats), L.ptr(gamma), L.ptr(beta),
+                                          L.ACT[act], float(alpha), L.ptr(out), L.ptr(dgamma), L.ptr(dbeta),
+                                          L.ptr(ws), L.stream()), "rgan_bn_backward_segments")
+    return out, dgamma, dbeta
+
+
 def bn_apply(y, stats, gamma, beta, act="none", alpha=0.0, out=None):
     P, C, sp, sc = _pc(y)
     if out is None:

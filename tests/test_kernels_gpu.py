@@ -783,3 +783,25 @@ def test_bn_two_segments_one_launch(K):
     a2 = K.bn_apply_segments(y, st2, gamma, beta, "lrelu", 0.2, out=torch.empty_like(y))
     assert torch.equal(st1, st2) and torch.equal(a1, a2)
     assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2) and int(n2.item()) == 2
+
+
+def test_bn_backward_two_segments(K):
+    """rgan_bn_backward_segments (both calls of the batched pass at once) == the per-call
+    backward sums + apply, bitwise: dy and the summed affine gradients."""
+    torch.manual_seed(19)
+    for act in ("lrelu", "relu", "none"):
+        C, B, H = 64, 8, 16
+        y = _nhwc(torch.randn(B, C, H, H, device=DEV))
+        da = _nhwc(torch.randn(B, C, H, H, device=DEV))
+        stats = torch.cat([torch.randn(2, C, device=DEV), torch.rand(2, C, device=DEV) + 0.5], 1)  # [2][2C]
+        gamma, beta = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+        dy1 = torch.empty_like(y)
+        dg1, db1 = torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        P = (B // 2) * H * H
+        for k in range(2):
+            sl = slice(k * B // 2, (k + 1) * B // 2)
+            sums, da_c = K.bn_backward_sums(da[sl], y[sl], stats[k], gamma, beta, act, 0.2)
+            K.bn_backward_apply_ex(da_c, y[sl], stats[k], gamma, beta, act, 0.2, sums, P, out=dy1[sl], dgamma=dg1,
+                                   dbeta=db1, accumulate_affine=k > 0)
+        dy2, dg2, db2 = K.bn_backward_segments(da, y, stats, gamma, beta, act, 0.2, True, True, torch.empty_like(y))
+        assert torch.equal(dy1, dy2) and torch.equal(dg1, dg2) and torch.equal(db1, db2), act
