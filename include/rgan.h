@@ -307,7 +307,7 @@ int rgan_spectral_power(const float* W, int rows, int cols, long long rs, long l
                         void* ws, void* stream);
 /* All spectral layers of one net call in FOUR launches (instead of four per layer):
  * each layer gets one power iteration exactly as rgan_spectral_power(do_iter=1).
- * n <= 16 layers; counters: unused, may be NULL (kept in the signature); ws:
+ * n <= 16 layers; every sum in a fixed order (no cross-block hand-off, no counters); ws:
  * rgan_spectral_batch_ws_bytes(n, layers). */
 typedef struct RganSnLayer {
   const float* W;
@@ -321,8 +321,7 @@ typedef struct RganSnLayer {
   float* inv_sigma;
 } RganSnLayer;
 size_t rgan_spectral_batch_ws_bytes(int n, const RganSnLayer* layers);
-int rgan_spectral_power_batch(int n, const RganSnLayer* layers, float eps, void* ws, unsigned* counters,
-                              void* stream);
+int rgan_spectral_power_batch(int n, const RganSnLayer* layers, float eps, void* ws, void* stream);
 /* dW_orig = dW_eff/sigma - (<dW_eff, W_orig>/sigma^2) u v^T (u, v constants); ws >= 2 KiB. */
 int rgan_spectral_backward(const float* W, const float* dWeff, int rows, int cols,
                            long long rs, long long hs, int lo, const float* u, const float* v,

@@ -95,7 +95,7 @@ _SIGS = {
     "rgan_spectral_power": (c_int, [c_vp, c_int, c_int, c_ll, c_ll, c_int, c_f, c_vp, c_vp, c_vp, c_int, c_vp,
                                     c_vp]),
     "rgan_spectral_batch_ws_bytes": (c_sz, [c_int, c_vp]),
-    "rgan_spectral_power_batch": (c_int, [c_int, c_vp, c_f, c_vp, c_vp, c_vp]),
+    "rgan_spectral_power_batch": (c_int, [c_int, c_vp, c_f, c_vp, c_vp]),
     "rgan_spectral_backward": (c_int, [c_vp, c_vp, c_int, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
                                        c_vp, c_vp]),
     "rgan_adam": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -1722,8 +1722,12 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
     const bool more = tn < tiles;
     // this tile's window landed: the previous tile's 16 stores went out after its DMA and
     // may stay in flight (vmcnt retires in issue order)
+#ifndef RGAN_IMG_WAIT_ALL
     if constexpr (decltype(first_c)::value) __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     else __builtin_amdgcn_s_waitcnt(0x4f70);                                      // vmcnt(16)
+#else
+    __builtin_amdgcn_s_waitcnt(0x0f70);
+#endif
     float bv[NS];
     auto read_step = [&](int s) {
       // k = 2 s + lk = 16 ci + 4 kh + kw; the lk part is in base (kw parity)
@@ -1744,6 +1748,9 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
         acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[i][s], bv[s], acc[i], 0, 0, 0);
     }
     if (more) fetch(tn, Wn);
+#ifdef RGAN_IMG_DMA_DRAIN
+    __builtin_amdgcn_s_waitcnt(0x0f70);
+#endif
     int b, oi0, oj0;
     tile_pos(t, b, oi0, oj0);
     const int tb4 = (int)(((long long)b * a.ysb + (long long)oi0 * a.ysh + (long long)oj0 * a.ysw) * 4);
@@ -1761,6 +1768,10 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
         const int pl = 8 * u + rp;
         ev[u] = *reinterpret_cast<const float4*>(T + pl * 32 + 4 * (rq ^ ((pl >> 1) & 7)));
       }
+#ifdef RGAN_IMG_LGKM0
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+      __builtin_amdgcn_sched_barrier(0);
+#endif
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         // pixels 8 u .. 8 u + 7 of the wave tile lie in one output row (WS >= 16).  The
@@ -2738,7 +2749,10 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
     // (32-channel tiles when the width is not a multiple of 128: D at h = 32, 64)
     const int tiles = a.B * a.Ho * a.Wo / 32;
     const bool wide = a.Cout % 128 == 0;
-    const dim3 grid(std::min(ceil_div(tiles, 4), 512), a.Cout / (wide ? 128 : 32));
+#ifndef RGAN_IMG_GRID
+#define RGAN_IMG_GRID 512
+#endif
+    const dim3 grid(std::min(ceil_div(tiles, 4), RGAN_IMG_GRID), a.Cout / (wide ? 128 : 32));
     const int act_kind = a.act == RGAN_ACT_NONE ? 0
                          : (a.act == RGAN_ACT_RELU || (a.act == RGAN_ACT_LRELU && a.alpha <= 1.f)) ? 1 : 2;
 #define RGAN_IMG_A(CC, WW, NN)                                                            \

@@ -651,10 +651,8 @@ extern "C" size_t rgan_spectral_batch_ws_bytes(int n, const RganSnLayer* layers)
   return f * sizeof(float) + 256;
 }
 
-extern "C" int rgan_spectral_power_batch(int n, const RganSnLayer* layers, float eps, void* ws, unsigned* counters,
-                                         void* stream) {
+extern "C" int rgan_spectral_power_batch(int n, const RganSnLayer* layers, float eps, void* ws, void* stream) {
   RGAN_REQUIRE(n > 0 && n <= SNB_MAX && layers && ws);
-  (void)counters;  // no cross-block hand-off any more (kept in the signature)
   SnBatch bv{}, bt{}, bu{};
   float* p = (float*)(((uintptr_t)ws + 255) & ~(uintptr_t)255);
   int nv = 0, nt = 0, nu = 0;

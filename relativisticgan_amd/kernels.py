@@ -736,9 +736,6 @@ def spectral_power(w, u, v, transposed, eps=1e-12, do_iter=True):
     return inv_sigma
 
 
-_SN_COUNTERS = {}
-
-
 def spectral_power_batch(layers, eps=1e-12):
     """One power iteration for every (w, u, v, transposed) of a net call, in four launches
     (rgan_spectral_power_batch): u, v updated in place; returns [(u_copy, v_copy, inv_sigma)]
@@ -760,11 +757,8 @@ def spectral_power_batch(layers, eps=1e-12):
         outs.append((uc, vc, inv))
     lib = L.lib()
     ws = L.workspace(lib.rgan_spectral_batch_ws_bytes(n, ctypes.cast(arr, ctypes.c_void_p)), dev)
-    cnt = _SN_COUNTERS.get(dev)
-    if cnt is None:  # zeroed once; every call leaves them zero (the last block of a layer resets its own)
-        cnt = _SN_COUNTERS[dev] = torch.zeros(16, dtype=torch.int32, device=dev)
-    L.check(lib.rgan_spectral_power_batch(n, ctypes.cast(arr, ctypes.c_void_p), float(eps), L.ptr(ws), L.ptr(cnt),
-                                          L.stream()), "rgan_spectral_power_batch")
+    L.check(lib.rgan_spectral_power_batch(n, ctypes.cast(arr, ctypes.c_void_p), float(eps), L.ptr(ws), L.stream()),
+            "rgan_spectral_power_batch")
     return outs
 
 

@@ -62,7 +62,27 @@ CONFIGS = {
                               "arch": 1, "n_iter": 2}, "seed": 1, "n_images": 64},
     "rahinge_arch1": {"args": {"image_size": 32, "batch_size": 8, "z_size": 16, "loss_D": 8,
                                "arch": 1, "n_iter": 2}, "seed": 1, "n_images": 64},
+    # the reference writes state_01.pth itself after iteration 1 (--gen_every 2 --save True,
+    # GLI:729-747); the file is kept as tests/golden/ralsgan_ckpt_state_01.pth
+    "ralsgan_ckpt": dict(_cfg(loss_D=7, n_iter=2), save_every=2),
+    # the other single-GPU BASELINE configs at FULL size (h = z = 128), 2 iterations each,
+    # captured at 8 threads (the reference is bitwise deterministic at a fixed thread count)
+    # C2 = configs[1]: RaSGAN DCGAN 128x128, batch 64 (GLI:636-637, 699-702)
+    "rasgan_c2": {"args": {"image_size": 128, "batch_size": 64, "z_size": 128, "G_h_size": 128,
+                           "D_h_size": 128, "loss_D": 6, "n_iter": 2}, "seed": 1, "n_images": 128,
+                  "threads": 8},
+    # C4' = configs[3] on the DCGAN nets at 64x64, h = 128, batch 32 (GLI:646-658)
+    "wgangp_c4p": {"args": {"image_size": 64, "batch_size": 32, "z_size": 128, "G_h_size": 128,
+                            "D_h_size": 128, "loss_D": 3, "n_iter": 2}, "seed": 1, "n_images": 64,
+                   "threads": 8},
+    # C5 = configs[4]: spectral-norm RaHingeGAN 128x128, batch 32 (GLI:408-446, 641, 709)
+    "rahinge_spectral_c5": {"args": {"image_size": 128, "batch_size": 32, "z_size": 128, "G_h_size": 128,
+                                     "D_h_size": 128, "loss_D": 8, "spectral": "True", "n_iter": 2},
+                            "seed": 1, "n_images": 64, "threads": 8},
 }
+
+# full-size configs: minutes of CPU oracle time each (GPU parity runs them with all host cores)
+FULL_SIZE = ("ralsgan_c1", "rasgan_c2", "wgangp_c4p", "rahinge_spectral_c5")
 
 
 # configs with a reference fixture (tests/golden/<name>.npz) pinning the oracle bitwise

@@ -109,7 +109,8 @@ def _script_globals():
 
 
 def run_config(name, cfg):
-    torch.set_num_threads(THREADS)
+    threads = cfg.get("threads", THREADS)
+    torch.set_num_threads(threads)
     args = cfg["args"]
     S = args.get("image_size", 64)
     dataset = synthetic_dataset(cfg.get("n_images", 64), S)
@@ -168,6 +169,7 @@ def run_config(name, cfg):
     torch.optim.Adam.__init__ = init_hook
     torch.optim.Adam.step = step_hook
     tmp = tempfile.mkdtemp(prefix="rgan_golden_")
+    os.makedirs(os.path.join(tmp, "extra"))  # GLI:103-104 only creates it when gen_extra_images > 0
     script = REF_SCRIPT_PAC if cfg.get("pac", 1) == 2 else REF_SCRIPT
     argv = [script, "--cuda", "False", "--seed", str(cfg.get("seed", 1)),
             "--n_iter", str(n_iter), "--gen_extra_images", "0", "--print_every", "1000",
@@ -176,6 +178,8 @@ def run_config(name, cfg):
         if k == "n_iter":
             continue
         argv += ["--" + k, str(v)]
+    if cfg.get("save_every"):  # the reference writes its own checkpoint (GLI:729-747)
+        argv += ["--gen_every", str(cfg["save_every"]), "--save", "True"]
     old_argv, old_cwd = sys.argv, os.getcwd()
     sys.argv = argv
     os.chdir(tmp)
@@ -188,10 +192,14 @@ def run_config(name, cfg):
         torch.optim.Adam.step = orig_step
     rec.store["meta.json"] = np.frombuffer(json.dumps({
         "config": name, "args": args, "seed": cfg.get("seed", 1), "n_iter": n_iter, "pac": cfg.get("pac", 1),
-        "n_images": cfg.get("n_images", 64), "threads": THREADS,
+        "n_images": cfg.get("n_images", 64), "threads": threads,
         "torch": torch.__version__}).encode(), dtype=np.uint8).copy()
     out = os.path.join(HERE, f"{name}.npz")
     np.savez_compressed(out, **rec.store)
+    if cfg.get("save_every"):
+        import shutil
+        for f in sorted(os.listdir(os.path.join(tmp, "extra", "models"))):
+            shutil.copy(os.path.join(tmp, "extra", "models", f), os.path.join(HERE, f"{name}_{f}"))
     return out
 
 

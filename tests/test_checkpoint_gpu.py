@@ -1,9 +1,11 @@
 """Checkpoint parity (GLI:536-552 load, GLI:733-747 save) in both directions.
 
-reference -> build: the oracle (torch modules, torch.optim.Adam, ExponentialLR) trains two
-  iterations and writes the reference's dict with torch.save; ``train.main --load`` resumes
-  it on the GPU for one iteration, and the oracle resumed from the same file runs the same
-  iteration.  Both runs re-seed and draw exactly as the reference does after a resume.
+reference -> build: ``tests/golden/ralsgan_ckpt_state_01.pth`` was written by the
+  unmodified reference itself (``--gen_every 2 --save True`` after two iterations,
+  tests/golden/make_golden.py; pinned bitwise against the oracle's ``checkpoint()`` dict by
+  tests/test_oracle_golden.py).  ``train.main --load`` resumes it on the GPU for one
+  iteration, and the oracle resumed from the same file runs the same iteration.  Both runs
+  re-seed and draw exactly as the reference does after a resume (GLI:537-560).
 build -> reference: the GPU trainer's ``state()`` file loads into the oracle (strict
   state_dict keys, torch Adam state) and the next iteration matches the GPU's own.
 
@@ -44,17 +46,17 @@ def _check_step(pre, ours, ref, what):
             assert (x - y).abs().max().item() <= 2.02 * upd + 1e-7, (what, side, k)
 
 
+REF_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ralsgan_ckpt_state_01.pth")
+
+
 def test_resume_reference_checkpoint_through_cli():
-    from oracle.reference_cpu import checkpoint, load_checkpoint
+    from oracle.reference_cpu import load_checkpoint
     from relativisticgan_amd.train import main
     root = tempfile.mkdtemp()
-    ref = _oracle()
-    for i in range(2):
-        ref.iteration(i)
-    path = os.path.join(root, "state_01.pth")
-    torch.save(checkpoint(ref, 2, 1), path)          # the reference's file (GLI:737)
-    pre = {"G": {k: v.clone() for k, v in ref.G.state_dict().items()},
-           "D": {k: v.clone() for k, v in ref.D.state_dict().items()}}
+    path = REF_FILE                                   # written by the reference (GLI:737)
+    ck = torch.load(path, weights_only=True)
+    pre = {"G": {k: v.clone() for k, v in ck["G_state"].items()},
+           "D": {k: v.clone() for k, v in ck["D_state"].items()}}
     # the reference resumed: re-seeded build, load, iteration 2 (GLI:537-560)
     ref2 = _oracle()
     it0, _ = load_checkpoint(ref2, torch.load(path, weights_only=True))

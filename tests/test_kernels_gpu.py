@@ -616,15 +616,18 @@ def test_gather(K):
 
 
 def test_spectral_power_batch(K):
-    """All spectral layers of a call in two launches == one power iteration per layer
+    """All spectral layers of a call in four launches == one power iteration per layer
     (torch spectral_norm, fp64 reference), incl. ConvT (dim 1), the rows = 1 end layer, a
-    non-float4 view and multi-chunk layers (cols > 1024, rows > 64); the completion counters
-    are left at zero for the next call."""
+    non-float4 view, multi-chunk layers (cols > 1024, rows > 64) and the largest layer of
+    the C5 D (Conv2d(1024, 2048): 2048 rows x 16384 columns); a second call (from the
+    updated u) equals a second fp64 iteration."""
     torch.manual_seed(9)
     specs = [(torch.nn.Conv2d(3, 16, 4, 2, 1, bias=False), False), (torch.nn.Conv2d(16, 300, 4, 2, 1, bias=False), False),
              (torch.nn.ConvTranspose2d(64, 24, 4, 2, 1, bias=False), True), (torch.nn.Conv2d(300, 1, 4, 1, 0, bias=False), False),
-             # scalar path (3-column rows, 2 row chunks) and the C5 D's largest layer (8 x 17 blocks)
-             (torch.nn.Conv2d(3, 70, 1, bias=False), False), (torch.nn.Conv2d(512, 1024, 4, 2, 1, bias=False), False)]
+             # scalar path (3-column rows, 2 row chunks), a 1024-row layer (8 x 17 blocks) and the
+             # C5 D's largest layer, Middle-Conv2d [4] at 128x128, h = 128: 1024 -> 2048 (GLI:420-428)
+             (torch.nn.Conv2d(3, 70, 1, bias=False), False), (torch.nn.Conv2d(512, 1024, 4, 2, 1, bias=False), False),
+             (torch.nn.Conv2d(1024, 2048, 4, 2, 1, bias=False), False)]
     layers, refs = [], []
     for conv, tr in specs:
         sn = torch.nn.utils.spectral_norm(conv)
@@ -638,16 +641,19 @@ def test_spectral_power_batch(K):
         v1 = F.normalize(Wm.t() @ sn.weight_u.double(), dim=0, eps=1e-12)
         u1 = F.normalize(Wm @ v1, dim=0, eps=1e-12)
         refs.append((u1, v1, torch.dot(u1, Wm @ v1)))
-    for rep in range(2):  # twice: a second call must find the counters reset
+    for rep in range(2):  # twice: the second call starts from the u the first one wrote
         outs = K.spectral_power_batch(layers)
         torch.cuda.synchronize()
-        if rep == 0:
-            for (w, u, v, tr), (uc, vc, inv), (u1, v1, sig) in zip(layers, outs, refs):
-                assert _rel(u, u1) < 1e-5 and _rel(v, v1) < 1e-5
-                assert torch.equal(uc, u) and torch.equal(vc, v)
-                assert abs(1 / inv.item() - sig.item()) < 1e-5 * sig.item()
-    cnt = next(iter(K._SN_COUNTERS.values()))
-    assert int(cnt.abs().sum()) == 0
+        for (w, u, v, tr), (uc, vc, inv), (u1, v1, sig) in zip(layers, outs, refs):
+            assert _rel(u, u1) < 1e-5 and _rel(v, v1) < 1e-5
+            assert torch.equal(uc, u) and torch.equal(vc, v)
+            assert abs(1 / inv.item() - sig.item()) < 1e-5 * sig.item()
+        for k, ((w, u, v, tr), (u1, v1, sig)) in enumerate(zip(layers, refs)):  # next fp64 iteration
+            W = w.detach().double().cpu()
+            Wm = (W.permute(1, 0, 2, 3) if tr else W).reshape(W.shape[1] if tr else W.shape[0], -1)
+            v2 = F.normalize(Wm.t() @ u1, dim=0, eps=1e-12)
+            u2 = F.normalize(Wm @ v2, dim=0, eps=1e-12)
+            refs[k] = (u2, v2, torch.dot(u2, Wm @ v2))
 
 
 @pytest.mark.parametrize("ci", [1, 3, 4])

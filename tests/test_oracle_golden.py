@@ -45,3 +45,38 @@ def test_oracle_pac2_semantics():
     assert tuple(recs["D"]["z"].shape) == (2 * B, p.z_size, 1, 1)
     assert tuple(recs["G"]["z"].shape) == (2 * B, p.z_size, 1, 1)
     assert int(t.G.state_dict()["main.Start-BatchNorm2d.num_batches_tracked"]) == nbt0 + 1
+
+
+def _same(a, b, path="ck"):
+    """Structural + bitwise equality of two checkpoint objects (dicts, lists, tensors, scalars)."""
+    import torch
+    if torch.is_tensor(a) or torch.is_tensor(b):
+        assert torch.is_tensor(a) and torch.is_tensor(b), path
+        assert a.dtype == b.dtype and a.shape == b.shape and torch.equal(a, b), path
+    elif isinstance(a, dict):
+        assert isinstance(b, dict) and list(a) == list(b), (path, list(a), list(b))
+        for k in a:
+            _same(a[k], b[k], f"{path}.{k}")
+    elif isinstance(a, (list, tuple)):
+        assert isinstance(b, (list, tuple)) and len(a) == len(b), path
+        for k, (x, y) in enumerate(zip(a, b)):
+            _same(x, y, f"{path}[{k}]")
+    else:
+        assert a == b and type(a) is type(b), (path, a, b)
+
+
+def test_oracle_checkpoint_matches_reference_file():
+    """The reference itself wrote tests/golden/ralsgan_ckpt_state_01.pth (GLI:729-747,
+    ``--gen_every 2 --save True``).  Loaded with ``weights_only=True`` (no code runs), it
+    must equal, key for key and bitwise, the dict the oracle's ``checkpoint()`` builds after
+    the same two iterations -- so the resume tests (tests/test_checkpoint_gpu.py) start from
+    exactly what the reference writes."""
+    import os
+    import torch
+    from oracle.reference_cpu import checkpoint
+    from tests.oracle_replay import GOLDEN_DIR
+    ref = torch.load(os.path.join(GOLDEN_DIR, "ralsgan_ckpt_state_01.pth"), weights_only=True)
+    _, t = replay("ralsgan_ckpt", n_iter=2, threads=1)
+    mine = checkpoint(t, 2, 1)
+    assert list(mine) == list(ref)
+    _same(mine, ref)
