@@ -15,7 +15,6 @@ plus torch tensor algebra for the per-channel BN normalisation and the activatio
 and differentiated with ``torch.autograd.grad``; ``gp.backward()`` then runs through
 those pieces.
 """
-import os
 
 import torch
 import torch.nn.functional as F
@@ -27,17 +26,9 @@ from . import kernels as K
 # Test/diagnostic hook: when a list, every fused layer whose activation has a derivative
 # discontinuous at 0 (ReLU, LeakyReLU, SELU) appends the sign mask of its output, in call
 # order, so parity tests can count sign flips against an exact (fp64) forward.
-# Image-layer gradients (k4 s2 p1, <= 4 image channels) as 1x1 GEMMs over a patch matrix
+# Image-layer gradients (k4 s2 p1, <= 4 image channels) run as 1x1 GEMMs over a patch matrix
 # (kernels.patches_k4s2); the forwards keep the direct narrow kernels (as fast: both are
-# bound by writing the 128-channel side).  False = narrow kernels / implicit GEMM throughout.
-PATCH_IMAGE_LAYERS = os.environ.get("RGAN_PATCH_IMAGE", "1") != "0"
-
-# RGAN_ACC_EPILOGUE=0: leave repeated weight-gradient contributions to autograd's add (A/B)
-ACCUMULATE_IN_EPILOGUE = os.environ.get("RGAN_ACC_EPILOGUE", "1") != "0"
-
-
-# RGAN_SEG_FUSED=0: the batched pass's per-call BatchNorm one call at a time (A/B switch)
-SEG_FUSED = os.environ.get("RGAN_SEG_FUSED", "1") != "0"
+# bound by writing the 128-channel side).
 
 
 class owning_grads:
@@ -221,7 +212,7 @@ class ConvLayerFn(torch.autograd.Function):
                 Bs = y.shape[0] // segs
                 a = torch.empty_like(y) if out is None else out
                 stats = torch.empty((segs, 2 * C), dtype=torch.float32, device=y.device)
-                if (SEG_FUSED and part is not None and segs == 2 and S % 2 == 0 and not dp.sync_bn() and K.is_nhwc(y)
+                if (part is not None and segs == 2 and S % 2 == 0 and not dp.sync_bn() and K.is_nhwc(y)
                         and K.is_nhwc(a) and y.data_ptr() % 16 == 0 and a.data_ptr() % 16 == 0 and C % 4 == 0):
                     # both calls' statistics (running stats in call order) and normalisation,
                     # one launch each
@@ -347,8 +338,12 @@ class ConvLayerFn(torch.autograd.Function):
     def _own_grad(w, bias):
         """This call may write its weight gradient into w.grad itself: one process (no
         gradient-bucket hooks waiting on AccumulateGrad), w a leaf, no bias gradient to
-        accumulate alongside, and .grad empty or a plain contiguous fp32 tensor of w's shape."""
-        if not (ACCUMULATE_IN_EPILOGUE and owning_grads.active and not dp.active() and w.is_leaf and bias is None):
+        accumulate alongside, no tensor / post-accumulate hook on w (they fire from autograd's
+        AccumulateGrad, which this path bypasses), and .grad empty or a plain contiguous fp32
+        tensor of w's shape."""
+        if not (owning_grads.active and not dp.active() and w.is_leaf and bias is None):
+            return False
+        if getattr(w, "_backward_hooks", None) or getattr(w, "_post_accumulate_grad_hooks", None):
             return False
         g = w.grad
         return g is None or (g.shape == w.shape and g.dtype == torch.float32 and g.is_contiguous()
@@ -356,12 +351,12 @@ class ConvLayerFn(torch.autograd.Function):
 
     @staticmethod
     def _patch_conv(spec, x):
-        return (PATCH_IMAGE_LAYERS and not spec.geom.transposed and not spec.bn and K.patchable(spec.geom, x.shape[1])
+        return (not spec.geom.transposed and not spec.bn and K.patchable(spec.geom, x.shape[1])
                 and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0)
 
     @staticmethod
     def _patch_convt(spec, w, bias):
-        return (PATCH_IMAGE_LAYERS and spec.geom.transposed and not spec.bn and bias is None
+        return (spec.geom.transposed and not spec.bn and bias is None
                 and K.patchable(spec.geom, w.shape[1]))
 
     @staticmethod
@@ -374,7 +369,7 @@ class ConvLayerFn(torch.autograd.Function):
         P = Bs * y.shape[2] * y.shape[3]
         C = y.shape[1]
         dgamma = dbeta = None
-        if (SEG_FUSED and ctx.segs == 2 and not dp.sync_bn() and K.is_nhwc(y) and C % 4 == 0
+        if (ctx.segs == 2 and not dp.sync_bn() and K.is_nhwc(y) and C % 4 == 0
                 and y.data_ptr() % 16 == 0 and da.data_ptr() % 16 == 0 and dy.data_ptr() % 16 == 0):
             # both calls' BatchNorm backward in one set of launches (affine gradients summed)
             return K.bn_backward_segments(da, y, stats, gamma, beta, spec.act, spec.alpha, ng, nbeta, dy)

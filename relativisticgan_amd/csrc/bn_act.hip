@@ -51,10 +51,7 @@ static BnGeo bn_geo(long long P, int C, long long sp, long long sc) {
   g.tpr = t;
   g.rp = 256 / t;
   g.cgroups = ceil_div(cq, t);
-  static const long long want_blocks = [] {
-    const char* e = getenv("RGAN_BN_CHUNKS");  // tuning experiments
-    return e ? atoll(e) : 512LL;
-  }();
+  constexpr long long want_blocks = 512;  // round-1 sweep (tools/bn_micro.py)
   long long chunks = std::max<long long>(1, want_blocks / g.cgroups);
   long long rows = (P + chunks - 1) / chunks;
   rows = std::max<long long>(rows, (long long)g.rp * 4);
@@ -442,14 +439,9 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
 }
 
 // apply-pass grid: pixel blocks per channel group, each thread at least `min_iter` pixel
-// rows (RGAN_BN_MIN_ITER / RGAN_BN_APPLY_BLOCKS: tuning experiments)
-static long long env_ll(const char* name, long long dflt) {
-  const char* e = getenv(name);
-  return e ? atoll(e) : dflt;
-}
-
+// rows (round-1 sweep with tools/bn_micro.py: 4096 blocks, 4 rows)
 static dim3 apply_grid(const BnGeo& g, long long P) {
-  static const long long blocks = env_ll("RGAN_BN_APPLY_BLOCKS", 4096), min_iter = env_ll("RGAN_BN_MIN_ITER", 4);
+  constexpr long long blocks = 4096, min_iter = 4;
   const long long rb = std::max<long long>(
       1, std::min<long long>((P + g.rp * min_iter - 1) / (g.rp * min_iter), std::max<long long>(1, blocks / g.cgroups)));
   return dim3(g.cgroups, (unsigned)rb);

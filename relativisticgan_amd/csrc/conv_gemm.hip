@@ -1001,7 +1001,7 @@ __global__ __launch_bounds__(256, RGAN_GEMM_SB ? 4 : 2) void gemm_kernel(GemmArg
   gemm_body<MODE, BM, BN, WM, WN, AV, BV, FAST, false>(g);
 }
 
-// Opt-in (RGAN_EMU_BF16X6=1): the FAST 128 x 128 CONV / CONVT2 GEMM with fp32 products
+// Opt-in (rgan_set_gemm_emulation): the FAST 128 x 128 CONV / CONVT2 GEMM with fp32 products
 // emulated on the bf16 MFMA (see gemm_body's EMU path).  Its own symbol, reported as such.
 template <int MODE>
 __global__ __launch_bounds__(256, 2) void gemm_bf16x6(GemmArgs g) {
@@ -1593,6 +1593,25 @@ __device__ __forceinline__ void dma_lds16(int m0, int voff, i32x4 rsrc) {
                : "memory", "m0");
 }
 
+// One 16-B-per-lane buffer store (raw descriptor rsrc, per-lane voff, wave-uniform soff) followed
+// by wait states IN THE SAME STATEMENT, so no instruction can sit between the store and them.
+// gfx950 does not interlock a VALU write of a wide store's data VGPRs against the store still
+// reading them, and LLVM inserts no wait state for a MUBUF store whose soffset is an SGPR: with
+// two blocks per CU a v_mul writing the data's first VGPR right behind the store replaced the
+// first dword of lanes 12-15 of every 16 (C2 / C3 image layers: 0.1-1 % of D's first-layer
+// outputs wrong on every wave's second and later tiles; tools/img_in_check.py).
+#ifndef RGAN_STORE_NOPS
+#define RGAN_STORE_NOPS "4"
+#endif
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store16_guarded(float4 f, int voff, i32x4 rsrc, int soff) {
+  const f32x4v v = {f.x, f.y, f.z, f.w};
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop " RGAN_STORE_NOPS
+               :
+               : "v"(v), "v"(voff), "s"(rsrc), "s"(soff)
+               : "memory");
+}
+
 // NI: 32-channel groups per block (4: 128-channel tiles; 1: 32-channel tiles for narrow D widths)
 template <int CI, int WS, int ACT, int NI = 4>  // ACT 0: identity, 1: max(v, v * neg) (ReLU / LeakyReLU, neg <= 1), 2: act_fwd
 __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
@@ -1615,7 +1634,7 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
   const int HWo = a.Ho * a.Wo;
   // raw buffer descriptor of x for the DMA pieces (stride 0, num_records = byte extent)
   const i32x4 xd = {(int)(uintptr_t)a.x, (int)((uintptr_t)a.x >> 32), a.x_bytes, 0x00020000};
-  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, a.y_bytes, 0x00020000);
+  const i32x4 yd = {(int)(uintptr_t)a.y, (int)((uintptr_t)a.y >> 32), a.y_bytes, 0x00020000};
   // weights: wa[i][s] = W[n0 + 32 i + l32][2 s + lk] / sigma  (torch [Cout][CI][4][4] = [n][k])
   // (staged through LDS by the whole block with coalesced loads: NCH x K floats, once)
   // (every global load of the prologue is issued before the first wait: at ~1-2 us per
@@ -1722,12 +1741,11 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
     const bool more = tn < tiles;
     // this tile's window landed: the previous tile's 16 stores went out after its DMA and
     // may stay in flight (vmcnt retires in issue order)
-#ifndef RGAN_IMG_WAIT_ALL
+    // (NI x 4 stores per tile: vmcnt(4 NI); a fixed vmcnt(16) let the 32-channel tiles read
+    // their window before its DMA landed)
+    constexpr int VMC = 4 * NI, VMC_ENC = 0x0f70 | (VMC & 15) | ((VMC >> 4) << 14);
     if constexpr (decltype(first_c)::value) __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-    else __builtin_amdgcn_s_waitcnt(0x4f70);                                      // vmcnt(16)
-#else
-    __builtin_amdgcn_s_waitcnt(0x0f70);
-#endif
+    else __builtin_amdgcn_s_waitcnt(VMC_ENC);                                     // vmcnt(4 NI)
     float bv[NS];
     auto read_step = [&](int s) {
       // k = 2 s + lk = 16 ci + 4 kh + kw; the lk part is in base (kw parity)
@@ -1748,9 +1766,6 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
         acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(wa[i][s], bv[s], acc[i], 0, 0, 0);
     }
     if (more) fetch(tn, Wn);
-#ifdef RGAN_IMG_DMA_DRAIN
-    __builtin_amdgcn_s_waitcnt(0x0f70);
-#endif
     int b, oi0, oj0;
     tile_pos(t, b, oi0, oj0);
     const int tb4 = (int)(((long long)b * a.ysb + (long long)oi0 * a.ysh + (long long)oj0 * a.ysw) * 4);
@@ -1768,21 +1783,14 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
         const int pl = 8 * u + rp;
         ev[u] = *reinterpret_cast<const float4*>(T + pl * 32 + 4 * (rq ^ ((pl >> 1) & 7)));
       }
-#ifdef RGAN_IMG_LGKM0
-      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-      __builtin_amdgcn_sched_barrier(0);
-#endif
+
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        // pixels 8 u .. 8 u + 7 of the wave tile lie in one output row (WS >= 16).  The
-        // offsets stay in SGPRs: a VALU write right behind a buffer_store may clobber its
-        // data registers before they are read (hipcc 7.2 / gfx950 inserted no wait state
-        // after a v_lshl_add_u64 there -- observed as corrupted lanes 12-15 of a store)
+        // pixels 8 u .. 8 u + 7 of the wave tile lie in one output row (WS >= 16); the
+        // store carries its own wait states (store16_guarded)
         const int p = 8 * u, prr = p / WS, pcc = p - prr * WS;
-        const int so = tb4 + prr * ysh4 + pcc * ysw4 + 128 * i;
-        __builtin_amdgcn_raw_buffer_store_b128(
-            u32x4{__float_as_uint(ev[u].x), __float_as_uint(ev[u].y), __float_as_uint(ev[u].z), __float_as_uint(ev[u].w)},
-            yr, lvo, so, 0);
+        const int so = __builtin_amdgcn_readfirstlane(tb4 + prr * ysh4 + pcc * ysw4 + 128 * i);
+        store16_guarded(ev[u], lvo, yd, so);
       }
     }
   };
@@ -2165,11 +2173,6 @@ struct Plan {
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
-static bool getenv_flag(const char* name) {  // A/B switches for experiments
-  const char* e = getenv(name);
-  return e && e[0] && e[0] != '0';
-}
-
 static void tile_dims(int cfg, int& bm, int& bn) {
   bm = cfg == CFG_N ? 256 : 128;
   bn = cfg == CFG_L ? 128 : (cfg == CFG_M ? 64 : 32);
@@ -2185,11 +2188,9 @@ static void choose_tiling(Plan& p) {
   const long long tiles = (long long)tiles_m * tiles_n * p.phases;
   const int nk = ceil_div(g.K, BK);
   int splits = 1;
-  // two resident 256-thread blocks per CU on 256 CUs (RGAN_SPLIT_TARGET: tuning experiments)
-  static const long long target = [] {
-    const char* e = getenv("RGAN_SPLIT_TARGET");
-    return e ? atoll(e) : 512LL;
-  }();
+  // two resident 256-thread blocks per CU on 256 CUs (round-1 sweep of this target: 256 / 384 / 768 /
+  // 1024 all lost to 512, profiles/round1_splitk_target_sweep.txt)
+  constexpr long long target = 512;
   if (tiles < target) {
     splits = (int)((target + tiles - 1) / tiles);
     splits = std::min(splits, std::max(1, nk / 4));
@@ -2262,9 +2263,7 @@ static void set_fast(Plan& p, int batch) {
     if (g.a.sh != (long long)g.a.W * g.a.sw || g.a.sb != (long long)g.a.H * g.a.sh) return;
     // a B tile is one tap's BN channels, or BN / Cin <= 4 whole taps of one kernel row
     const int cin = g.im.C;
-    static const bool multitap = !getenv_flag("RGAN_NO_MULTITAP");  // A/B switch
-    if (cin % bn != 0 &&
-        !(multitap && bn % cin == 0 && cin % 4 == 0 && bn / cin <= 4 && g.KW % (bn / cin) == 0))
+    if (cin % bn != 0 && !(bn % cin == 0 && cin % 4 == 0 && bn / cin <= 4 && g.KW % (bn / cin) == 0))
       return;
     g.a_bytes = (int)a_bytes;
     g.im_bytes = (int)im_bytes;
@@ -2335,7 +2334,7 @@ static bool plan_narrow_t(Plan& p, int batch, const float* x, const long long* x
   const long long ntiles = (long long)batch * ceil_div(H, NM_TR) * ceil_div(W, NM_TC);
   const int chunks = ceil_div(C, NM_CH);
   int splits = 1;
-  if (ntiles < 256 && !getenv_flag("RGAN_NO_NARROW_SPLIT"))
+  if (ntiles < 256)
     splits = (int)std::min<long long>(std::min(chunks, 8), ceil_div(512, (int)std::max<long long>(ntiles, 1)));
   a.cps = ceil_div(chunks, std::max(splits, 1)) * NM_CH;
   a.splits = ceil_div(C, a.cps);
@@ -2357,7 +2356,7 @@ static bool plan_narrow_in(Plan& p, const RganConv* d, const float* x, const flo
                               (d->win - 1) * d->xs[3]);
   const long long yext = 4 * (1 + (d->batch - 1) * d->ys[0] + (d->cout - 1) * d->ys[1] + (d->hout - 1) * d->ys[2] +
                               (d->wout - 1) * d->ys[3]);
-  p.img_in = !getenv_flag("RGAN_NO_IMG_IN") && d->stride == 2 && d->pad == 1 && d->hout * 2 == d->hin &&
+  p.img_in = d->stride == 2 && d->pad == 1 && d->hout * 2 == d->hin &&
              d->wout * 2 == d->win && d->cin <= 3 && (d->cout % 128 == 0 || (d->cin == 3 && d->cout % 32 == 0)) &&
              vec_nhwc(y, d->ys, d->cout) &&
              (d->wout == 16 || d->wout % 32 == 0) && ((long long)d->batch * d->hout * d->wout / 32) < (1LL << 31) &&
@@ -2631,18 +2630,10 @@ static void launch_cfg(const Plan& p, dim3 grid, hipStream_t s) {
   else gemm_kernel<MODE, BM, BN, WM, WN, false, false, false><<<grid, 256, 0, s>>>(p.g);
 }
 
-// FAST 128x128 CONV / CONVT2 GEMMs (fwd + dgrad of Conv and ConvT) on the bf16x6 emulation: opt-in, by RGAN_EMU_BF16X6=1 at
-// load or rgan_set_gemm_emulation (read at every launch: a captured graph keeps its kernels)
-static std::atomic<int> g_emu{-1};
-static bool emu_bf16x6() {
-  int v = g_emu.load(std::memory_order_relaxed);
-  if (v < 0) {
-    int expect = -1;
-    g_emu.compare_exchange_strong(expect, getenv_flag("RGAN_EMU_BF16X6") ? 1 : 0);
-    v = g_emu.load(std::memory_order_relaxed);
-  }
-  return v == 1;
-}
+// FAST 128x128 CONV / CONVT2 GEMMs (fwd + dgrad of Conv and ConvT) on the bf16x6 emulation: opt-in
+// by rgan_set_gemm_emulation (read at every launch: a captured graph keeps its kernels)
+static std::atomic<int> g_emu{0};
+static bool emu_bf16x6() { return g_emu.load(std::memory_order_relaxed) == 1; }
 static bool plan_emu(const Plan& p) {
   return p.fast && p.cfg == CFG_L && (p.mode == MODE_CONV || p.mode == MODE_CONVT2) && emu_bf16x6();
 }
@@ -2749,10 +2740,7 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
     // (32-channel tiles when the width is not a multiple of 128: D at h = 32, 64)
     const int tiles = a.B * a.Ho * a.Wo / 32;
     const bool wide = a.Cout % 128 == 0;
-#ifndef RGAN_IMG_GRID
-#define RGAN_IMG_GRID 512
-#endif
-    const dim3 grid(std::min(ceil_div(tiles, 4), RGAN_IMG_GRID), a.Cout / (wide ? 128 : 32));
+    const dim3 grid(std::min(ceil_div(tiles, 4), 512), a.Cout / (wide ? 128 : 32));
     const int act_kind = a.act == RGAN_ACT_NONE ? 0
                          : (a.act == RGAN_ACT_RELU || (a.act == RGAN_ACT_LRELU && a.alpha <= 1.f)) ? 1 : 2;
 #define RGAN_IMG_A(CC, WW, NN)                                                            \
@@ -2831,8 +2819,7 @@ static bool red_vec_ok(const Plan& p, bool check_ptr) {
 
 static bool bn_reduce_ok(const Plan& p, bool check_ptr) {
   const GemmArgs& g = p.g;
-  static const bool off = getenv_flag("RGAN_NO_REDUCE_BN");  // A/B switch
-  if (off || (p.mode != MODE_CONV && p.mode != MODE_CONVT2)) return false;
+  if (p.mode != MODE_CONV && p.mode != MODE_CONVT2) return false;
   if (g.splits <= 1 || p.tap_stage || g.accum || !red_vec_ok(p, check_ptr) || g.N < 4 * REDBN_QB) return false;
   if (g.out.fnc.d != (uint32_t)g.N || g.M % 64 != 0 || p.bn_segs < 1) return false;
   if (p.bn_segs > 1 && (p.phases != 1 || g.M % p.bn_segs != 0 || (g.M / p.bn_segs) % 64 != 0)) return false;

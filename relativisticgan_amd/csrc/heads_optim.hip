@@ -298,9 +298,11 @@ extern "C" int rgan_gp_penalty(const float* g, int batch, long long per, float l
   return 0;
 }
 
-__global__ void gp_bwd_kernel(const float* __restrict__ g, const float* __restrict__ norms, int batch,
+// dg may alias g (the GP engine rewrites the gradient image in place): each thread reads
+// g[i] and then writes dg[i], so neither pointer is __restrict__
+__global__ void gp_bwd_kernel(const float* g, const float* __restrict__ norms, int batch,
                               long long per, float lam, int n_global, const float* gscale,
-                              float* __restrict__ dg) {
+                              float* dg) {
   const long long total = (long long)batch * per;
   const float gs = gscale ? gscale[0] : 1.f;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;

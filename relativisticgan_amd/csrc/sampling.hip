@@ -59,52 +59,80 @@ __global__ __launch_bounds__(256) void rng_fill(float* out, long long n, int kin
 
 __global__ void rng_advance(unsigned long long* counter, unsigned long long by) { counter[0] += by; }
 
-// n distinct indices of [0, N) (Floyd's algorithm: for j = N-n .. N-1 take t uniform in
-// [0, j], or j itself when t is already taken), one wave, output in draw order; the wave
-// advances the counter itself (every lane read it before lane 0 writes).
+// n distinct indices of [0, N) in uniformly random order, like numpy.random.choice(N, n,
+// replace=False) (every ordered n-tuple equally likely; callers split the draw by position:
+// data-parallel shards, PacGAN slots).  Floyd's algorithm (for j = N-n .. N-1 take t
+// uniform in [0, j], or j itself when t is already taken) picks a uniform SET, but step s
+// yields j = N-n+s on a collision, so late positions lean to high indices; a Fisher-Yates
+// pass over the n picks then makes the order uniform.  Uniform integers in [0, m) are
+// 64 random bits x m >> 64 (bias <= m / 2^64).  One wave; counters base .. base+n-1 feed
+// Floyd, base+n .. base+2n-1 the shuffle; the wave advances the counter by 2n itself
+// (every lane read it before lane 0 writes).
 //   n <= 64: lane s draws step s and keeps its pick in a register; each step broadcasts its
-//            t, the lanes holding earlier picks compare, a ballot decides (no LDS, no barrier);
-//   else:    the taken set in LDS, the membership test a ballot over it.
+//            t, the lanes holding earlier picks compare, a ballot decides (no LDS, no
+//            barrier); the shuffle swaps registers through wave shuffles;
+//   else:    the taken set in LDS, the membership test a ballot over it; the shuffle's
+//            swap positions drawn lane-parallel, the swaps by one lane.
 constexpr int CHOICE_MAX = 4096;
+
+__device__ __forceinline__ int uniform_below(const u32x4s& r, unsigned long long m) {
+  return (int)__umul64hi(((unsigned long long)r.y << 32) | r.x, m);
+}
 
 __global__ __launch_bounds__(64) void rng_choice_small(long long* out, int N, int n, unsigned long long seed,
                                                        unsigned long long* counter) {
   const unsigned long long base = counter[0];
   const int lane = threadIdx.x;
   int t_own = 0, pick = -1;  // -1: no pick yet (never equal to a draw)
+  int j_own = 0;  // Fisher-Yates: position `lane` swaps with j_own, uniform in [0, lane]
   if (lane < n) {
     const u32x4s r = philox(base + (unsigned long long)lane, seed);
-    t_own = (int)(((unsigned long long)r.x * (unsigned long long)(N - n + lane + 1)) >> 32);
+    t_own = uniform_below(r, (unsigned long long)(N - n + lane + 1));
+    j_own = uniform_below(philox(base + (unsigned long long)(n + lane), seed), (unsigned long long)(lane + 1));
   }
   for (int s = 0; s < n; ++s) {
     const int t = __shfl(t_own, s);
     const bool any = __ballot(pick == t) != 0;
     if (lane == s) pick = any ? N - n + s : t;
   }
+  for (int s = n - 1; s >= 1; --s) {
+    const int j = __shfl(j_own, s);
+    const int ps = __shfl(pick, s), pj = __shfl(pick, j);
+    if (lane == s) pick = pj;
+    else if (lane == j) pick = ps;
+  }
   if (lane < n) out[lane] = pick;
-  if (lane == 0) counter[0] = base + (unsigned long long)n;
+  if (lane == 0) counter[0] = base + 2ULL * (unsigned long long)n;
 }
 
 __global__ __launch_bounds__(64) void rng_choice(long long* out, int N, int n, unsigned long long seed,
                                                  unsigned long long* counter) {
   __shared__ int taken[CHOICE_MAX];
+  __shared__ int swap_with[CHOICE_MAX];
   const unsigned long long base = counter[0];
   const int lane = threadIdx.x;
+  for (int s = lane; s < n; s += 64)
+    swap_with[s] = uniform_below(philox(base + (unsigned long long)(n + s), seed), (unsigned long long)(s + 1));
   for (int s = 0; s < n; ++s) {
     const int j = N - n + s;
     const u32x4s r = philox(base + (unsigned long long)s, seed);
-    const int t = (int)(((unsigned long long)r.x * (unsigned long long)(j + 1)) >> 32);
+    const int t = uniform_below(r, (unsigned long long)(j + 1));
     bool hit = false;
     for (int i = lane; i < s; i += 64) hit |= taken[i] == t;
     const bool any = __ballot(hit) != 0;
-    const int pick = any ? j : t;
-    if (lane == 0) {
-      taken[s] = pick;
-      out[s] = pick;
-    }
+    if (lane == 0) taken[s] = any ? j : t;
     __syncthreads();
   }
-  if (lane == 0) counter[0] = base + (unsigned long long)n;
+  if (lane == 0) {
+    for (int s = n - 1; s >= 1; --s) {
+      const int j = swap_with[s], v = taken[s];
+      taken[s] = taken[j];
+      taken[j] = v;
+    }
+  }
+  __syncthreads();
+  for (int s = lane; s < n; s += 64) out[s] = taken[s];
+  if (lane == 0) counter[0] = base + 2ULL * (unsigned long long)n;
 }
 
 }  // namespace rgan

@@ -6,7 +6,6 @@ allocator and launches on the current stream.  Internal activations are NHWC
 wherever the reference hands them over (images into D, out of G).
 """
 import ctypes
-import os
 import weakref
 from dataclasses import dataclass
 
@@ -282,11 +281,6 @@ def conv_fwd(x, w, geom, bias=None, act="none", alpha=0.0, wscale=None, out=None
     return out
 
 
-# BatchNorm batch statistics from the conv GEMM's epilogue (rgan_conv_fwd_bn); "0" = always
-# the separate moments pass (A/B switch and parity cross-check).
-BN_EPILOGUE = os.environ.get("RGAN_BN_EPILOGUE", "1") != "0"
-
-
 def conv_fwd_bn(x, w, geom, bias=None, wscale=None, cache=False, segs=1):
     """y = conv(x, w)*wscale + bias (NHWC) for a layer followed by train-mode BatchNorm.
 
@@ -294,7 +288,7 @@ def conv_fwd_bn(x, w, geom, bias=None, wscale=None, cache=False, segs=1):
     layer, ``part`` is
     its per-64-row segment sums (sum y, sum y^2) double[S][2][C] (merge with bn_segment_stats; batch
     segment k = segments [k*S/segs, (k+1)*S/segs)); otherwise (y, None, 0)."""
-    if geom.upsample != 1 or not BN_EPILOGUE:
+    if geom.upsample != 1:
         return conv_fwd(x, w, geom, bias=bias, wscale=wscale, cache=cache), None, 0
     L.require_cuda(x, w, bias, wscale)
     _f32(x, w, bias)
@@ -702,6 +696,8 @@ def gp_penalty(g, lam, n_global):
 
 
 def gp_penalty_backward(g, norms, lam, n_global, gscale, out=None):
+    """dGP/dg = gscale * lam * 2 (n_b - 1) / n_global * g / n_b per sample b.  ``out`` may be
+    ``g`` itself (in place: each element is read before it is written)."""
     B = g.shape[0]
     if not g.is_contiguous():
         raise L.RganError("gp_penalty_backward: g must be contiguous")

@@ -10,16 +10,11 @@ layouts of the updated weights are then repacked in one batched launch.  Hyper-p
 device buffer (doubles, as torch keeps them in Python floats), refreshed only when a
 group's values change; the step counter is a device scalar incremented by the kernel.
 """
-import os
 
 import torch
 from torch.autograd.graph import increment_version
 
 from . import kernels as K
-
-# RGAN_REFRESH_PACKS=0: leave repacking to the next convolution of each weight (A/B switch)
-REFRESH_PACKS = os.environ.get("RGAN_REFRESH_PACKS", "1") != "0"
-
 
 class Adam(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, amsgrad=False):
@@ -92,8 +87,7 @@ class Adam(torch.optim.Optimizer):
             for p in ps:
                 self.state[p]["step"] += 1  # host mirror of state['step'] (torch Adam's state_dict layout)
                 increment_version(p)        # the kernel wrote p: invalidate cached packed layouts
-            if REFRESH_PACKS:
-                K.PACKS.refresh(ps)  # ... and repack the ones in use, in one batched launch
+            K.PACKS.refresh(ps)  # ... and repack the ones in use, in one batched launch
         return loss
 
     def load_state_dict(self, state_dict):

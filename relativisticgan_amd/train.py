@@ -84,8 +84,11 @@ class Trainer:
         self.redG = dp.GradReducer(self.G.parameters()) if self.world > 1 else None
         self._pending_G, self._pending_decay_G = None, False
         self.host_rng = getattr(p, "rgan_rng", "host") == "host"
+        if not self.host_rng and self.device.type != "cuda":
+            raise ValueError("--rgan_rng device draws in HIP kernels: it needs a CUDA (HIP) device, "
+                             f"got {self.device}; use --rgan_rng host")
         # --rgan_rng device: counter-based draws in HIP kernels (same seed on every rank)
-        self.dev_rng = (None if self.host_rng or self.device.type != "cuda" else
+        self.dev_rng = (None if self.host_rng else
                         DeviceRNG(p.seed if p.seed is not None else torch.initial_seed(), self.device))
         self.pac = getattr(p, "pac", 1)  # 2: code/GAN_losses_iter_PAC.py
         # one batched D pass per D step where the nets allow it (--rgan_batch_D).  Default

@@ -691,6 +691,24 @@ def test_conv_image_window_kernel(K, ci, hw, cout):
     assert _rel(dx, x64.grad) < 3e-6
 
 
+@pytest.mark.parametrize("B,S,C", [(32, 128, 128), (64, 128, 128), (8, 256, 128), (32, 256, 32), (16, 256, 128)])
+def test_conv_image_window_full_batch(K, B, S, C):
+    """conv_img_in at the BASELINE batch sizes, where every persistent wave runs several
+    tiles and two blocks share a CU (C2's batched D pass: 128 x 128^2; C3: 256^2; C3 at
+    h = 32: 32-channel tiles): each sample's outputs vs torch fp64.  The bounded per-sample
+    max error catches the two faults smaller grids never reached: a wide store's data VGPR
+    rewritten behind it (lanes 12-15 of every 16) and a window read before its DMA landed."""
+    g = K.ConvGeom(4, 2, 1, False)
+    torch.manual_seed(B + S + C)
+    img = torch.rand(B, 3, S, S, device=DEV) * 2 - 1
+    w = torch.nn.Parameter(torch.randn(C, 3, 4, 4, device=DEV) * 0.05)
+    y = K.conv_fwd(img, w, g, act="lrelu", alpha=0.2, cache=True)
+    torch.cuda.synchronize()
+    ref = F.leaky_relu(F.conv2d(img.double().cpu(), w.detach().double().cpu(), stride=2, padding=1), 0.2)
+    err = (y.double().cpu() - ref).abs().flatten(1).amax(1) / ref.abs().amax()
+    assert err.max().item() < 1e-6, f"samples off: {(err > 1e-6).nonzero().flatten().tolist()[:16]}"
+
+
 def test_pack_batch_refresh(K):
     """PACKS.refresh (one rgan_conv_pack_batch launch after an optimizer step) leaves every
     cached layout bitwise equal to a fresh single pack: 4x4 tiled16 (fwd, ConvT phases),
@@ -752,6 +770,18 @@ def test_device_rng(K):
     for _ in range(200):
         counts.index_add_(0, a.choice(20, 5), torch.ones(5, device=DEV))
     assert counts.min().item() > 20 and counts.max().item() < 80  # ~50 each
+    # positional uniformity (numpy.random.choice's order is exchangeable; callers split the
+    # draw by position): every position's index is uniform over [0, N): chi-square per
+    # position below N - 1 + 6 sd, for the wave path (n <= 64) and the LDS path
+    for N, n, reps in ((12, 8, 3000), (100, 80, 600)):
+        pos = torch.zeros(n, N, dtype=torch.float64)
+        for _ in range(reps):
+            d = a.choice(N, n).cpu()
+            assert d.unique().numel() == n
+            pos[torch.arange(n), d] += 1
+        exp = reps / N
+        chi = ((pos - exp) ** 2 / exp).sum(1)
+        assert chi.max().item() < N - 1 + 6 * (2 * (N - 1)) ** 0.5, (N, n, chi.max().item())
     g = torch.cuda.CUDAGraph()
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())

@@ -120,3 +120,30 @@ def test_nets_vs_fp64_torch(case):
     for (n, b), (_, b32), (_, b64) in zip(D.named_buffers(), Do32.named_buffers(), Do64.named_buffers()):
         if "running" in n:
             env(n, b, b32, b64, 1e-5)
+
+
+def test_weight_hooks_fire_in_trainer_backward():
+    """A fused layer writes its weight gradient into .grad itself inside the trainer's
+    backward (autograd.owning_grads) -- unless the weight carries a tensor hook or a
+    post-accumulate-grad hook, which only autograd's AccumulateGrad would fire: then the
+    gradient goes through autograd and the hooks run (and the result is the same)."""
+    from relativisticgan_amd.config import make_param
+    from relativisticgan_amd.train import Trainer
+    from oracle.reference_cpu import synthetic_images
+    kw = dict(loss_D=7, image_size=32, batch_size=8, z_size=16, G_h_size=8, D_h_size=8, seed=1, print_every=1000)
+    plain = Trainer(make_param(**kw), synthetic_images(64, 32).cuda())
+    hooked = Trainer(make_param(**kw), synthetic_images(64, 32).cuda())
+    wd = hooked.D.main[0].weight
+    wg = hooked.G.main[0].weight
+    fired = {"post": 0, "tensor": 0}
+    wd.register_post_accumulate_grad_hook(lambda p: fired.__setitem__("post", fired["post"] + 1))
+    wg.register_hook(lambda g: fired.__setitem__("tensor", fired["tensor"] + 1))
+    for t in (plain, hooked):
+        t.iteration(0)
+    torch.cuda.synchronize()
+    assert fired["post"] >= 1 and fired["tensor"] >= 1
+    # the two accumulation paths round differently (one vs two roundings of grad + dw), and
+    # Adam's first step is a sign step: parameters agree to 2 lr, buffers closely
+    for a, b in ((plain.D, hooked.D), (plain.G, hooked.G)):
+        for (n, x), (_, y) in zip(a.state_dict().items(), b.state_dict().items()):
+            assert torch.allclose(x.float(), y.float(), rtol=1e-5, atol=2.02e-4), n
