@@ -19,7 +19,11 @@ Prints ONE JSON line (rank 0).  Extra fields:
                   conv GEMMs on the bf16x6 fp32 emulation (rgan_set_gemm_emulation): its
                   throughput and roofline, priced against the bf16 MFMA peak / 6 products;
   cpu_baseline -- the oracle (CPU restatement of the reference step, torch CPU fp32) on
-                  a bounded sample of the same workload on this host (rank 0, N=1).
+                  a bounded sample of the same workload on this host (rank 0, N=1); C1's
+                  own (>= 5 timed iterations) under extra_workloads.C1;
+  dp_path_n1   -- (N=1) the workload (and C1) run exactly as each rank of an N>1 run does
+                  (separate D(x) / D(x_fake) passes, eager launches): the like-for-like
+                  baseline of the scaling runs.
 Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
 """
 import argparse
@@ -146,10 +150,11 @@ def host_cpus():
             "physical_cores_in_affinity": len(cores) or None, "model": model}
 
 
-def cpu_baseline(loss_D, size, batch, h, spectral, seconds_hint, arch=0):
+def cpu_baseline(loss_D, size, batch, h, spectral, seconds_hint, arch=0, min_iters=1):
     """Oracle (CPU restatement, pinned bitwise to the reference) on this host's CPUs:
     every CPU the process is allowed (affinity, capped by the cgroup quota), 1 warm-up
-    iteration, then timed iterations until ~seconds_hint of CPU work or 5 iterations."""
+    iteration, then timed iterations until ~seconds_hint of CPU work or 5 iterations
+    (at least ``min_iters``)."""
     from oracle.reference_cpu import Trainer as OracleTrainer, make_param, synthetic_images
     cpus = host_cpus()
     threads = cpus["threads"]
@@ -163,7 +168,7 @@ def cpu_baseline(loss_D, size, batch, h, spectral, seconds_hint, arch=0):
         t.iteration(2 + n)
         n += 1
         el = time.perf_counter() - t0
-        if el > seconds_hint or n >= 5:
+        if (el > seconds_hint and n >= min_iters) or n >= max(5, min_iters):
             break
     return {"value": batch * n / el, "unit": "images/s", "cores": threads, "kind": "port",
             "cpu": cpus, "s_per_iter": el / n,
@@ -171,22 +176,25 @@ def cpu_baseline(loss_D, size, batch, h, spectral, seconds_hint, arch=0):
                       f"torch {torch.__version__} CPU fp32, {threads} threads on {cpus['model']}"}
 
 
-def run_workload(name, steps, warmup, world, args, K, emu=False):
+def run_workload(name, steps, warmup, world, args, K, emu=False, dp_path=False):
     """Train `steps` timed iterations of workload `name` (after `warmup`); returns the
-    measurement (max over ranks).  emu: forward / data-gradient GEMMs on bf16x6."""
+    measurement (max over ranks).  emu: forward / data-gradient GEMMs on bf16x6.  dp_path:
+    run one process exactly as every rank of an N > 1 run does (separate D(x) / D(x_fake)
+    passes, eager launches, no HIP graph) -- the like-for-like N = 1 baseline of the scaling
+    runs."""
     prev_emu = K.set_gemm_emulation(emu)
     try:
-        return _run_workload(name, steps, warmup, world, args, K)
+        return _run_workload(name, steps, warmup, world, args, K, dp_path)
     finally:
         K.set_gemm_emulation(prev_emu)
 
 
-def _run_workload(name, steps, warmup, world, args, K):
+def _run_workload(name, steps, warmup, world, args, K, dp_path=False):
     from relativisticgan_amd.config import make_param
     from relativisticgan_amd.train import Trainer, synthetic_images
     loss_D, size, bpg, h = WORKLOADS[name]
     spectral = name == "C5"
-    bd = {"auto": None, "on": True, "off": False}[args.batch_d]
+    bd = False if dp_path else {"auto": None, "on": True, "off": False}[args.batch_d]
     p = make_param(loss_D=loss_D, image_size=size, batch_size=bpg * world, G_h_size=h, D_h_size=h, seed=1,
                    print_every=10 ** 9, spectral=spectral, rgan_rng="device", arch=ARCH.get(name, 0),
                    rgan_batch_D=bd)
@@ -194,7 +202,7 @@ def _run_workload(name, steps, warmup, world, args, K):
     t = Trainer(p, images)
     flops_iter = conv_flops_per_iteration(t)
 
-    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+    use_graph = not dp_path and (args.graph == "on" or (args.graph == "auto" and world == 1))
     # graph mode runs every iteration on one side stream: autograd's per-parameter
     # AccumulateGrad nodes keep the stream of the first backward, and the captured backward
     # must accumulate on the capturing stream
@@ -310,6 +318,8 @@ def main():
     ap.add_argument("--no-emu-extra", action="store_true",
                     help="skip the N=1 re-run of the workload with the bf16x6 fp32-emulated GEMMs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dp-path", action="store_true",
+                    help="skip the N=1 runs of the data-parallel launch mode (dp_path_n1)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--sync-bn", action="store_true",
                     help="SyncBN over ranks (default: per-shard BN = the reference's DataParallel)")
@@ -335,7 +345,7 @@ def main():
     emu_res = None
     if world == 1 and not args.no_emu_extra:
         emu_res = run_workload(args.workload, args.steps, min(args.warmup, 5), world, args, K, emu=True)
-    extras = {}
+    extras, dp_paths = {}, {}
     if world == 1:
         for name in [w for w in args.extra.split(",") if w and w != args.workload]:
             r = run_workload(name, args.steps, min(args.warmup, 5), world, args, K)
@@ -343,6 +353,14 @@ def main():
                             "ms_per_step": r["ms_per_step"], "steps": r["steps"], "hip_graph": r["graph"],
                             "step_mfma_util": r["flops_iter"] / (r["ms_per_step"] / 1000.0) / FP32_MFMA_PEAK,
                             "roofline": {k: v for k, v in roofline_of(r, name).items() if k != "conv_family"}}
+            if name == "C1" and not args.no_cpu_baseline:
+                extras[name]["cpu_baseline"] = cpu_baseline(r["loss_D"], r["size"], r["bpg"], r["h"], r["spectral"],
+                                                            args.cpu_seconds, arch=r["arch"], min_iters=5)
+        if not args.no_dp_path:
+            for name in [args.workload] + [w for w in ("C1",) if w in args.extra.split(",")]:
+                r = run_workload(name, args.steps, min(args.warmup, 5), world, args, K, dp_path=True)
+                dp_paths[name] = {"value": r["value"], "unit": "images/s", "ms_per_step": r["ms_per_step"],
+                                  "steps": r["steps"], "batched_D_step": r["batch_D"], "hip_graph": r["graph"]}
     if rank != 0:
         torch.distributed.destroy_process_group()
         return
@@ -361,6 +379,10 @@ def main():
     }
     if extras:
         out["extra_workloads"] = extras
+    if dp_paths:
+        # what each rank of the N > 1 runs executes (separate D passes, eager), on one GPU:
+        # the like-for-like N = 1 baseline for the scaling efficiency of `value` at N > 1
+        out["dp_path_n1"] = dp_paths
     if emu_res is not None:
         out["fp32_emulated_bf16x6"] = {
             "value": emu_res["value"], "unit": "images/s", "ms_per_step": emu_res["ms_per_step"],

@@ -335,6 +335,24 @@ int rgan_spectral_backward(const float* W, const float* dWeff, int rows, int col
 int rgan_adam(int ntensors, float* const* params, const float* const* grads,
               float* const* exp_avg, float* const* exp_avg_sq, const long long* numel,
               const double* hyper, float* step, void* stream);
+/* step[0] += 1 (the bump rgan_adam / rgan_adam_packed issue before the update). */
+int rgan_adam_step_inc(float* step, void* stream);
+/* rgan_adam that also writes the cached GEMM layouts of the weights it updates (what
+ * rgan_conv_pack(d, which, w, packed) would produce from the new values), instead of a
+ * repack pass reading every weight again after the step.  packs[i].tensor indexes the
+ * params arrays; layouts the Adam kernel cannot write (non-contiguous weights, generic
+ * packs) are repacked by their own launch after it, so every listed layout is current
+ * when the call's work completes. */
+typedef struct RganAdamPack {
+  int tensor;
+  int which;               /* 0 forward layout, 1 data-gradient layout (rgan_conv_pack) */
+  const RganConv* d;       /* the descriptor the layout was packed for */
+  float* packed;           /* rgan_conv_pack_floats(d, which) floats */
+} RganAdamPack;
+int rgan_adam_packed(int ntensors, float* const* params, const float* const* grads,
+                     float* const* exp_avg, float* const* exp_avg_sq, const long long* numel,
+                     const double* hyper, float* step, int npacks, const RganAdamPack* packs,
+                     void* stream);
 /* hyper[0] *= gamma (ExponentialLR.step, GLI:533-534,713-714). */
 int rgan_lr_decay(double* hyper, double gamma, void* stream);
 

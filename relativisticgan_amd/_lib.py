@@ -25,6 +25,10 @@ class RganConv(ctypes.Structure):
                 ("transposed", c_int), ("xs", c_ll * 4), ("ys", c_ll * 4)]
 
 
+class RganAdamPack(ctypes.Structure):
+    _fields_ = [("tensor", c_int), ("which", c_int), ("d", ctypes.POINTER(RganConv)), ("packed", c_vp)]
+
+
 class RganSnLayer(ctypes.Structure):
     _fields_ = [("W", c_vp), ("rows", c_int), ("cols", c_int), ("lo", c_int), ("rs", c_ll), ("hs", c_ll),
                 ("u", c_vp), ("v", c_vp), ("u_copy", c_vp), ("v_copy", c_vp), ("inv_sigma", c_vp)]
@@ -99,6 +103,8 @@ _SIGS = {
     "rgan_spectral_backward": (c_int, [c_vp, c_vp, c_int, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
                                        c_vp, c_vp]),
     "rgan_adam": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "rgan_adam_packed": (c_int, [c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "rgan_adam_step_inc": (c_int, [c_vp, c_vp]),
     "rgan_lr_decay": (c_int, [c_vp, c_d, c_vp]),
     "rgan_gather_images": (c_int, [c_vp, c_vp, c_int, c_ll, c_vp, c_vp]),
     "rgan_rng_fill": (c_int, [c_vp, c_ll, c_int, ctypes.c_ulonglong, c_vp, c_vp]),

@@ -294,7 +294,8 @@ class ConvLayerFn(torch.autograd.Function):
             if nw or nb:
                 g1, db = K.conv_wgrad(K.patches_k4s2(x), dy, K.G1X1, (w.shape[0], 64, 1, 1),
                                       with_bias=bias is not None and nb)
-                dw = K.unpatch_grad(g1, w.shape[0], w.shape[1], 64, 1)
+                dw = K.unpatch_grad(g1, w.shape[0], w.shape[1], 64, 1,
+                                    into=dp.grad_view(w) if nw and not spec.spectral else None)
         elif ConvLayerFn._patch_convt(spec, w, bias):
             # image-side ConvTranspose2d (G's last layer): both gradients are 1x1 GEMMs over
             # the patch matrix of the image gradient, on x's grid
@@ -303,7 +304,8 @@ class ConvLayerFn(torch.autograd.Function):
             dw = db = None
             if nw:
                 g1, _ = K.conv_wgrad(Xg, x, K.G1X1, (w.shape[0], 64, 1, 1))
-                dw = K.unpatch_grad(g1, w.shape[0], w.shape[1], 64, 1)
+                dw = K.unpatch_grad(g1, w.shape[0], w.shape[1], 64, 1,
+                                    into=dp.grad_view(w) if not spec.spectral else None)
         else:
             dx = K.conv_dgrad(dy, w, spec.geom, tuple(x.shape), wscale=wscale, like=x, cache=True) if nx else None
             dw = db = None
@@ -325,7 +327,11 @@ class ConvLayerFn(torch.autograd.Function):
                     w.grad = g
                 return dx, None, None, dgamma, dbeta, None, None, None, None, None
             if nw or nb:
-                dw, db = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), with_bias=bias is not None and nb)
+                # data parallel: the weight gradient lands in its gradient bucket's slice
+                # (dp.grad_view), which autograd then adopts as .grad (no bucket copy)
+                into = (dp.grad_view(w) if nw and not (bias is not None and nb) and not spec.spectral
+                        and spec.geom.upsample == 1 else None)
+                dw, db = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), with_bias=bias is not None and nb, into=into)
         if nw or nb:
             if spec.spectral and nw:
                 u, v, inv_sigma = sn

@@ -164,4 +164,39 @@ __device__ __forceinline__ double block_sum_d(double v, double* red) {
 
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// ---- Adam (torch/optim/adam.py _single_tensor_adam, the reference's optimizer GLI:529-530):
+// the per-step constants in double (torch computes them in Python floats), the update in fp32
+// with torch's operation order (lerp for m; v * b2 + (1 - b2) g^2; sqrt(v) / sqrt(bc2) + eps)
+struct AdamConst {
+  float neg_step, bc2s, w, fb2, f1mb2, feps, fwd;
+  bool has_wd;
+};
+
+// hyper = {lr, beta1, beta2, eps, weight_decay}; step = the step being taken (>= 1)
+__device__ __forceinline__ AdamConst adam_const(const double* hyper, const float* step) {
+  const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
+  const double st = (double)step[0];
+  const double bc1 = 1.0 - pow(b1, st), bc2 = 1.0 - pow(b2, st);
+  AdamConst k;
+  k.neg_step = (float)(-(lr / bc1));
+  k.bc2s = (float)sqrt(bc2);
+  k.w = (float)(1.0 - b1);
+  k.fb2 = (float)b2;
+  k.f1mb2 = (float)(1.0 - b2);
+  k.feps = (float)eps;
+  k.fwd = (float)wd;
+  k.has_wd = wd != 0.0;
+  return k;
+}
+
+__device__ __forceinline__ void adam_elem(const AdamConst& k, float g, float& p, float& m, float& v) {
+  if (k.has_wd) g = g + k.fwd * p;
+  const float diff = g - m;
+  m = k.w < 0.5f ? m + k.w * diff : g - diff * (1.f - k.w);
+  v = v * k.fb2;
+  v = v + k.f1mb2 * g * g;
+  const float denom = sqrtf(v) / k.bc2s + k.feps;
+  p = p + k.neg_step * (m / denom);
+}
+
 }  // namespace rgan

@@ -2140,6 +2140,176 @@ __global__ __launch_bounds__(256) void pack_multi(PackBatch b) {
   else pack_tiled_body(b.a[j], bx, by, t);
 }
 
+// ---------------------------------------------------------------- Adam writing the GEMM layouts
+// The optimizer step (GLI:659, 712) rewrites every weight; the conv GEMMs read packed copies
+// ([phase][N][K], tiled16 / t2d / narrow layouts above).  Re-reading each weight after Adam
+// to repack it cost 8 B per weight element and a launch per net (pack_multi: 2.9 GB, 0.57 ms
+// per C3 iteration); here the Adam kernel writes the packed copies of the values it has in
+// registers.  Weight viewed [A][B][KK] (contiguous); per cached layout:
+//   APK_TILED   out[((phase Nout + o) K + kt Nin + i)], (i, o) = (a, b) or (b, a), the tap
+//               -> (phase, kt) map of pack_tiled_body (flip / 4 sub-pixel phases);
+//   APK_T2D     out[(tap Cout + co) K + ci]  (G's 1x1 -> 4x4 first layer, pack_t2d);
+//   APK_NARROW  out[ci 256 + (t >> 2) 64 + (t & 3) 16 + x 4 + co], x = 0..3 (pack_narrow).
+// A tensor whose layouts are all 4x4-tap tiled with A, B multiples of 32 runs as 32 x 32 x 16
+// bricks: Adam on the brick (coalesced 2-KB rows), the new values into LDS, then each layout
+// written as float4 runs of 4 consecutive in-indices (pack_tiled16's store pattern); other
+// tensors run the flat 4096-element blocks of adam_kernel with per-element scatters.
+enum { APK_TILED = 0, APK_T2D = 1, APK_NARROW = 2 };
+struct AdamPackT {
+  float* out;
+  int kind, in_is_a, A, B, KK, KW, flip, convt2, Nin, Nout, K, NC;
+};
+struct AdamPackTensor {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  long long n;
+  int brick, bricks_b, pk0, npk;
+};
+constexpr int AP_MAXT = 24, AP_MAXP = 24, AP_BRICK = 32 * 32 * 16, AP_FLAT = 4096, AP_TLD = 32 * 17;
+struct AdamPackBatch {
+  AdamPackTensor t[AP_MAXT];
+  AdamPackT pk[AP_MAXP];
+  int first[AP_MAXT + 1];
+  int cnt;
+};
+
+__device__ __forceinline__ long long apk_tiled_dst(const AdamPackT& t, int a, int b, int tap) {
+  const int i = t.in_is_a ? a : b, o = t.in_is_a ? b : a;
+  const int kh = tap / t.KW, kw = tap - kh * t.KW;
+  int phase = 0, kt;
+  if (t.convt2) {
+    phase = (1 - (kh & 1)) * 2 + (1 - (kw & 1));
+    kt = (kh >> 1) * 2 + (kw >> 1);
+  } else {
+    kt = t.flip ? t.KK - 1 - tap : tap;
+  }
+  return ((long long)phase * t.Nout + o) * t.K + (long long)kt * t.Nin + i;
+}
+
+// element e (flat index of the [A][B][KK] weight) with its new value into one layout
+__device__ __forceinline__ void apk_scatter(const AdamPackT& t, long long e, float val) {
+  const int tap = (int)(e % t.KK);
+  const long long r = e / t.KK;
+  const int a = (int)(r / t.B), b = (int)(r - (long long)a * t.B);
+  if (t.kind == APK_TILED) {
+    t.out[apk_tiled_dst(t, a, b, tap)] = val;
+  } else if (t.kind == APK_T2D) {
+    t.out[((long long)tap * t.B + b) * t.K + a] = val;
+  } else {
+    const long long o = (long long)a * 256 + (tap >> 2) * 64 + (tap & 3) * 16 + b;
+#pragma unroll
+    for (int x = 0; x < 4; ++x) t.out[o + 4 * x] = val;
+  }
+}
+
+__global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackBatch b, const double* __restrict__ hyper,
+                                                        const float* __restrict__ step) {
+  __shared__ float T[32 * AP_TLD];  // brick [a][b][tap] (tap stride 17: conflict-light column reads)
+  int j = 0;
+  while (j + 1 < b.cnt && (int)blockIdx.x >= b.first[j + 1]) ++j;
+  const AdamPackTensor X = b.t[j];
+  const AdamConst k = adam_const(hyper, step);
+  const int local = (int)blockIdx.x - b.first[j], tid = threadIdx.x;
+  if (X.brick) {
+    const AdamPackT& t0 = b.pk[X.pk0];
+    const int B = t0.B, a0 = 32 * (local / X.bricks_b), b0 = 32 * (local % X.bricks_b);
+    for (int pass = 0; pass < 4; ++pass) {  // 8 rows of 32 b x 16 taps (2 KB contiguous) per pass
+      float4 P[4], G[4], M[4], V[4];
+      long long off[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int jj = tid + 256 * u, al = 8 * pass + (jj >> 7), f = jj & 127;
+        off[u] = ((long long)(a0 + al) * B + b0) * 16 + 4 * f;
+        P[u] = *reinterpret_cast<const float4*>(X.p + off[u]);
+        G[u] = *reinterpret_cast<const float4*>(X.g + off[u]);
+        M[u] = *reinterpret_cast<const float4*>(X.m + off[u]);
+        V[u] = *reinterpret_cast<const float4*>(X.v + off[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        adam_elem(k, G[u].x, P[u].x, M[u].x, V[u].x);
+        adam_elem(k, G[u].y, P[u].y, M[u].y, V[u].y);
+        adam_elem(k, G[u].z, P[u].z, M[u].z, V[u].z);
+        adam_elem(k, G[u].w, P[u].w, M[u].w, V[u].w);
+        *reinterpret_cast<float4*>(X.m + off[u]) = M[u];
+        *reinterpret_cast<float4*>(X.v + off[u]) = V[u];
+        *reinterpret_cast<float4*>(X.p + off[u]) = P[u];
+        const int jj = tid + 256 * u, al = 8 * pass + (jj >> 7), f = jj & 127, bl = f >> 2, tq = f & 3;
+        float* d = T + al * AP_TLD + bl * 17 + 4 * tq;
+        d[0] = P[u].x; d[1] = P[u].y; d[2] = P[u].z; d[3] = P[u].w;
+      }
+    }
+    __syncthreads();
+    for (int q = 0; q < X.npk; ++q) {
+      const AdamPackT& t = b.pk[X.pk0 + q];
+#pragma unroll 4
+      for (int u = 0; u < 16; ++u) {  // 32 x 16 x 8 float4 of 4 consecutive in-indices
+        const int jj = tid + 256 * u, iq = jj & 7, tap = (jj >> 3) & 15, ol = jj >> 7;
+        float4 v4;
+        long long dst;
+        if (t.in_is_a) {  // in = a: T[4 iq + c][ol][tap]
+          const float* s = T + (4 * iq) * AP_TLD + ol * 17 + tap;
+          v4 = make_float4(s[0], s[AP_TLD], s[2 * AP_TLD], s[3 * AP_TLD]);
+          dst = apk_tiled_dst(t, a0 + 4 * iq, b0 + ol, tap);
+        } else {          // in = b: T[ol][4 iq + c][tap]
+          const float* s = T + ol * AP_TLD + (4 * iq) * 17 + tap;
+          v4 = make_float4(s[0], s[17], s[34], s[51]);
+          dst = apk_tiled_dst(t, a0 + ol, b0 + 4 * iq, tap);
+        }
+        *reinterpret_cast<float4*>(t.out + dst) = v4;
+      }
+    }
+    return;
+  }
+  const long long e0 = (long long)local * AP_FLAT, e1 = min(X.n, e0 + AP_FLAT);
+  const bool vec = (X.n & 3) == 0 && ((((uintptr_t)X.p | (uintptr_t)X.g | (uintptr_t)X.m | (uintptr_t)X.v) & 15) == 0);
+  if (vec) {
+    constexpr int U = AP_FLAT / 1024;
+    float4 P[U], G[U], M[U], V[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = e0 + 4 * (tid + 256 * u);
+      if (i < e1) {
+        P[u] = *reinterpret_cast<const float4*>(X.p + i);
+        G[u] = *reinterpret_cast<const float4*>(X.g + i);
+        M[u] = *reinterpret_cast<const float4*>(X.m + i);
+        V[u] = *reinterpret_cast<const float4*>(X.v + i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = e0 + 4 * (tid + 256 * u);
+      if (i < e1) {
+        adam_elem(k, G[u].x, P[u].x, M[u].x, V[u].x);
+        adam_elem(k, G[u].y, P[u].y, M[u].y, V[u].y);
+        adam_elem(k, G[u].z, P[u].z, M[u].z, V[u].z);
+        adam_elem(k, G[u].w, P[u].w, M[u].w, V[u].w);
+        *reinterpret_cast<float4*>(X.m + i) = M[u];
+        *reinterpret_cast<float4*>(X.v + i) = V[u];
+        *reinterpret_cast<float4*>(X.p + i) = P[u];
+        for (int q = 0; q < X.npk; ++q) {
+          const AdamPackT& t = b.pk[X.pk0 + q];
+          apk_scatter(t, i, P[u].x);
+          apk_scatter(t, i + 1, P[u].y);
+          apk_scatter(t, i + 2, P[u].z);
+          apk_scatter(t, i + 3, P[u].w);
+        }
+      }
+    }
+  } else {
+    for (long long i = e0 + tid; i < e1; i += 256) {
+      float p = X.p[i], m = X.m[i], v = X.v[i];
+      adam_elem(k, X.g[i], p, m, v);
+      X.m[i] = m;
+      X.v[i] = v;
+      X.p[i] = p;
+      for (int q = 0; q < X.npk; ++q) apk_scatter(b.pk[X.pk0 + q], i, p);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- host planning
 enum { CFG_L = 0, CFG_M = 1, CFG_N = 2 };
 
@@ -3048,6 +3218,114 @@ extern "C" int rgan_conv_pack_batch(int n, const RganConv* const* d, const int* 
   }
   flush();
   RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int rgan_adam_step_inc(float* step, void* stream);
+
+extern "C" int rgan_adam_packed(int ntensors, float* const* params, const float* const* grads,
+                                float* const* exp_avg, float* const* exp_avg_sq, const long long* numel,
+                                const double* hyper, float* step, int npacks, const RganAdamPack* packs,
+                                void* stream) {
+  RGAN_REQUIRE(ntensors >= 0 && npacks >= 0 && hyper && step && (npacks == 0 || packs));
+  hipStream_t s = (hipStream_t)stream;
+  alignas(16) static const float dummy[4] = {0, 0, 0, 0};
+  for (int j = 0; j < ntensors; ++j)
+    RGAN_REQUIRE(params[j] && grads[j] && exp_avg[j] && exp_avg_sq[j] && numel[j] >= 0 && numel[j] < (1LL << 31));
+  // plan every layout: in-kernel (AdamPackT) or a repack launch after the step
+  std::vector<std::vector<AdamPackT>> per(ntensors);
+  std::vector<Plan> later;
+  std::vector<float*> later_out;
+  for (int i = 0; i < npacks; ++i) {
+    const RganAdamPack& q = packs[i];
+    RGAN_REQUIRE(q.d && q.packed && q.tensor >= 0 && q.tensor < ntensors && (q.which == 0 || q.which == 1));
+    Plan p;
+    const float* W = params[q.tensor];
+    const int rc = q.which == 0 ? plan_fwd(q.d, dummy, W, nullptr, nullptr, (float*)dummy, 0, 0.f, p)
+                                : plan_dgrad(q.d, dummy, W, nullptr, (float*)dummy, p);
+    if (rc) return rc;
+    RGAN_REQUIRE(p.pack);
+    const long long n = numel[q.tensor];
+    AdamPackT t{};
+    t.out = q.packed;
+    bool ok = false;
+    const PackArgs& a = p.pk;
+    if (p.mode == MODE_NARROW_T) {
+      const int C = p.na.C, NC = p.na.Cout;
+      ok = p.pn_s_out == 16 && p.pn_s_in == 16LL * NC && (long long)C * NC * 16 == n;
+      t.kind = APK_NARROW; t.A = C; t.B = NC; t.KK = 16;
+    } else if (pack_t2d_ok(a)) {
+      const int T = a.KH * a.KW, Cout = (int)a.fnco.d;
+      ok = (long long)a.K * Cout * T == n;
+      t.kind = APK_T2D; t.A = a.K; t.B = Cout; t.KK = T; t.K = a.K;
+    } else {
+      int gx, gy;
+      const int kind = pack_kind(a, gx, gy);
+      const int KK = a.KH * a.KW, Nin = (int)a.fpci.d, Nout = a.N;
+      if (kind >= 0 && a.s_kw == 1 && a.s_kh == a.KW && (long long)Nin * Nout * KK == n) {
+        t.kind = APK_TILED; t.KK = KK; t.KW = a.KW; t.flip = a.flip; t.convt2 = a.convt2;
+        t.Nin = Nin; t.Nout = Nout; t.K = a.K;
+        if (a.s_in == KK && a.s_out == (long long)Nin * KK) {         // in = second index
+          ok = true; t.in_is_a = 0; t.A = Nout; t.B = Nin;
+        } else if (a.s_out == KK && a.s_in == (long long)Nout * KK) {  // in = first index
+          ok = true; t.in_is_a = 1; t.A = Nin; t.B = Nout;
+        }
+      }
+    }
+    if (ok) {
+      per[q.tensor].push_back(t);
+    } else {
+      later.push_back(p);
+      later_out.push_back(q.packed);
+    }
+  }
+  RGAN_CHECK_LAUNCH();
+  const int rs = rgan_adam_step_inc(step, stream);
+  if (rs) return rs;
+  AdamPackBatch b{};
+  long long blocks = 0;
+  int np = 0;
+  auto flush = [&]() -> int {
+    if (b.cnt == 0) return 0;
+    b.first[b.cnt] = (int)blocks;
+    if (blocks > 0) adam_pack_kernel<<<(unsigned)blocks, 256, 0, s>>>(b, hyper, step);
+    RGAN_CHECK_LAUNCH();
+    b = AdamPackBatch{};
+    blocks = 0;
+    np = 0;
+    return 0;
+  };
+  for (int j = 0; j < ntensors; ++j) {
+    auto& L = per[j];
+    const int nt = (int)L.size();
+    RGAN_REQUIRE(nt <= AP_MAXP);
+    if (b.cnt == AP_MAXT || np + nt > AP_MAXP) {
+      const int rc = flush();
+      if (rc) return rc;
+    }
+    AdamPackTensor X{params[j], grads[j], exp_avg[j], exp_avg_sq[j], numel[j], 0, 0, np, nt};
+    bool brick = nt > 0 && ((((uintptr_t)params[j] | (uintptr_t)grads[j] | (uintptr_t)exp_avg[j] |
+                               (uintptr_t)exp_avg_sq[j]) & 15) == 0);
+    for (const auto& t : L) {
+      brick = brick && t.kind == APK_TILED && t.KK == 16 && t.A == L[0].A && t.B == L[0].B && t.A % 32 == 0 &&
+              t.B % 32 == 0 && aligned16(t.out);
+      b.pk[np++] = t;
+    }
+    X.brick = brick;
+    X.bricks_b = brick ? L[0].B / 32 : 0;
+    const long long nb = brick ? (long long)(L[0].A / 32) * (L[0].B / 32) : (numel[j] + AP_FLAT - 1) / AP_FLAT;
+    b.t[b.cnt] = X;
+    b.first[b.cnt] = (int)blocks;
+    blocks += nb;
+    RGAN_REQUIRE(blocks < (1LL << 30));
+    ++b.cnt;
+  }
+  int rc = flush();
+  if (rc) return rc;
+  for (size_t i = 0; i < later.size(); ++i) {  // layouts the kernel does not write: repack
+    launch_pack_plan(later[i], later_out[i], s);
+    RGAN_CHECK_LAUNCH();
+  }
   return 0;
 }
 

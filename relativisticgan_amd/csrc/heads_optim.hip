@@ -809,20 +809,10 @@ struct AdamBatch {
 };
 
 __global__ void adam_step_inc(float* step) { step[0] += 1.f; }
-
-struct AdamConst {
-  float neg_step, bc2s, w, fb2, f1mb2, feps, fwd;
-  bool has_wd;
-};
-
-__device__ __forceinline__ void adam_elem(const AdamConst& k, float g, float& p, float& m, float& v) {
-  if (k.has_wd) g = g + k.fwd * p;
-  const float diff = g - m;
-  m = k.w < 0.5f ? m + k.w * diff : g - diff * (1.f - k.w);
-  v = v * k.fb2;
-  v = v + k.f1mb2 * g * g;
-  const float denom = sqrtf(v) / k.bc2s + k.feps;
-  p = p + k.neg_step * (m / denom);
+extern "C" int rgan_adam_step_inc(float* step, void* stream) {  // (rgan_adam_packed, conv_gemm.hip)
+  adam_step_inc<<<1, 1, 0, (hipStream_t)stream>>>(step);
+  RGAN_CHECK_LAUNCH();
+  return 0;
 }
 
 __global__ __launch_bounds__(256) void adam_kernel(AdamBatch b, const double* __restrict__ hyper,
@@ -830,18 +820,7 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamBatch b, const double* __
   int j = 0;
   while (j + 1 < b.cnt && (int)blockIdx.x >= b.first[j + 1]) ++j;
   const AdamTensor T = b.t[j];
-  const double lr = hyper[0], b1 = hyper[1], b2 = hyper[2], eps = hyper[3], wd = hyper[4];
-  const double st = (double)step[0];
-  const double bc1 = 1.0 - pow(b1, st), bc2 = 1.0 - pow(b2, st);
-  AdamConst k;
-  k.neg_step = (float)(-(lr / bc1));
-  k.bc2s = (float)sqrt(bc2);
-  k.w = (float)(1.0 - b1);
-  k.fb2 = (float)b2;
-  k.f1mb2 = (float)(1.0 - b2);
-  k.feps = (float)eps;
-  k.fwd = (float)wd;
-  k.has_wd = wd != 0.0;
+  const AdamConst k = adam_const(hyper, step);
   const long long e0 = (long long)((int)blockIdx.x - b.first[j]) * ADAM_BLOCK_ELEMS;
   const long long e1 = min(T.n, e0 + ADAM_BLOCK_ELEMS);
   const bool vec = (T.n & 3) == 0 && ((((uintptr_t)T.p | (uintptr_t)T.g | (uintptr_t)T.m | (uintptr_t)T.v) & 15) == 0);

@@ -30,6 +30,7 @@ class _State:
     world = 1
     rank = 0
     sync_bn = False
+    slots = {}         # id(parameter) -> (GradReducer, bucket, offset): gradient-bucket storage
 
 
 _S = _State()
@@ -73,6 +74,25 @@ def group():
 
 def sync_bn():
     return _S.world > 1 and _S.sync_bn
+
+
+def grad_view(w):
+    """The slice of ``w``'s gradient bucket shaped like ``w`` -- for a layer to write w's
+    gradient into when w has none yet this step (autograd then adopts the returned tensor
+    as ``w.grad`` without copying: a fresh view has no other reference), or None (one
+    process, w not bucketed, or a gradient already accumulating)."""
+    if _S.world == 1 or w.grad is not None:
+        return None
+    slot = _S.slots.get(id(w))
+    if slot is None or slot[0].params_by_id.get(id(w)) is not w:
+        return None
+    red, bi, off = slot
+    # once per step: two calls of one net in one backward (D(x), D(fake)) both see
+    # w.grad None until autograd sums their gradients -- the second must not reuse the slice
+    if id(w) in red.handed:
+        return None
+    red.handed.add(id(w))
+    return red.region(bi, off, w)
 
 
 def all_reduce_sum(t):
@@ -130,6 +150,11 @@ class GradReducer:
     whose gradient came only from an earlier backward of the same step), waits, and
     points each ``.grad`` at its slice of the reduced flat buffer (no copy back).
 
+    Gradient-as-bucket-view: each bucket is one persistent flat buffer, and the fused conv
+    layers write their weight gradients straight into their slices (``grad_view``), so a
+    bucket is all-reduced in place; only gradients produced elsewhere (BatchNorm affine,
+    biases, spectral weights -- small, or rare) are copied into their slices at launch.
+
     Arm only around the LAST backward of an optimizer step: the loop's heads 1-4 run two
     backwards (GLI:596-624) and WGAN-GP a third (GLI:658); gradients accumulated by the
     earlier ones are already in ``.grad`` when the last one's hooks fire."""
@@ -145,10 +170,19 @@ class GradReducer:
                 cur, size = [], 0
         if cur:
             self.buckets.append(cur)
-        self.where = {}
+        self.where, self.offset, self.params_by_id = {}, {}, {}
+        self.sizes = []
         for bi, b in enumerate(self.buckets):
+            off = 0
             for q in b:
                 self.where[id(q)] = bi
+                self.offset[id(q)] = off
+                self.params_by_id[id(q)] = q
+                _S.slots[id(q)] = (self, bi, off)
+                off += q.numel()
+            self.sizes.append(off)
+        self.flats = [None] * len(self.buckets)
+        self.handed = set()  # parameters whose slice a layer was given this step (grad_view)
         self.armed = False
         self.handles = [q.register_post_accumulate_grad_hook(self._hook) for q in self.params]
         self._reset()
@@ -173,13 +207,29 @@ class GradReducer:
             self._launch(self.next)
             self.next += 1
 
+    def _flat(self, bi):
+        f = self.flats[bi]
+        if f is None:
+            q0 = self.buckets[bi][0]
+            f = self.flats[bi] = torch.empty(self.sizes[bi], dtype=q0.dtype, device=q0.device)
+        return f
+
+    def region(self, bi, off, q):
+        return self._flat(bi)[off:off + q.numel()].view_as(q)
+
     def _launch(self, bi):
         qs = [q for q in self.buckets[bi] if q.grad is not None]
         if not qs:
             return
-        flat = torch.cat([q.grad.reshape(-1) for q in qs])
+        flat = self._flat(bi)
+        for q in self.buckets[bi]:
+            v = self.region(bi, self.offset[id(q)], q)
+            if q.grad is None:
+                v.zero_()              # no gradient this step: contributes nothing
+            elif q.grad.data_ptr() != v.data_ptr():
+                v.copy_(q.grad)        # produced outside the bucket (BN affine, bias, ...)
         work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=_S.grad_group, async_op=True)
-        self.inflight.append((work, flat, qs))
+        self.inflight.append((work, bi, qs))
 
     def finish(self):
         """Complete every bucket's all-reduce; afterwards .grad holds the global SUM."""
@@ -190,20 +240,21 @@ class GradReducer:
         while self.next < len(self.buckets):
             self._launch(self.next)
             self.next += 1
-        for work, flat, qs in self.inflight:
+        for work, bi, qs in self.inflight:
             work.wait()
-            off = 0
             for q in qs:
-                n = q.numel()
-                q.grad = flat[off:off + n].view_as(q)
-                off += n
+                q.grad = self.region(bi, self.offset[id(q)], q)
         self.inflight = []
+        self.handed = set()
         self.armed = False
 
     def remove(self):
         for h in self.handles:
             h.remove()
         self.handles = []
+        for q in self.params:
+            if _S.slots.get(id(q), (None,))[0] is self:
+                del _S.slots[id(q)]
 
 
 def allreduce_grads(params, bucket_bytes=64 << 20):

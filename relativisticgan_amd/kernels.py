@@ -136,6 +136,27 @@ class _PackCache:
         for key, ent, w in todo:
             self.entries[key] = (ent[0], w._version, ent[2], w.data_ptr()) + ent[4:]
 
+    def layouts_of(self, params):
+        """[(param index, key, entry)] of every cached layout of ``params`` (for
+        rgan_adam_packed, which rewrites them with the new values)."""
+        idx = {id(p): i for i, p in enumerate(params)}
+        out = []
+        for key, ent in self.entries.items():
+            base, w = ent[0](), ent[6]()
+            if base is None or w is None or id(base) not in idx or w.data_ptr() != params[idx[id(base)]].data_ptr():
+                continue
+            if w.numel() != params[idx[id(base)]].numel():
+                continue
+            out.append((idx[id(base)], key, ent))
+        return out
+
+    def mark_current(self, layouts):
+        """The listed layouts were rewritten from their weights' current values."""
+        for _, key, ent in layouts:
+            w = ent[6]()
+            if w is not None and self.entries.get(key) is ent:
+                self.entries[key] = (ent[0], w._version, ent[2], w.data_ptr()) + ent[4:]
+
     def _drop(self, key):
         def cb(_ref):
             ent = self.entries.get(key)
@@ -218,11 +239,14 @@ def patch_weight(w, transposed):
 PATCHW = _FoldCache(patch_weight)
 
 
-def unpatch_grad(g1, O, C, row_stride, col_stride, out=None):
+def unpatch_grad(g1, O, C, row_stride, col_stride, out=None, into=None):
     """1x1-GEMM weight gradient -> torch layout [O][C][4][4] (dw[o][c][t] = g1[o*rs + (4t+c)*cs]);
-    ``out`` given: added into it (gradient accumulation)."""
+    ``out`` given: added into it (gradient accumulation); ``into``: written into it."""
     acc = out is not None
-    dw = out if acc else torch.empty((O, C, 4, 4), dtype=torch.float32, device=g1.device)
+    if into is not None and (acc or tuple(into.shape) != (O, C, 4, 4) or not into.is_contiguous()):
+        raise L.RganError("unpatch_grad: `into` must be a contiguous [O][C][4][4] tensor (no accumulation)")
+    dw = out if acc else (into if into is not None else torch.empty((O, C, 4, 4), dtype=torch.float32,
+                                                                    device=g1.device))
     L.check(L.lib().rgan_unpatch_grad(L.ptr(g1), O, C, row_stride, col_stride, L.ptr(dw), int(acc), L.stream()),
             "rgan_unpatch_grad")
     return dw
@@ -358,11 +382,18 @@ def conv_dgrad(dy, w, geom, x_shape, wscale=None, out=None, like=None, cache=Fal
     return out
 
 
-def conv_wgrad(x, dy, geom, w_shape, with_bias=False, out=None, out_bias=None):
+def conv_wgrad(x, dy, geom, w_shape, with_bias=False, out=None, out_bias=None, into=None):
     """(dw in torch layout, dbias or None).  ``out`` / ``out_bias`` given: the gradients are
-    ADDED into them in the GEMM epilogue (autograd accumulation without an add pass)."""
+    ADDED into them in the GEMM epilogue (autograd accumulation without an add pass);
+    ``into``: dw is WRITTEN into that tensor (e.g. its slice of a data-parallel gradient
+    bucket, dp.grad_view) instead of a new one."""
     L.require_cuda(x, dy)
     _f32(x, dy)
+    if into is not None:
+        if out is not None or geom.upsample != 1:
+            raise L.RganError("conv_wgrad: `into` excludes accumulation and NN_conv")
+        if tuple(into.shape) != tuple(w_shape) or not into.is_contiguous():
+            raise L.RganError("conv_wgrad: `into` must be a contiguous tensor of the weight's shape")
     if geom.upsample != 1:
         _nn_check(geom)
         if out is not None:
@@ -373,7 +404,7 @@ def conv_wgrad(x, dy, geom, w_shape, with_bias=False, out=None, out_bias=None):
     acc = out is not None
     if acc and (tuple(out.shape) != tuple(w_shape) or not out.is_contiguous()):
         raise L.RganError("conv_wgrad: out must be a contiguous tensor of the weight's shape")
-    dw = out if acc else torch.empty(w_shape, dtype=torch.float32, device=x.device)
+    dw = out if acc else (into if into is not None else torch.empty(w_shape, dtype=torch.float32, device=x.device))
     db = None
     if with_bias:
         if acc != (out_bias is not None):
@@ -811,6 +842,26 @@ def adam(params, grads, exp_avgs, exp_avg_sqs, hyper, step):
     L.check(L.lib().rgan_adam(n, ctypes.cast(P, ctypes.c_void_p), ctypes.cast(G, ctypes.c_void_p),
                               ctypes.cast(M, ctypes.c_void_p), ctypes.cast(V, ctypes.c_void_p),
                               ctypes.cast(N, ctypes.c_void_p), L.ptr(hyper), L.ptr(step), L.stream()), "rgan_adam")
+
+
+def adam_packed(params, grads, exp_avgs, exp_avg_sqs, hyper, step, layouts):
+    """``adam`` that also writes the cached GEMM layouts ``layouts`` ([(param index, key,
+    pack-cache entry)], _PackCache.layouts_of) from the updated values (rgan_adam_packed)."""
+    n = len(params)
+    arr = ctypes.c_void_p * max(n, 1)
+    P = arr(*[p.data_ptr() for p in params])
+    G = arr(*[g.data_ptr() for g in grads])
+    M = arr(*[m.data_ptr() for m in exp_avgs])
+    V = arr(*[v.data_ptr() for v in exp_avg_sqs])
+    N = (ctypes.c_longlong * max(n, 1))(*[p.numel() for p in params])
+    k = len(layouts)
+    packs = (L.RganAdamPack * max(k, 1))()
+    for i, (j, _key, ent) in enumerate(layouts):
+        packs[i] = L.RganAdamPack(j, ent[5], ctypes.pointer(ent[4]), ent[2].data_ptr())
+    L.check(L.lib().rgan_adam_packed(n, ctypes.cast(P, ctypes.c_void_p), ctypes.cast(G, ctypes.c_void_p),
+                                     ctypes.cast(M, ctypes.c_void_p), ctypes.cast(V, ctypes.c_void_p),
+                                     ctypes.cast(N, ctypes.c_void_p), L.ptr(hyper), L.ptr(step), k,
+                                     ctypes.cast(packs, ctypes.c_void_p), L.stream()), "rgan_adam_packed")
 
 
 def lr_decay(hyper, gamma):

@@ -5,8 +5,9 @@ uses it: the same param_groups and per-parameter state layout
 (``state[p] = {step, exp_avg, exp_avg_sq}``), so ``state_dict()`` / ``load_state_dict()``
 and ``torch.optim.lr_scheduler.ExponentialLR`` (GLI:533-534, 713-714) work unchanged.
 One launch updates every tensor of a param group (multi-tensor, a size-proportional
-grid of 4096-element blocks, float4 loads, 28 B/element of HBM traffic); the cached GEMM
-layouts of the updated weights are then repacked in one batched launch.  Hyper-parameters live in a
+grid of 4096-element blocks or 32 x 32 x 16 weight bricks, float4 loads, 28 B/element of
+HBM traffic) and writes the cached GEMM layouts of the updated weights from the values it
+holds (rgan_adam_packed: +4 B/element per layout, no repack pass re-reading the weights).  Hyper-parameters live in a
 device buffer (doubles, as torch keeps them in Python floats), refreshed only when a
 group's values change; the step counter is a device scalar incremented by the kernel.
 """
@@ -83,11 +84,13 @@ class Adam(torch.optim.Optimizer):
             if len(steps) != 1:
                 raise RuntimeError(f"Adam: parameters of group {gi} are at different steps {sorted(steps)}; "
                                    "the fused kernel keeps one step count per group")
-            K.adam(ps, gs, ms, vs, hyper, step)
+            # the kernel also rewrites every cached GEMM layout of these weights from the new values
+            layouts = K.PACKS.layouts_of(ps)
+            K.adam_packed(ps, gs, ms, vs, hyper, step, layouts)
             for p in ps:
                 self.state[p]["step"] += 1  # host mirror of state['step'] (torch Adam's state_dict layout)
-                increment_version(p)        # the kernel wrote p: invalidate cached packed layouts
-            K.PACKS.refresh(ps)  # ... and repack the ones in use, in one batched launch
+                increment_version(p)        # the kernel wrote p: layouts not listed above are stale
+            K.PACKS.mark_current(layouts)
         return loss
 
     def load_state_dict(self, state_dict):

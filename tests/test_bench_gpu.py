@@ -39,6 +39,9 @@ def test_bench_one_gpu_line():
     assert d["config"]["parallelism"] == "dp1" and d["config"]["global_batch"] == 32
     rf = d["roofline"]
     assert rf["bound"] == "mfma" and 0 < rf["frac"] < 1 and rf["peak"] == 157.3
+    # the N > 1 launch mode on one GPU (the scaling runs' like-for-like baseline)
+    dpp = d["dp_path_n1"]["C1"]
+    assert dpp["value"] > 0 and dpp["batched_D_step"] is False and dpp["hip_graph"] is False
 
 
 def test_bench_two_rank_rehearsal():

@@ -266,3 +266,92 @@ def test_n_gpu_without_processes_fails_loudly():
     p = make_param(loss_D=7, image_size=32, batch_size=8, z_size=16, G_h_size=8, D_h_size=8, seed=1, n_gpu=2)
     with pytest.raises(ValueError, match="n_gpu"):
         Trainer(p, synthetic_images(16, 32, device="cpu"), device="cpu")
+
+
+class _WgradLike(torch.autograd.Function):
+    """y = x * w; backward writes dL/dw the way the fused conv layers do under data
+    parallelism: into w's gradient-bucket slice when dp.grad_view hands one out."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x * w
+
+    @staticmethod
+    def backward(ctx, g):
+        from relativisticgan_amd import dp
+        x, w = ctx.saved_tensors
+        dw = (g * x).sum(0)
+        into = dp.grad_view(w)
+        if into is not None:
+            into.copy_(dw)
+            dw = into
+        return g * w, dw
+
+
+def _bucket_view_worker(rank, world, port, q):
+    try:
+        dp = _init(rank, world, port)
+        g = torch.Generator().manual_seed(7)
+        w1 = torch.nn.Parameter(torch.randn(5, generator=g))
+        w2 = torch.nn.Parameter(torch.randn(3, generator=g))
+        bn = torch.nn.Parameter(torch.randn(4, generator=g))   # gradient produced outside the bucket
+        red = dp.GradReducer([w1, w2, bn], bucket_bytes=1 << 20)
+        assert len(red.buckets) == 1
+
+        def losses(rk):
+            gx = torch.Generator().manual_seed(50 + rk)
+            xa, xb = torch.randn(6, 5, generator=gx), torch.randn(6, 5, generator=gx)
+            # w1 used twice in ONE backward (as D(x), D(fake)): one slice, summed correctly
+            ya, yb = _WgradLike.apply(xa, w1), _WgradLike.apply(xb, w1)
+            y2 = _WgradLike.apply(torch.randn(2, 3, generator=gx), w2)
+            return ya.pow(2).mean() + yb.sin().mean() + y2.sum() + (bn * (rk + 1)).pow(2).sum()
+
+        want = [torch.zeros_like(t) for t in (w1, w2, bn)]
+        for rk in range(world):
+            ref = [t.detach().clone().requires_grad_(True) for t in (w1, w2, bn)]
+            gx = torch.Generator().manual_seed(50 + rk)
+            xa, xb = torch.randn(6, 5, generator=gx), torch.randn(6, 5, generator=gx)
+            x2 = torch.randn(2, 3, generator=gx)
+            lref = (xa * ref[0]).pow(2).mean() + (xb * ref[0]).sin().mean() + (x2 * ref[1]).sum() + \
+                (ref[2] * (rk + 1)).pow(2).sum()
+            for w_, g_ in zip(want, torch.autograd.grad(lref, ref)):
+                w_ += g_
+        for step in range(2):
+            for t in (w1, w2, bn):
+                t.grad = None
+            red.arm()
+            losses(rank).backward()
+            # the layer-written gradients are the bucket's own storage (no copy)
+            flat = red.flats[0]
+            assert w2.grad.data_ptr() == flat[red.offset[id(w2)]:].data_ptr()
+            red.finish()
+            for t, w_ in zip((w1, w2, bn), want):
+                assert torch.allclose(t.grad, w_, atol=1e-5), (step, t.shape)
+                assert flat.data_ptr() <= t.grad.data_ptr() < flat.data_ptr() + 4 * flat.numel()
+        assert dp.grad_view(w1) is None  # has a gradient now
+        q.put((rank, "ok"))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_gradient_bucket_views_gloo_world2():
+    """Gradient-as-bucket-view: layers write weight gradients into their bucket slices
+    (dp.grad_view), autograd adopts them as .grad, the bucket is all-reduced in place
+    (gradients produced elsewhere are copied in), a weight used by two calls in one
+    backward gets its slice once, and the result is the global SUM."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bucket_view_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(120)
+    res = [q.get() for _ in range(world)]
+    assert all(msg == "ok" for _, msg in res), res

@@ -749,6 +749,78 @@ def test_pack_batch_refresh(K):
     assert checked >= 17
 
 
+def test_adam_writes_packed_layouts(K):
+    """optim.Adam (rgan_adam_packed) rewrites every cached GEMM layout of the weights it
+    steps from the new values: p / exp_avg / exp_avg_sq bitwise equal to the plain multi-
+    tensor Adam (rgan_adam), every layout bitwise equal to a fresh rgan_conv_pack of the
+    updated weight -- brick path (4x4 tiled, both directions: Conv2d fwd + its 4-phase dgrad,
+    ConvTranspose2d), per-element scatters (a 3x3 tiled layout, the t2d layout of G's 1x1 ->
+    4x4 first layer, the narrow ConvT layouts of both image layers), BN vectors without
+    layouts -- and the cache then serves them without repacking."""
+    import ctypes
+    from relativisticgan_amd import _lib as L
+    from relativisticgan_amd.optim import Adam
+    torch.manual_seed(21)
+    g4, gt, g3, g41 = K.ConvGeom(4, 2, 1, False), K.ConvGeom(4, 2, 1, True), K.ConvGeom(3, 1, 1, False), \
+        K.ConvGeom(4, 1, 0, True)
+    conv = torch.nn.Parameter(torch.randn(256, 128, 4, 4, device=DEV) * 0.05)   # D middle: fwd + dgrad
+    convt = torch.nn.Parameter(torch.randn(128, 64, 4, 4, device=DEV) * 0.05)   # G middle: fwd + dgrad
+    start = torch.nn.Parameter(torch.randn(32, 512, 4, 4, device=DEV) * 0.05)   # G 1x1 -> 4x4 (t2d)
+    g_end = torch.nn.Parameter(torch.randn(64, 3, 4, 4, device=DEV) * 0.05)     # G image ConvT (narrow)
+    d_img = torch.nn.Parameter(torch.randn(64, 3, 4, 4, device=DEV) * 0.05)     # D image conv (narrow dgrad)
+    c3 = torch.nn.Parameter(torch.randn(24, 20, 3, 3, device=DEV) * 0.05)       # 3x3 (arch 1)
+    gamma = torch.nn.Parameter(torch.randn(256, device=DEV))
+    beta = torch.nn.Parameter(torch.randn(256, device=DEV))
+    x = _nhwc(torch.randn(2, 128, 16, 16, device=DEV))
+    y = K.conv_fwd(x, conv, g4, cache=True)
+    K.conv_dgrad(y, conv, g4, x.shape, like=x, cache=True)
+    xt = _nhwc(torch.randn(2, 128, 8, 8, device=DEV))
+    yt = K.conv_fwd(xt, convt, gt, cache=True)
+    K.conv_dgrad(yt, convt, gt, xt.shape, like=xt, cache=True)
+    K.conv_fwd(_nhwc(torch.randn(4, 32, 1, 1, device=DEV)), start, g41, cache=True)
+    K.conv_fwd(_nhwc(torch.randn(2, 64, 16, 16, device=DEV)), g_end, gt, cache=True)
+    img = torch.randn(2, 3, 32, 32, device=DEV)
+    K.conv_dgrad(_nhwc(torch.randn(2, 64, 16, 16, device=DEV)), d_img, g4, img.shape, like=img, cache=True)
+    K.conv_fwd(_nhwc(torch.randn(2, 20, 8, 8, device=DEV)), c3, g3, cache=True)
+    params = [conv, convt, start, g_end, d_img, c3, gamma, beta]
+    for p in params:
+        p.grad = torch.randn_like(p) * 1e-3
+    twins = [torch.nn.Parameter(p.detach().clone()) for p in params]
+    for p, q in zip(params, twins):
+        q.grad = p.grad.clone()
+    before = len(K.PACKS.layouts_of(params))
+    assert before >= 9
+    opt, ref = Adam(params, lr=1e-3, betas=(0.5, 0.999)), Adam(twins, lr=1e-3, betas=(0.5, 0.999))
+    for step in range(2):
+        opt.step()
+        # the reference: the plain multi-tensor kernel on the twins
+        hyper, _, dstep = ref._group_dev(0, ref.param_groups[0], DEV, ref.state.get(twins[0]) or None)
+        for q in twins:
+            st = ref.state[q]
+            if not st:
+                st["step"] = torch.tensor(0.0)
+                st["exp_avg"] = torch.zeros_like(q)
+                st["exp_avg_sq"] = torch.zeros_like(q)
+        K.adam(twins, [q.grad for q in twins], [ref.state[q]["exp_avg"] for q in twins],
+               [ref.state[q]["exp_avg_sq"] for q in twins], hyper, dstep)
+        for q in twins:
+            ref.state[q]["step"] += 1
+        torch.cuda.synchronize()
+        for p, q in zip(params, twins):
+            assert torch.equal(p.detach(), q.detach())
+            assert torch.equal(opt.state[p]["exp_avg"], ref.state[q]["exp_avg"])
+            assert torch.equal(opt.state[p]["exp_avg_sq"], ref.state[q]["exp_avg_sq"])
+        lay = K.PACKS.layouts_of(params)
+        assert len(lay) == before
+        for _, _, ent in lay:
+            w = ent[6]()
+            assert ent[1] == w._version  # current: the next conv reuses it
+            fresh = torch.empty_like(ent[2])
+            L.check(L.lib().rgan_conv_pack(ctypes.byref(ent[4]), ent[5], L.ptr(w), L.ptr(fresh), L.stream()), "pack")
+            torch.cuda.synchronize()
+            assert torch.equal(fresh, ent[2]), (tuple(w.shape), ent[5])
+
+
 def test_device_rng(K):
     """--rgan_rng device draws: N(0,1) / U[0,1) moments, distinct in-range batch indices, the
     device counter advancing (fresh draws per call, the same sequence for the same seed --
