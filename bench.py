@@ -202,7 +202,21 @@ def _run_workload(name, steps, warmup, world, args, K, dp_path=False):
     t = Trainer(p, images)
     flops_iter = conv_flops_per_iteration(t)
 
-    use_graph = not dp_path and (args.graph == "on" or (args.graph == "auto" and world == 1))
+    # launch mode: "graph" = one iteration captured as a HIP graph (one process);
+    # "piecewise" = the iteration captured as HIP graphs cut at its collectives, which run
+    # eagerly between the replays (dp.PiecewiseGraph); "eager".  auto: graph for one
+    # process; under DP piecewise for small (launch-bound) models, eager for large ones,
+    # whose gradient buckets all-reduce overlapped with the backward (a captured backward
+    # cannot launch them mid-way)
+    n_params = sum(q.numel() for q in list(t.G.parameters()) + list(t.D.parameters()))
+    multi = world > 1 or dp_path
+    if args.graph == "auto":
+        mode = ("piecewise" if n_params < 50e6 else "eager") if multi else "graph"
+    elif args.graph == "on":
+        mode = "piecewise" if multi else "graph"
+    else:
+        mode = args.graph if args.graph == "piecewise" else "eager"
+    use_graph = mode in ("graph", "piecewise")
     # graph mode runs every iteration on one side stream: autograd's per-parameter
     # AccumulateGrad nodes keep the stream of the first backward, and the captured backward
     # must accumulate on the capturing stream
@@ -225,10 +239,16 @@ def _run_workload(name, steps, warmup, world, args, K, dp_path=False):
         # state updates (Adam's device step counter, the device RNG's philox offsets), without
         # the ~10-20 us of Python + ctypes per launch that leaves a small model's step
         # launch-bound.
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=side):
-            t.iteration(it)
+        if mode == "piecewise":
+            from relativisticgan_amd import dp as _dp
+            t.defer_G = False
+            graph = _dp.PiecewiseGraph(side).capture(lambda: t.iteration(it))
+        else:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=side):
+                t.iteration(it)
         it += 1
+        graph_segments = getattr(graph, "n_segments", 1)
         graph.replay()  # one untimed replay
         barrier()
         t0 = time.perf_counter()
@@ -250,6 +270,7 @@ def _run_workload(name, steps, warmup, world, args, K, dp_path=False):
         prof["steps"] = nprof
         del graph
     else:
+        graph_segments = 0
         barrier()
         K.profile_begin(capacity=400 * steps + 64)
         t0 = time.perf_counter()
@@ -265,7 +286,8 @@ def _run_workload(name, steps, warmup, world, args, K, dp_path=False):
         torch.distributed.all_reduce(e, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(e.item())
     res = {"name": name, "loss_D": loss_D, "size": size, "bpg": bpg, "h": h, "spectral": spectral,
-           "arch": ARCH.get(name, 0), "batch_D": t.batch_D, "elapsed": elapsed, "steps": steps,
+           "arch": ARCH.get(name, 0), "batch_D": t.batch_D, "elapsed": elapsed, "steps": steps, "mode": mode,
+           "segments": graph_segments,
            "value": bpg * world * steps / elapsed, "ms_per_step": 1000.0 * elapsed / steps,
            "flops_iter": flops_iter, "prof": prof, "graph": use_graph}
     del t, images
@@ -313,8 +335,10 @@ def main():
     ap.add_argument("--batch-d", default="auto", choices=("auto", "on", "off"),
                     help="D(x), D(x_fake) as one batched pass (auto: on for 1 process, off under DP -- "
                          "'off' at N=1 is the like-for-like baseline of the N>1 runs)")
-    ap.add_argument("--graph", default="auto", choices=("auto", "on", "off"),
-                    help="time replays of one iteration captured as a HIP graph (auto: 1 process)")
+    ap.add_argument("--graph", default="auto", choices=("auto", "on", "off", "piecewise"),
+                    help="time replays of one iteration captured as a HIP graph (one process) or as graphs "
+                         "cut at the collectives (piecewise, DP); auto: graph at N=1, under DP piecewise "
+                         "below 50M parameters (launch-bound), else eager (bucket all-reduce overlapped)")
     ap.add_argument("--no-emu-extra", action="store_true",
                     help="skip the N=1 re-run of the workload with the bf16x6 fp32-emulated GEMMs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -360,7 +384,7 @@ def main():
             for name in [args.workload] + [w for w in ("C1",) if w in args.extra.split(",")]:
                 r = run_workload(name, args.steps, min(args.warmup, 5), world, args, K, dp_path=True)
                 dp_paths[name] = {"value": r["value"], "unit": "images/s", "ms_per_step": r["ms_per_step"],
-                                  "steps": r["steps"], "batched_D_step": r["batch_D"], "hip_graph": r["graph"]}
+                                  "steps": r["steps"], "batched_D_step": r["batch_D"], "launch_mode": r["mode"]}
     if rank != 0:
         torch.distributed.destroy_process_group()
         return
@@ -371,7 +395,8 @@ def main():
         "config": {"workload": describe(res), "loss_D": res["loss_D"], "image_size": res["size"],
                    "batch_per_gpu": res["bpg"], "global_batch": res["bpg"] * world, "G_h_size": res["h"],
                    "D_h_size": res["h"], "arch": res["arch"], "parallelism": f"dp{world}",
-                   "batched_D_step": res["batch_D"], "hip_graph": res["graph"],
+                   "batched_D_step": res["batch_D"], "hip_graph": res["graph"], "launch_mode": res["mode"],
+                   "graph_segments": res["segments"],
                    "batchnorm": "SyncBN" if args.sync_bn else "per-shard (reference DataParallel)"},
         "step_mfma_util": res["flops_iter"] * args.steps / res["elapsed"] / (world * FP32_MFMA_PEAK),
         "conv_tflop_per_step": res["flops_iter"] / 1e12,

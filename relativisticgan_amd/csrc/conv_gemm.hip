@@ -2167,7 +2167,10 @@ struct AdamPackTensor {
   long long n;
   int brick, bricks_b, pk0, npk;
 };
-constexpr int AP_MAXT = 24, AP_MAXP = 24, AP_BRICK = 32 * 32 * 16, AP_FLAT = 4096, AP_TLD = 32 * 17;
+// 1024 threads: a brick's 4096 float4 (or a flat block's 16384 elements) are one pass of 4
+// float4 loads per thread and array, all in flight together (two 68-KB blocks per CU)
+constexpr int AP_MAXT = 24, AP_MAXP = 24, AP_BRICK = 32 * 32 * 16, AP_FLAT = 16384, AP_TLD = 32 * 17 + 4,
+              AP_THREADS = 1024;
 struct AdamPackBatch {
   AdamPackTensor t[AP_MAXT];
   AdamPackT pk[AP_MAXP];
@@ -2204,9 +2207,9 @@ __device__ __forceinline__ void apk_scatter(const AdamPackT& t, long long e, flo
   }
 }
 
-__global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackBatch b, const double* __restrict__ hyper,
-                                                        const float* __restrict__ step) {
-  __shared__ float T[32 * AP_TLD];  // brick [a][b][tap] (tap stride 17: conflict-light column reads)
+__global__ __launch_bounds__(AP_THREADS) void adam_pack_kernel(AdamPackBatch b, const double* __restrict__ hyper,
+                                                               const float* __restrict__ step) {
+  __shared__ float T[32 * AP_TLD];  // brick [a][b][tap]: b stride 17, a stride 548 (4 consecutive a: distinct banks)
   int j = 0;
   while (j + 1 < b.cnt && (int)blockIdx.x >= b.first[j + 1]) ++j;
   const AdamPackTensor X = b.t[j];
@@ -2215,12 +2218,12 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackBatch b, const d
   if (X.brick) {
     const AdamPackT& t0 = b.pk[X.pk0];
     const int B = t0.B, a0 = 32 * (local / X.bricks_b), b0 = 32 * (local % X.bricks_b);
-    for (int pass = 0; pass < 4; ++pass) {  // 8 rows of 32 b x 16 taps (2 KB contiguous) per pass
+    {  // 32 rows of 32 b x 16 taps (2 KB contiguous each)
       float4 P[4], G[4], M[4], V[4];
       long long off[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int jj = tid + 256 * u, al = 8 * pass + (jj >> 7), f = jj & 127;
+        const int jj = tid + AP_THREADS * u, al = jj >> 7, f = jj & 127;
         off[u] = ((long long)(a0 + al) * B + b0) * 16 + 4 * f;
         P[u] = *reinterpret_cast<const float4*>(X.p + off[u]);
         G[u] = *reinterpret_cast<const float4*>(X.g + off[u]);
@@ -2236,7 +2239,7 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackBatch b, const d
         *reinterpret_cast<float4*>(X.m + off[u]) = M[u];
         *reinterpret_cast<float4*>(X.v + off[u]) = V[u];
         *reinterpret_cast<float4*>(X.p + off[u]) = P[u];
-        const int jj = tid + 256 * u, al = 8 * pass + (jj >> 7), f = jj & 127, bl = f >> 2, tq = f & 3;
+        const int jj = tid + AP_THREADS * u, al = jj >> 7, f = jj & 127, bl = f >> 2, tq = f & 3;
         float* d = T + al * AP_TLD + bl * 17 + 4 * tq;
         d[0] = P[u].x; d[1] = P[u].y; d[2] = P[u].z; d[3] = P[u].w;
       }
@@ -2244,9 +2247,9 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackBatch b, const d
     __syncthreads();
     for (int q = 0; q < X.npk; ++q) {
       const AdamPackT& t = b.pk[X.pk0 + q];
-#pragma unroll 4
-      for (int u = 0; u < 16; ++u) {  // 32 x 16 x 8 float4 of 4 consecutive in-indices
-        const int jj = tid + 256 * u, iq = jj & 7, tap = (jj >> 3) & 15, ol = jj >> 7;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // 32 x 16 x 8 float4 of 4 consecutive in-indices
+        const int jj = tid + AP_THREADS * u, iq = jj & 7, tap = (jj >> 3) & 15, ol = jj >> 7;
         float4 v4;
         long long dst;
         if (t.in_is_a) {  // in = a: T[4 iq + c][ol][tap]
@@ -2266,11 +2269,11 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackBatch b, const d
   const long long e0 = (long long)local * AP_FLAT, e1 = min(X.n, e0 + AP_FLAT);
   const bool vec = (X.n & 3) == 0 && ((((uintptr_t)X.p | (uintptr_t)X.g | (uintptr_t)X.m | (uintptr_t)X.v) & 15) == 0);
   if (vec) {
-    constexpr int U = AP_FLAT / 1024;
+    constexpr int U = AP_FLAT / (4 * AP_THREADS);
     float4 P[U], G[U], M[U], V[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long long i = e0 + 4 * (tid + 256 * u);
+      const long long i = e0 + 4 * (tid + AP_THREADS * u);
       if (i < e1) {
         P[u] = *reinterpret_cast<const float4*>(X.p + i);
         G[u] = *reinterpret_cast<const float4*>(X.g + i);
@@ -2280,7 +2283,7 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackBatch b, const d
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const long long i = e0 + 4 * (tid + 256 * u);
+      const long long i = e0 + 4 * (tid + AP_THREADS * u);
       if (i < e1) {
         adam_elem(k, G[u].x, P[u].x, M[u].x, V[u].x);
         adam_elem(k, G[u].y, P[u].y, M[u].y, V[u].y);
@@ -2299,7 +2302,7 @@ __global__ __launch_bounds__(256) void adam_pack_kernel(AdamPackBatch b, const d
       }
     }
   } else {
-    for (long long i = e0 + tid; i < e1; i += 256) {
+    for (long long i = e0 + tid; i < e1; i += AP_THREADS) {
       float p = X.p[i], m = X.m[i], v = X.v[i];
       adam_elem(k, X.g[i], p, m, v);
       X.m[i] = m;
@@ -3288,7 +3291,7 @@ extern "C" int rgan_adam_packed(int ntensors, float* const* params, const float*
   auto flush = [&]() -> int {
     if (b.cnt == 0) return 0;
     b.first[b.cnt] = (int)blocks;
-    if (blocks > 0) adam_pack_kernel<<<(unsigned)blocks, 256, 0, s>>>(b, hyper, step);
+    if (blocks > 0) adam_pack_kernel<<<(unsigned)blocks, AP_THREADS, 0, s>>>(b, hyper, step);
     RGAN_CHECK_LAUNCH();
     b = AdamPackBatch{};
     blocks = 0;

@@ -31,6 +31,7 @@ class _State:
     rank = 0
     sync_bn = False
     slots = {}         # id(parameter) -> (GradReducer, bucket, offset): gradient-bucket storage
+    capture = None     # the PiecewiseGraph being captured (collectives become cut points)
 
 
 _S = _State()
@@ -96,10 +97,86 @@ def grad_view(w):
 
 
 def all_reduce_sum(t):
-    """In-place SUM over ranks (no-op for world 1)."""
+    """In-place SUM over ranks (no-op for world 1).  While a PiecewiseGraph is being
+    captured the collective becomes a cut point: the graph segment so far ends, and at every
+    replay the all-reduce runs eagerly on ``t`` (a static address) before the next segment."""
     if _S.world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=_S.group)
+        if _S.capture is not None:
+            grp = _S.group
+            _S.capture.cut(lambda: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=grp))
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=_S.group)
     return t
+
+
+class PiecewiseGraph:
+    """One training iteration as HIP graphs cut at its collectives (the data-parallel step
+    cannot be one graph: RCCL / gloo collectives run between the replays instead).
+
+    ``capture(fn)`` runs ``fn`` once under stream capture; every ``all_reduce_sum`` and
+    ``GradReducer.finish`` inside it ends the current graph and records the collective as
+    an action.  ``replay()`` then replays segment, action, segment, ... on the capture
+    stream: the same kernels, static buffers and device-side state updates (Adam's step
+    counter, the device RNG's Philox offsets) as eager iterations, with the ~10-20 us of
+    Python + ctypes per launch gone from everything between the collectives.  All segments
+    share one memory pool and replay in capture order, so a tensor produced in one segment
+    and consumed in a later one keeps its address."""
+
+    def __init__(self, stream):
+        self.stream = stream
+        self.items = []
+        self.pool = None
+        self.cur = None
+
+    def _begin(self):
+        import torch
+        self.cur = torch.cuda.CUDAGraph()
+        self.cur.capture_begin(pool=self.pool)
+
+    def _end(self):
+        self.cur.capture_end()
+        if self.pool is None:
+            self.pool = self.cur.pool()
+        self.items.append(("graph", self.cur))
+        self.cur = None
+
+    def cut(self, action):
+        """End the current segment, record ``action`` (run at every replay), start the next."""
+        self._end()
+        self.items.append(("action", action))
+        self._begin()
+
+    def capture(self, fn):
+        import torch
+        torch.cuda.synchronize()
+        with torch.cuda.stream(self.stream):
+            _S.capture = self
+            try:
+                self._begin()
+                fn()
+                self._end()
+            finally:
+                _S.capture = None
+                if self.cur is not None:  # fn raised mid-segment
+                    try:
+                        self.cur.capture_end()
+                    except RuntimeError:
+                        pass
+                    self.cur = None
+        return self
+
+    @property
+    def n_segments(self):
+        return sum(1 for k, _ in self.items if k == "graph")
+
+    def replay(self):
+        import torch
+        with torch.cuda.stream(self.stream):
+            for kind, x in self.items:
+                if kind == "graph":
+                    x.replay()
+                else:
+                    x()
 
 
 def all_gather_cat(t):
@@ -194,7 +271,9 @@ class GradReducer:
         self.inflight = []
 
     def arm(self):
-        if _S.world > 1:
+        # under PiecewiseGraph capture the buckets are reduced at the cut finish() makes:
+        # hooks firing inside the captured backward cannot launch collectives
+        if _S.world > 1 and _S.capture is None:
             self._reset()
             self.armed = True
 
@@ -235,6 +314,9 @@ class GradReducer:
         """Complete every bucket's all-reduce; afterwards .grad holds the global SUM."""
         if _S.world == 1:
             return
+        if _S.capture is not None:
+            self._finish_captured()
+            return
         if not self.armed:  # no overlapped backward this step: reduce everything now
             self._reset()
         while self.next < len(self.buckets):
@@ -245,6 +327,40 @@ class GradReducer:
             for q in qs:
                 q.grad = self.region(bi, self.offset[id(q)], q)
         self.inflight = []
+        self.handed = set()
+        self.armed = False
+
+    def _finish_captured(self):
+        """PiecewiseGraph cut: .grad becomes the bucket slices now (the captured optimizer
+        step reads them); at every replay, gradients produced outside the buckets are copied
+        into their slices, then every bucket is all-reduced in place."""
+        copies, flats = [], []
+        for bi, b in enumerate(self.buckets):
+            has = [q for q in b if q.grad is not None]
+            if not has:
+                continue
+            flats.append(self._flat(bi))
+            for q in b:
+                v = self.region(bi, self.offset[id(q)], q)
+                if q.grad is None:
+                    copies.append((None, v))
+                elif q.grad.data_ptr() != v.data_ptr():
+                    copies.append((q.grad, v))   # (keeps the source alive: static address)
+            for q in has:
+                q.grad = self.region(bi, self.offset[id(q)], q)
+        grp = _S.grad_group
+
+        def action():
+            for src, v in copies:
+                if src is None:
+                    v.zero_()
+                else:
+                    v.copy_(src)
+            works = [dist.all_reduce(f, op=dist.ReduceOp.SUM, group=grp, async_op=True) for f in flats]
+            for w in works:
+                w.wait()
+
+        _S.capture.cut(action)
         self.handed = set()
         self.armed = False
 

@@ -83,6 +83,9 @@ class Trainer:
         self.redD = dp.GradReducer(self.D.parameters()) if self.world > 1 else None
         self.redG = dp.GradReducer(self.G.parameters()) if self.world > 1 else None
         self._pending_G, self._pending_decay_G = None, False
+        # under DP, G's optimizer step waits for the next use of G (flush) so its gradient
+        # all-reduce overlaps the next D forward; a PiecewiseGraph capture steps it in place
+        self.defer_G = True
         self.host_rng = getattr(p, "rgan_rng", "host") == "host"
         if not self.host_rng and self.device.type != "cuda":
             raise ValueError("--rgan_rng device draws in HIP kernels: it needs a CUDA (HIP) device, "
@@ -282,7 +285,7 @@ class Trainer:
             self._backward(errG)
             recG.update(y_pred_fake=y_pred_fake.detach(), errG=errG.detach())
             self._pending_G = (hooks, recG)
-            if self.redG is None:
+            if self.redG is None or not self.defer_G:
                 self._step_G()
         self.errG = errG
         self.last["G"] = recG

@@ -195,3 +195,62 @@ def _compare(name, dpres, single):
                 elif d.max() > 2 * 2 * p.lr_D * 1.01 or (d > 1e-6).double().mean() > 0.01:
                     errs.append(f"it{i} {net}.{k} max {d.max():.2e} frac {(d > 1e-6).double().mean():.2%}")
     assert not errs, "\n".join(errs[:20])
+
+
+def _piecewise_worker(rank, world, port, path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from relativisticgan_amd import dp
+        from relativisticgan_amd.train import Trainer
+        dp.setup(sync_bn=False)
+        out = {}
+        for mode in ("eager", "piecewise"):
+            p = param_for("ralsgan")
+            p.rgan_rng = "device"  # captured iterations draw on the device
+            t = Trainer(p, dataset_for("ralsgan").cuda())
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                t.iteration(1)
+                t.flush()
+                if mode == "eager":
+                    for i in (2, 3):
+                        t.iteration(i)
+                    t.flush()
+                else:
+                    t.defer_G = False
+                    g = dp.PiecewiseGraph(side).capture(lambda: t.iteration(2))
+                    assert g.n_segments >= 4  # 2 collectives per loss head x 2 steps + 2 gradient cuts
+                    g.replay()
+                    g.replay()
+            torch.cuda.synchronize()
+            out[mode] = {k: v.detach().cpu().clone() for k, v in list(t.G.state_dict().items()) +
+                         list(t.D.state_dict().items())}
+        bad = [k for k in out["eager"] if not torch.allclose(out["eager"][k].float(), out["piecewise"][k].float(),
+                                                              rtol=0, atol=1e-6)]
+        torch.save({"bad": bad, "n": len(out["eager"])}, path + f".{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp2_piecewise_graph_replays_equal_eager():
+    """dp.PiecewiseGraph (bench --graph piecewise): one data-parallel iteration captured as
+    HIP graphs cut at its collectives (loss-head all-reduces, gradient buckets), replayed
+    twice with the collectives run eagerly in between, leaves the same parameters and BN
+    buffers as two eager iterations (device RNG: the replays draw fresh numbers)."""
+    world = 2
+    port = _free_port()
+    path = tempfile.mktemp()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_piecewise_worker, args=(r, world, port, path)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    for pr in procs:
+        pr.join(300)
+        assert pr.exitcode == 0
+    for r in range(world):
+        res = torch.load(path + f".{r}", weights_only=True)
+        assert res["n"] > 10 and not res["bad"], res["bad"][:10]

@@ -789,7 +789,7 @@ def test_adam_writes_packed_layouts(K):
     for p, q in zip(params, twins):
         q.grad = p.grad.clone()
     before = len(K.PACKS.layouts_of(params))
-    assert before >= 9
+    assert before >= 7, before
     opt, ref = Adam(params, lr=1e-3, betas=(0.5, 0.999)), Adam(twins, lr=1e-3, betas=(0.5, 0.999))
     for step in range(2):
         opt.step()

@@ -131,16 +131,18 @@ def test_weight_hooks_fire_in_trainer_backward():
     from relativisticgan_amd.train import Trainer
     from oracle.reference_cpu import synthetic_images
     kw = dict(loss_D=7, image_size=32, batch_size=8, z_size=16, G_h_size=8, D_h_size=8, seed=1, print_every=1000)
-    plain = Trainer(make_param(**kw), synthetic_images(64, 32).cuda())
-    hooked = Trainer(make_param(**kw), synthetic_images(64, 32).cuda())
-    wd = hooked.D.main[0].weight
-    wg = hooked.G.main[0].weight
     fired = {"post": 0, "tensor": 0}
-    wd.register_post_accumulate_grad_hook(lambda p: fired.__setitem__("post", fired["post"] + 1))
-    wg.register_hook(lambda g: fired.__setitem__("tensor", fired["tensor"] + 1))
-    for t in (plain, hooked):
+    nets = []
+    for with_hooks in (False, True):  # each trainer re-seeds at construction: the same draws
+        t = Trainer(make_param(**kw), synthetic_images(64, 32).cuda())
+        if with_hooks:
+            t.D.main[0].weight.register_post_accumulate_grad_hook(
+                lambda p: fired.__setitem__("post", fired["post"] + 1))
+            t.G.main[0].weight.register_hook(lambda g: fired.__setitem__("tensor", fired["tensor"] + 1))
         t.iteration(0)
-    torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        nets.append(t)
+    plain, hooked = nets
     assert fired["post"] >= 1 and fired["tensor"] >= 1
     # the two accumulation paths round differently (one vs two roundings of grad + dw), and
     # Adam's first step is a sign step: parameters agree to 2 lr, buffers closely
