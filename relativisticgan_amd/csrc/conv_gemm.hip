@@ -2191,6 +2191,12 @@ __device__ __forceinline__ long long apk_tiled_dst(const AdamPackT& t, int a, in
   return ((long long)phase * t.Nout + o) * t.K + (long long)kt * t.Nin + i;
 }
 
+// brick path: destination of element (a, b, tap) of a TILED or T2D layout
+__device__ __forceinline__ long long apk_brick_dst(const AdamPackT& t, int a, int b, int tap) {
+  if (t.kind == APK_T2D) return ((long long)tap * t.B + b) * t.K + a;
+  return apk_tiled_dst(t, a, b, tap);
+}
+
 // element e (flat index of the [A][B][KK] weight) with its new value into one layout
 __device__ __forceinline__ void apk_scatter(const AdamPackT& t, long long e, float val) {
   const int tap = (int)(e % t.KK);
@@ -2255,11 +2261,11 @@ __global__ __launch_bounds__(AP_THREADS) void adam_pack_kernel(AdamPackBatch b, 
         if (t.in_is_a) {  // in = a: T[4 iq + c][ol][tap]
           const float* s = T + (4 * iq) * AP_TLD + ol * 17 + tap;
           v4 = make_float4(s[0], s[AP_TLD], s[2 * AP_TLD], s[3 * AP_TLD]);
-          dst = apk_tiled_dst(t, a0 + 4 * iq, b0 + ol, tap);
+          dst = apk_brick_dst(t, a0 + 4 * iq, b0 + ol, tap);
         } else {          // in = b: T[ol][4 iq + c][tap]
           const float* s = T + ol * AP_TLD + (4 * iq) * 17 + tap;
           v4 = make_float4(s[0], s[17], s[34], s[51]);
-          dst = apk_tiled_dst(t, a0 + ol, b0 + 4 * iq, tap);
+          dst = apk_brick_dst(t, a0 + ol, b0 + 4 * iq, tap);
         }
         *reinterpret_cast<float4*>(t.out + dst) = v4;
       }
@@ -3261,6 +3267,7 @@ extern "C" int rgan_adam_packed(int ntensors, float* const* params, const float*
       const int T = a.KH * a.KW, Cout = (int)a.fnco.d;
       ok = (long long)a.K * Cout * T == n;
       t.kind = APK_T2D; t.A = a.K; t.B = Cout; t.KK = T; t.K = a.K;
+      t.in_is_a = 1;  // k = ci = the weight's first index: runs of 4 consecutive ci
     } else {
       int gx, gy;
       const int kind = pack_kind(a, gx, gy);
@@ -3310,8 +3317,8 @@ extern "C" int rgan_adam_packed(int ntensors, float* const* params, const float*
     bool brick = nt > 0 && ((((uintptr_t)params[j] | (uintptr_t)grads[j] | (uintptr_t)exp_avg[j] |
                                (uintptr_t)exp_avg_sq[j]) & 15) == 0);
     for (const auto& t : L) {
-      brick = brick && t.kind == APK_TILED && t.KK == 16 && t.A == L[0].A && t.B == L[0].B && t.A % 32 == 0 &&
-              t.B % 32 == 0 && aligned16(t.out);
+      brick = brick && (t.kind == APK_TILED || t.kind == APK_T2D) && t.KK == 16 && t.A == L[0].A &&
+              t.B == L[0].B && t.A % 32 == 0 && t.B % 32 == 0 && aligned16(t.out);
       b.pk[np++] = t;
     }
     X.brick = brick;
