@@ -217,6 +217,10 @@ def _run_workload(name, steps, warmup, world, args, K, dp_path=False):
     else:
         mode = args.graph if args.graph == "piecewise" else "eager"
     use_graph = mode in ("graph", "piecewise")
+    if mode == "piecewise" and bd is None or (dp_path and mode == "piecewise"):
+        # nothing to overlap with a deferred G step inside graphs: D(x) and D(x_fake) run as
+        # one batched pass, as on one GPU
+        t.batch_D = t.pac == 1 and t.D.segmentable
     # graph mode runs every iteration on one side stream: autograd's per-parameter
     # AccumulateGrad nodes keep the stream of the first backward, and the captured backward
     # must accumulate on the capturing stream

@@ -41,7 +41,7 @@ def test_bench_one_gpu_line():
     assert rf["bound"] == "mfma" and 0 < rf["frac"] < 1 and rf["peak"] == 157.3
     # the N > 1 launch mode on one GPU (the scaling runs' like-for-like baseline)
     dpp = d["dp_path_n1"]["C1"]
-    assert dpp["value"] > 0 and dpp["batched_D_step"] is False and dpp["launch_mode"] == "piecewise"
+    assert dpp["value"] > 0 and dpp["batched_D_step"] is True and dpp["launch_mode"] == "piecewise"
 
 
 def test_bench_two_rank_rehearsal():
@@ -56,6 +56,6 @@ def test_bench_two_rank_rehearsal():
     assert KEYS <= set(d)
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 64
     # C1 (24M parameters) under DP: HIP graphs cut at the collectives
-    assert d["config"]["batched_D_step"] is False and d["config"]["launch_mode"] == "piecewise"
+    assert d["config"]["batched_D_step"] is True and d["config"]["launch_mode"] == "piecewise"
     assert d["config"]["graph_segments"] > 4
     assert "cpu_baseline" not in d and d["value"] > 0

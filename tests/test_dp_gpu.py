@@ -53,11 +53,12 @@ def _capture(t, store):
 N_ITER = {"ralsgan_pac2": 1}
 
 
-def _run(name, world, rank, n_iter=None, device="cuda:0"):
+def _run(name, world, rank, n_iter=None, device="cuda:0", batch_D=None):
     n_iter = n_iter or N_ITER.get(name, 2)
     from relativisticgan_amd.train import Trainer
     p = param_for(name)
     p.rgan_rng = "host"
+    p.rgan_batch_D = batch_D
     t = Trainer(p, dataset_for(name).to(device))
     out = []
     for i in range(n_iter):
@@ -70,7 +71,7 @@ def _run(name, world, rank, n_iter=None, device="cuda:0"):
     return out
 
 
-def _worker(rank, world, port, name, path, sync_bn=True, n_iter=None, backend="gloo"):
+def _worker(rank, world, port, name, path, sync_bn=True, n_iter=None, backend="gloo", batch_D=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dev = rank if backend == "nccl" else 0  # RCCL: one GPU per rank; gloo: both ranks on cuda:0
@@ -79,7 +80,7 @@ def _worker(rank, world, port, name, path, sync_bn=True, n_iter=None, backend="g
     from relativisticgan_amd import dp
     dp.setup(sync_bn=sync_bn)
     try:
-        res = _run(name, world, rank, n_iter, device=f"cuda:{dev}")
+        res = _run(name, world, rank, n_iter, device=f"cuda:{dev}", batch_D=batch_D)
         # gather the per-rank D outputs so rank 0 holds the global vectors
         for st in res:
             for k in ("y_pred", "y_pred_fake"):
@@ -98,11 +99,12 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-def _spawn(name, sync_bn=True, n_iter=None, backend="gloo"):
+def _spawn(name, sync_bn=True, n_iter=None, backend="gloo", batch_D=None):
     path = os.path.join(tempfile.mkdtemp(), "dp.pt")
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, path, sync_bn, n_iter, backend)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, path, sync_bn, n_iter, backend, batch_D))
+             for r in range(2)]
     for pr in procs:
         pr.start()
     for pr in procs:
@@ -115,6 +117,16 @@ def _spawn(name, sync_bn=True, n_iter=None, backend="gloo"):
 def test_dp2_matches_single_process(name):
     single = _run(name, 1, 0)
     dpres = _spawn(name)
+    _compare(name, dpres, single)
+
+
+@pytest.mark.parametrize("name", ["ralsgan", "sgan"])
+def test_dp2_batched_D_matches_single_process(name):
+    """--rgan_batch_D True under data parallelism (the piecewise-graph launch mode's
+    default): D(x) and D(x_fake) as one pass per rank, per-call BN statistics (SyncBN),
+    distributed heads on the halves == the single-process global-batch step."""
+    single = _run(name, 1, 0)
+    dpres = _spawn(name, batch_D=True)
     _compare(name, dpres, single)
 
 
@@ -210,6 +222,7 @@ def _piecewise_worker(rank, world, port, path):
         for mode in ("eager", "piecewise"):
             p = param_for("ralsgan")
             p.rgan_rng = "device"  # captured iterations draw on the device
+            p.rgan_batch_D = True  # as bench.py's piecewise mode runs it
             t = Trainer(p, dataset_for("ralsgan").cuda())
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
