@@ -125,7 +125,7 @@ def _force_activations(net, queue):
         def fwd(x):
             if not queue:
                 raise RuntimeError("forced activation masks exhausted")
-            m = queue.pop(0).to(x.device)
+            m = queue.pop(0).to(x.device).contiguous()  # GPU masks are NHWC-strided; keep x's layout
             if m.shape != x.shape:
                 raise RuntimeError(f"forced mask shape {tuple(m.shape)} vs {tuple(x.shape)}")
             if isinstance(mod, torch.nn.ReLU):
