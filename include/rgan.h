@@ -94,6 +94,41 @@ int rgan_conv_fwd_bn(const RganConv* d, const float* x, const float* w, const fl
 int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* w, const float* wpacked,
                     const float* wscale, float* dx, void* ws, size_t ws_bytes, void* stream);
 
+/* Post-op for the layer that PRODUCED a GEMM's output operand, applied where the output
+ * value is final (the GEMM epilogue or its split-K reduce) instead of a separate pass over
+ * it.  `x` has the output's element strides (same shape).
+ *   mode 1 (activation backward, aten's threshold/leaky_relu/tanh backward of GLI:345,370,
+ *          417 behind the conv's data gradient): out = v * act'(x), x = the producer's
+ *          activation output;
+ *   mode 2 (BatchNorm2d backward sums, the first half of aten native_batch_norm_backward,
+ *          GLI:341-345/366-370/433-437): out = g = v * act'(x * al + be), x = the producer's
+ *          BatchNorm input y, al = gamma * invstd, be = beta - mean * al from stats[k] of the
+ *          output row's batch segment k (nseg equal segments of every phase's rows), and
+ *          part[S][2][C] = (sum g, sum g (y - mean)) per 64-row segment in double, S =
+ *          rgan_conv_post_segments(...); finish with rgan_bn_backward_parts. */
+typedef struct RganPost {
+  int mode;                /* 1 or 2 */
+  int act;                 /* RGAN_ACT_* of the producer */
+  float alpha;
+  int nseg;                /* mode 2: batch segments with their own statistics (1 or 2) */
+  const float* x;          /* activation output (mode 1) / BatchNorm input y (mode 2) */
+  const float* stats;      /* mode 2: [nseg][2C] (mean, invstd) */
+  const float* gamma;      /* mode 2: nullable */
+  const float* beta;       /* mode 2: nullable */
+  double* part;            /* mode 2: [part_segments][2][C] */
+  long long part_segments;
+} RganPost;
+
+/* rgan_conv_fwd (which = 0, act none, no bias) or rgan_conv_dgrad (which = 1) with a
+ * producer post-op.  *fused (host int) = 1 when the post-op was applied (else `out` holds
+ * the plain result and the caller runs the separate pass).  rgan_conv_post_segments: S for
+ * mode 2 (0: this GEMM cannot emit the sums) and (nullable *phases) the phase-major blocks
+ * the S segments come in (4 for a k4 s2 p1 Conv2d data gradient, else 1). */
+long long rgan_conv_post_segments(const RganConv* d, int which, int mode, int nseg, int* phases);
+int rgan_conv_post(const RganConv* d, int which, const float* in, const float* w, const float* wpacked,
+                   const float* wscale, float* out, void* ws, size_t ws_bytes, const RganPost* post,
+                   int* fused, void* stream);
+
 /* dw = d conv / d w applied to dy (aten convolution_backward, grad_weight), written
  * in torch weight layout; dbias (nullable) = per-output-channel sum of dy.
  * accumulate != 0: dw += ..., dbias += ... (autograd's gradient accumulation into an
@@ -189,6 +224,14 @@ int rgan_bn_finalize(const double* moments, int nranks, int C, float eps, float 
 int rgan_bn_backward_segments(const float* da, const float* y, long long P, int C, int nseg, const float* stats,
                               const float* gamma, const float* beta, int act, float act_alpha, float* dy,
                               float* dgamma, float* dbeta, void* partial, void* stream);
+/* The rest of the BatchNorm backward after a GEMM's post-op wrote g = da * act' and the
+ * segment sums (rgan_conv_post mode 2): merge part[S][2][C] (phases phase-major blocks of
+ * S / phases segments, each split into nseg batch segments) into sums[nseg][2][C] (caller's
+ * scratch), then dy = al (g - sum_g / Pk - (y - mean) invstd^2 sum_gx / Pk) per batch segment,
+ * dgamma / dbeta = the segments' sum (nullable).  Dense NHWC g, y, dy. */
+int rgan_bn_backward_parts(const float* g, const float* y, long long P, int C, int nseg, const float* stats,
+                           const float* gamma, const float* beta, const double* part, long long S, int phases,
+                           float* dy, float* dgamma, float* dbeta, double* sums, void* stream);
 /* Backward through act(BN(y)): given da, produce dy, dgamma, dbeta. */
 int rgan_bn_backward(const float* da, long long dsp, long long dsc,
                      const float* y, long long P, int C, long long sp, long long sc,

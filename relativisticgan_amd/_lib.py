@@ -25,6 +25,11 @@ class RganConv(ctypes.Structure):
                 ("transposed", c_int), ("xs", c_ll * 4), ("ys", c_ll * 4)]
 
 
+class RganPost(ctypes.Structure):
+    _fields_ = [("mode", c_int), ("act", c_int), ("alpha", c_f), ("nseg", c_int), ("x", c_vp), ("stats", c_vp),
+                ("gamma", c_vp), ("beta", c_vp), ("part", c_vp), ("part_segments", c_ll)]
+
+
 class RganAdamPack(ctypes.Structure):
     _fields_ = [("tensor", c_int), ("which", c_int), ("d", ctypes.POINTER(RganConv)), ("packed", c_vp)]
 
@@ -52,6 +57,11 @@ _SIGS = {
     "rgan_bn_apply_segments": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_f, c_vp, c_vp]),
     "rgan_bn_segment_stats": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp]),
+    "rgan_conv_post_segments": (c_ll, [ctypes.POINTER(RganConv), c_int, c_int, c_int, ctypes.POINTER(c_int)]),
+    "rgan_conv_post": (c_int, [ctypes.POINTER(RganConv), c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz,
+                               ctypes.POINTER(RganPost), ctypes.POINTER(c_int), c_vp]),
+    "rgan_bn_backward_parts": (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_vp,
+                                       c_vp, c_vp, c_vp, c_vp]),
     "rgan_conv_dgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "rgan_conv_wgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_sz, c_vp]),
     "rgan_nn_fold_weight": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),

@@ -50,6 +50,35 @@ ACT_LAYERS = []    # per ACT_TRACE entry: the layer's index in the net's plan
 TRACE_NET = None
 TRACE_LAYER = -1
 _KINKED = ("relu", "lrelu", "selu")
+_POST_ACTS = ("relu", "lrelu", "tanh", "selu")  # act' from the output (act_grad_from_out)
+LINKS = True  # LayerLink hand-offs on (tools/ab_links.py measures them off in the same process)
+
+
+class LayerLink:
+    """Hand-off between two consecutive fused layers of one net call (nets._Net): the lower
+    layer's forward records how its backward starts -- its activation (``mode`` 1), or its
+    train-mode BatchNorm + activation (``mode`` 2) -- and the upper layer's backward applies
+    that in the epilogue of the GEMM that produces the lower layer's output gradient
+    (kernels.Post), leaving ``done`` = (gradient data_ptr, Post); the lower layer's backward
+    then starts from that gradient instead of running its own pass (act_bwd_kernel /
+    bn_bwd_partial).  Only within one chain: each layer output has this one consumer."""
+
+    __slots__ = ("mode", "act", "alpha", "x", "stats", "gamma", "beta", "segs", "done")
+
+    def __init__(self):
+        self.mode = 0
+        self.done = None
+
+    def post(self, rows, gsegs):
+        """The kernels.Post for the lower layer's leading ``rows`` (its ``gsegs`` of ``segs``
+        batch segments), or None."""
+        if self.mode == 1:
+            return K.Post(1, self.act, self.alpha, self.x[:rows])
+        if self.mode == 2:
+            st = self.stats if self.stats.dim() == 2 else self.stats.view(1, -1)
+            return K.Post(2, self.act, self.alpha, self.x[:rows], stats=st[:gsegs].contiguous(), gamma=self.gamma,
+                          beta=self.beta, nseg=gsegs)
+        return None
 
 
 class LayerSpec:
@@ -193,10 +222,16 @@ class ConvLayerFn(torch.autograd.Function):
     separate forward calls of the same net (D(x) and D(x_fake), GLI:580-605): one conv
     GEMM over all of them, BatchNorm statistics and running-stat updates per segment in
     segment order, one dgrad and one wgrad in the backward (the weight gradient of both
-    calls in a single K-doubled GEMM instead of two GEMMs and a gradient add)."""
+    calls in a single K-doubled GEMM instead of two GEMMs and a gradient add).
+    ``gsegs`` < ``segs``: only the leading ``gsegs`` segments carry an output gradient (the
+    G step's batched [D(G(z)); D(x)] pass, whose D(x) half the reference runs without a
+    graph, GLI:673-707): the backward runs over those rows only, and the input gradient's
+    rows of the later segments are left unwritten (nothing reads them: the layer below is
+    restricted the same way, and the net's input hands only the leading rows on)."""
 
     @staticmethod
-    def forward(ctx, x, w, bias, gamma, beta, spec, bufs, sn, segs=1, out=None):
+    def forward(ctx, x, w, bias, gamma, beta, spec, bufs, sn, segs=1, out=None, gsegs=None, link_in=None,
+                link_out=None):
         # bufs = (running_mean, running_var, num_batches_tracked, training)
         # sn   = (u, v, inv_sigma) clones for spectral layers, else None
         wscale = sn[2] if spec.spectral else None
@@ -244,6 +279,18 @@ class ConvLayerFn(torch.autograd.Function):
         ctx.stats_eval = stats_eval
         ctx.training = bufs[3] if bufs is not None else True
         ctx.segs = segs
+        ctx.gsegs = segs if gsegs is None else gsegs
+        ctx.link_in, ctx.link_out = link_in, link_out
+        if link_out is not None and LINKS:
+            # how this layer's backward starts, for the layer above to fuse (LayerLink)
+            link_out.done = None
+            link_out.mode = 0
+            if spec.bn and ctx.stats_eval is None and ctx.training and not dp.sync_bn() and K.is_nhwc(y):
+                link_out.mode, link_out.x, link_out.stats = 2, y, stats
+                link_out.gamma, link_out.beta, link_out.segs = gamma, beta, segs
+            elif not spec.bn and spec.act in _POST_ACTS and not spec.nchw_out and K.is_nhwc(a):
+                link_out.mode, link_out.x = 1, a
+            link_out.act, link_out.alpha = spec.act, spec.alpha
         return a
 
     @staticmethod
@@ -256,7 +303,34 @@ class ConvLayerFn(torch.autograd.Function):
         if torch.is_grad_enabled():
             if ctx.segs > 1:
                 raise NotImplementedError("double backward through a segmented (batched) layer call")
+            # the graph this builds reads the layer's activations: a later backward through the
+            # forward nodes sums its gradients with the chain's, so the chain's hand-offs
+            # (LayerLink: one consumer per output) are off for this call
+            for lk in (ctx.link_in, ctx.link_out):
+                if lk is not None:
+                    lk.mode, lk.done = 0, None
             return ConvLayerFn._create_graph_backward(ctx, da, x, w, bias, gamma, beta, sn)
+        dx_full = dx_out = None
+        Bg = x.shape[0]
+        if ctx.gsegs < ctx.segs:
+            # gradient rows of the leading segments only (NHWC / NCHW: a batch prefix)
+            Bg = x.shape[0] * ctx.gsegs // ctx.segs
+            da, x, t5 = da[:Bg], x[:Bg], t5[:Bg]
+            if stats is not None and stats.dim() == 2:
+                stats = stats[0] if ctx.gsegs == 1 else stats[:ctx.gsegs]
+            if nx:
+                dx_full = torch.empty_like(saved[0])
+                dx_out = dx_full[:Bg]
+        # this layer's output gradient may arrive with its first backward pass already applied
+        # by the layer above (LayerLink): g = da * act' (+ BN sums), or da * act'
+        done = ctx.link_out.done if ctx.link_out is not None else None
+        if done is not None:
+            ctx.link_out.done = None
+            if done[0] != da.data_ptr() or not done[1].fused:
+                done = None
+        # ... and this layer's data gradient may carry the layer below's first pass
+        # (the two layers ran in one chain call: same batch segments, same gradient rows)
+        post = ctx.link_in.post(Bg, ctx.gsegs) if nx and ctx.link_in is not None else None
         wscale = sn[2] if spec.spectral else None
         dgamma = dbeta = None
         if spec.bn:
@@ -265,7 +339,10 @@ class ConvLayerFn(torch.autograd.Function):
             if ctx.stats_eval is not None:
                 # the reference never calls .eval() (GLI:560-714): no training path reaches this
                 raise NotImplementedError("backward through eval-mode BatchNorm is not on the training path")
-            if stats.dim() == 2:  # segmented call: BN backward per segment, one dy
+            if done is not None and done[1].mode == 2:
+                # da is g = da * act' and the sums are in done[1].part (the layer above's GEMM)
+                dy, dgamma, dbeta = K.bn_backward_parts(da, y, stats, gamma, beta, done[1], ng, nbeta)
+            elif stats.dim() == 2:  # segmented call: BN backward per segment, one dy
                 dy, dgamma, dbeta = ConvLayerFn._seg_bn_backward(ctx, da, y, stats, gamma, beta, ng, nbeta)
             elif dp.sync_bn():
                 sums, da_c = K.bn_backward_sums(da, y, stats, gamma, beta, spec.act, spec.alpha)
@@ -282,14 +359,15 @@ class ConvLayerFn(torch.autograd.Function):
             else:
                 dy, dgamma, dbeta = K.bn_backward(da, y, stats, gamma, beta, spec.act, spec.alpha,
                                                   need_affine=ng or nbeta)
-        elif spec.act != "none":
+        elif spec.act != "none" and not (done is not None and done[1].mode == 1):
             dy = K.act_backward(da, t5, spec.act, spec.alpha)
         else:
             dy = da
         if ConvLayerFn._patch_conv(spec, x):
             # image-side Conv2d (D's first layer; the forward ran the direct narrow kernel):
             # the weight gradient is a 1x1 GEMM over the image's patch matrix
-            dx = K.conv_dgrad(dy, w, spec.geom, tuple(x.shape), wscale=wscale, like=x, cache=True) if nx else None
+            dx = (K.conv_dgrad(dy, w, spec.geom, tuple(x.shape), wscale=wscale, out=dx_out, like=x, cache=True,
+                               post=post) if nx else None)
             dw = db = None
             if nw or nb:
                 g1, db = K.conv_wgrad(K.patches_k4s2(x), dy, K.G1X1, (w.shape[0], 64, 1, 1),
@@ -300,14 +378,16 @@ class ConvLayerFn(torch.autograd.Function):
             # image-side ConvTranspose2d (G's last layer): both gradients are 1x1 GEMMs over
             # the patch matrix of the image gradient, on x's grid
             Xg = K.patches_k4s2(dy)
-            dx = K.conv_fwd(Xg, K.PATCHW.get(w, True), K.G1X1, wscale=wscale, cache=True) if nx else None
+            dx = (K.conv_fwd(Xg, K.PATCHW.get(w, True), K.G1X1, wscale=wscale, out=dx_out, cache=True, post=post)
+                  if nx else None)
             dw = db = None
             if nw:
                 g1, _ = K.conv_wgrad(Xg, x, K.G1X1, (w.shape[0], 64, 1, 1))
                 dw = K.unpatch_grad(g1, w.shape[0], w.shape[1], 64, 1,
                                     into=dp.grad_view(w) if not spec.spectral else None)
         else:
-            dx = K.conv_dgrad(dy, w, spec.geom, tuple(x.shape), wscale=wscale, like=x, cache=True) if nx else None
+            dx = (K.conv_dgrad(dy, w, spec.geom, tuple(x.shape), wscale=wscale, out=dx_out, like=x, cache=True,
+                               post=post) if nx else None)
             dw = db = None
             if nw and not nb and spec.geom.upsample == 1 and ConvLayerFn._own_grad(w, bias):
                 # The weight gradient goes straight into w.grad: set when it is empty (what
@@ -325,7 +405,9 @@ class ConvLayerFn(torch.autograd.Function):
                     g, _ = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), out=acc)
                 if acc is None:
                     w.grad = g
-                return dx, None, None, dgamma, dbeta, None, None, None, None, None
+                ConvLayerFn._hand_down(ctx, post, dx)
+                return ((dx if dx_full is None else dx_full), None, None, dgamma, dbeta, None, None, None, None, None,
+                        None, None, None)
             if nw or nb:
                 # data parallel: the weight gradient lands in its gradient bucket's slice
                 # (dp.grad_view), which autograd then adopts as .grad (no bucket copy)
@@ -338,7 +420,16 @@ class ConvLayerFn(torch.autograd.Function):
                 dw = K.spectral_backward(w, dw, u, v, inv_sigma, spec.geom.transposed)
             if not nw:
                 dw = None
-        return dx, dw, db, dgamma, dbeta, None, None, None, None, None
+        ConvLayerFn._hand_down(ctx, post, dx)
+        if dx_full is not None:
+            dx = dx_full
+        return dx, dw, db, dgamma, dbeta, None, None, None, None, None, None, None, None
+
+    @staticmethod
+    def _hand_down(ctx, post, dx):
+        """The layer below starts its backward from dx as the post-op left it (LayerLink)."""
+        if post is not None and post.fused and dx is not None:
+            ctx.link_in.done = (dx.data_ptr(), post)
 
     @staticmethod
     def _own_grad(w, bias):
@@ -409,7 +500,7 @@ class ConvLayerFn(torch.autograd.Function):
         spec = ctx.spec
         slots = [i for i, t in enumerate((x, w, bias, gamma, beta))
                  if t is not None and ctx.needs_input_grad[i]]
-        out = [None] * 10
+        out = [None] * 13
         if not slots:
             return tuple(out)
         src = (x, w, bias, gamma, beta)

@@ -63,6 +63,9 @@ def make_parser(script="GAN_losses_iter"):
     p.add_argument("--rgan_batch_D", type="bool", default=None,
                    help="run the D step's D(x) and D(x_fake) as one batched pass (per-call BN kept); "
                         "default: on for 1 process, off under data parallelism")
+    p.add_argument("--rgan_batch_G", type="bool", default=None,
+                   help="run the G step's D(G(z)) and D(x) (heads 5-8) as one batched pass (per-call BN "
+                        "kept, gradient through the D(G(z)) half only); default: on")
     p.add_argument("--rgan_pac", dest="pac", type=int, default=2 if script == "GAN_losses_iter_PAC" else 1,
                    choices=(1, 2),
                    help="2 = PacGAN-2, the reference's code/GAN_losses_iter_PAC.py (D sees 2 samples packed "

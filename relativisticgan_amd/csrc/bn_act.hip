@@ -737,6 +737,67 @@ extern "C" int rgan_bn_backward_segments(const float* da, const float* y, long l
   return 0;
 }
 
+// Backward sums written by a GEMM's post-op (rgan_conv_post mode 2): part[S][2][C], segment
+// s = phase * Sp + j (Sp = S / phases 64-row segments per phase); batch segment k owns
+// j in [k Sp/nseg, (k+1) Sp/nseg) of every phase.  -> sums[k][2][C]: lane r of a 16-channel x
+// 64-lane block sums its segments in order, then a fixed LDS tree (deterministic).
+__global__ __launch_bounds__(1024) void bn_part_merge(const double* __restrict__ part, int S, int phases, int C,
+                                                      double* __restrict__ sums) {
+  __shared__ double sh[2][MERGE_ROWS][MERGE_CPB];
+  const int k = blockIdx.y, nseg = gridDim.y;
+  const int cl = threadIdx.x % MERGE_CPB, r = threadIdx.x / MERGE_CPB;
+  const int c = blockIdx.x * MERGE_CPB + cl;
+  const int Sp = S / phases, J = Sp / nseg, cnt = phases * J;
+  double a1 = 0.0, a2 = 0.0;
+  if (c < C)
+    for (int i = r; i < cnt; i += MERGE_ROWS) {
+      const int ph = i / J, s = ph * Sp + k * J + (i - ph * J);
+      a1 += part[((size_t)s * 2 + 0) * C + c];
+      a2 += part[((size_t)s * 2 + 1) * C + c];
+    }
+  sh[0][r][cl] = a1;
+  sh[1][r][cl] = a2;
+  __syncthreads();
+  for (int h = MERGE_ROWS / 2; h > 0; h >>= 1) {
+    if (r < h) {
+      sh[0][r][cl] += sh[0][r + h][cl];
+      sh[1][r][cl] += sh[1][r + h][cl];
+    }
+    __syncthreads();
+  }
+  if (r == 0 && c < C) {
+    sums[((size_t)k * 2 + 0) * C + c] = sh[0][0][cl];
+    sums[((size_t)k * 2 + 1) * C + c] = sh[1][0][cl];
+  }
+}
+
+extern "C" int rgan_bn_backward_parts(const float* g, const float* y, long long P, int C, int nseg,
+                                      const float* stats, const float* gamma, const float* beta, const double* part,
+                                      long long S, int phases, float* dy, float* dgamma, float* dbeta, double* sums,
+                                      void* stream) {
+  // g = da * act' (rgan_conv_post mode 2 output), dense NHWC g, y, dy; stats [nseg][2C];
+  // sums: [nseg][2][C] doubles of scratch
+  RGAN_REQUIRE(g && y && stats && part && dy && sums && P > 0 && C > 0 && (nseg == 1 || nseg == 2) &&
+               P % nseg == 0 && phases >= 1 && S > 0 && S % phases == 0 && (S / phases) % nseg == 0);
+  hipStream_t s = (hipStream_t)stream;
+  const BnGeo ga = bn_geo(P, C, C, 1);
+  RGAN_REQUIRE(ga.vec && dense_nhwc(C, 1, C, y) && dense_nhwc(C, 1, C, g) && dense_nhwc(C, 1, C, dy));
+  bn_part_merge<<<dim3(ceil_div(C, MERGE_CPB), nseg), 1024, 0, s>>>(part, (int)S, phases, C, sums);
+  RGAN_CHECK_LAUNCH();
+  const long long Ps = P / nseg;
+  const double inv_pg = 1.0 / (double)Ps;
+  if (nseg == 1)
+    bn_bwd_apply<4, 1><<<apply_grid(ga, P), 256, 0, s>>>(g, C, 1, y, P, C, C, 1, stats, gamma, beta, RGAN_ACT_NONE,
+                                                        0.f, sums, inv_pg, dy, C, 1, dgamma, dbeta, ga.tpr, nullptr, 0,
+                                                        0);
+  else
+    bn_bwd_apply<4, 2><<<apply_grid(ga, P), 256, 0, s>>>(g, C, 1, y, P, C, C, 1, stats, gamma, beta, RGAN_ACT_NONE,
+                                                        0.f, sums, inv_pg, dy, C, 1, dgamma, dbeta, ga.tpr, nullptr, 0,
+                                                        Ps);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int rgan_bn_backward(const float* da, long long dsp, long long dsc, const float* y, long long P,
                                 int C, long long sp, long long sc, const float* stats, const float* gamma,
                                 const float* beta, int act, float act_alpha, float* dy, long long ysp,

@@ -51,6 +51,9 @@ constexpr int BK = 32;
 #ifndef RGAN_XGROUP
 #define RGAN_XGROUP 1
 #endif
+#ifndef RGAN_SPLIT_TARGET  // split-K occupancy target (blocks); variant builds sweep it (tools/build_variant.py)
+#define RGAN_SPLIT_TARGET 512
+#endif
 
 // n / d for 0 <= n < 2^31 via multiply-high (host-computed magic numbers)
 struct FastDiv {
@@ -105,7 +108,36 @@ struct GemmArgs {
   int xgroup, nph;        // XCD-grouped tile order (blocks sharing A rows on one XCD); phases
   double* bnp;            // nullable: BatchNorm moments of every 64-row output segment (vector epilogue)
   int accum;              // WGRAD: add into C (gradient accumulation) instead of overwriting it
+  // Post-op for the layer that PRODUCED this GEMM's output operand (rgan_conv_post: a data
+  // gradient, or G's image-layer gradient GEMM), applied where the value is final (unsplit
+  // epilogue or split-K reduce); px has C's layout (host-checked):
+  //   pmode 1: C = v * act'(px), px = the producer's activation output (its act backward);
+  //   pmode 2: C = g = v * act'(px * al + be), px = the producer's BatchNorm input y, al/be
+  //            from (mean, invstd) pst[k][2N] of batch segment k and gamma/beta, plus the
+  //            BatchNorm backward sums (sum g, sum g (y - mean)) of every 64-row segment into
+  //            ppart[seg][2][N] in double (seg as bnp's) -- the bn_bwd_partial pass.
+  const float* px;
+  const float* pst;
+  const float* pgam;
+  const float* pbet;
+  double* ppart;
+  int pmode, pact, pnseg;
+  float palpha;
 };
+
+// per-channel BatchNorm affine of the producer (pmode 2): z = y * al + be
+__device__ __forceinline__ void post_consts(const GemmArgs& g, int k, int n, float& al, float& be, float& mu) {
+  const int c = min(n, g.N - 1);
+  const float* st = g.pst + (size_t)k * 2 * g.N;
+  mu = st[c];
+  al = (g.pgam ? g.pgam[c] : 1.f) * st[g.N + c];
+  be = (g.pbet ? g.pbet[c] : 0.f) - mu * al;
+}
+
+// batch segment of output row m (pmode 2, pnseg equal segments of the M rows of every phase)
+__device__ __forceinline__ int post_seg(const GemmArgs& g, int m) {
+  return g.pnseg > 1 ? m / (g.M / g.pnseg) : 0;
+}
 
 __device__ __forceinline__ long long row_offset(const OutMap& o, int m, int phase) {
   uint32_t b = o.fghw.div(m);
@@ -887,6 +919,16 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
       const int q = lane & 15, n = n0 + wn + 4 * q;
       float* slab = slab_out ? g.slab + (size_t)z * g.M * g.N : nullptr;
       const long long noff = (slab_out || n >= g.N) ? 0 : col_offset(g.out, n);
+      // producer post-op (unsplit only; the reduce applies it to split tiles).  pmode 2: the
+      // wave's 64 rows are one 64-row segment of one batch segment (host: bn_post_ok)
+      const int pmode = slab_out ? 0 : g.pmode;
+      float p_al[4], p_be[4], p_mu[4];
+      double p1[4] = {0.0, 0.0, 0.0, 0.0}, p2[4] = {0.0, 0.0, 0.0, 0.0};
+      if (pmode == 2) {
+        const int k = post_seg(g, m0 + wm);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) post_consts(g, k, n + i, p_al[i], p_be[i], p_mu[i]);
+      }
 #pragma unroll
       for (int pp = 0; pp < NP; ++pp) {
         if (pp > 0) __syncthreads();  // the previous pass's T reads are done
@@ -915,8 +957,25 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
           for (int s4 = 0; s4 < EPR / 4; ++s4) {
             const int rl = 4 * s4 + (lane >> 4), m = m0 + wm + EPR * pp + rl;
             if (m < g.M) {
-              const float4 v = *reinterpret_cast<const float4*>(T + rl * EP_LD + 4 * q);
-              float* dst = slab_out ? slab + (size_t)m * g.N + n : g.C + emoff[wm + EPR * pp + rl] + noff;
+              float4 v = *reinterpret_cast<const float4*>(T + rl * EP_LD + 4 * q);
+              const long long ooff = slab_out ? 0 : emoff[wm + EPR * pp + rl] + noff;
+              float* dst = slab_out ? slab + (size_t)m * g.N + n : g.C + ooff;
+              if (pmode) {
+                const float4 a = *reinterpret_cast<const float4*>(g.px + ooff);
+                float vv[4] = {v.x, v.y, v.z, v.w};
+                const float aa[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  if (pmode == 1) {
+                    vv[i] *= act_grad_from_out(aa[i], g.pact, g.palpha);
+                  } else {
+                    vv[i] *= act_grad_from_in(aa[i] * p_al[i] + p_be[i], g.pact, g.palpha);
+                    p1[i] += (double)vv[i];
+                    p2[i] += (double)vv[i] * (double)(aa[i] - p_mu[i]);
+                  }
+                }
+                v = make_float4(vv[0], vv[1], vv[2], vv[3]);
+              }
 #if RGAN_EXP_NOSTORE
               if (v.x == 1234.5f)
 #endif
@@ -931,6 +990,28 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
           const size_t seg = (size_t)phase * (uint32_t)(g.M >> 6) + (uint32_t)(mrow >> 6);
           g.bnp[(seg * 2) * g.N + col] = s1;
           g.bnp[(seg * 2 + 1) * g.N + col] = s2;
+        }
+      }
+      if (pmode == 2) {
+        // the 4 row groups (lane >> 4) of each column quad: fixed xor-butterfly (a + b == b + a
+        // bitwise, so every lane of a group ends with the same sums)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          p1[i] += __shfl_xor(p1[i], 16);
+          p2[i] += __shfl_xor(p2[i], 16);
+          p1[i] += __shfl_xor(p1[i], 32);
+          p2[i] += __shfl_xor(p2[i], 32);
+        }
+        const int mrow = m0 + wm;
+        if ((lane >> 4) == 0 && mrow < g.M) {
+          const size_t seg = (size_t)phase * (uint32_t)(g.M >> 6) + (uint32_t)(mrow >> 6);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            if (n + i < g.N) {
+              g.ppart[(seg * 2) * g.N + n + i] = p1[i];
+              g.ppart[(seg * 2 + 1) * g.N + n + i] = p2[i];
+            }
+          }
         }
       }
       return;
@@ -982,6 +1063,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
             {
               float* dst = g.C + moff[rl] + noff[cl];
               v = actf(v);
+              if (MODE != MODE_WGRAD && g.pmode == 1) v *= act_grad_from_out(g.px[moff[rl] + noff[cl]], g.pact, g.palpha);
               *dst = (MODE == MODE_WGRAD && g.accum) ? *dst + v : v;
             }
           }
@@ -1066,10 +1148,17 @@ __global__ __launch_bounds__(256) void splitk_reduce(GemmArgs g, FastDiv fdiv, u
       const int n = 4 * (int)(idx - m * fdiv.d);
       float v[4];
       red_sum<4>(base + (size_t)m * g.N + n, MN, g.splits, v);
-      const float4 o = make_float4(red_epi(g, v[0], wsc, n), red_epi(g, v[1], wsc, n + 1),
-                                   red_epi(g, v[2], wsc, n + 2), red_epi(g, v[3], wsc, n + 3));
-      float4* dst = reinterpret_cast<float4*>(g.C + row_offset(g.out, (int)m, MODE == MODE_CONVT2 ? phase : 0) +
-                                              col_offset(g.out, n));
+      float4 o = make_float4(red_epi(g, v[0], wsc, n), red_epi(g, v[1], wsc, n + 1),
+                             red_epi(g, v[2], wsc, n + 2), red_epi(g, v[3], wsc, n + 3));
+      const long long ooff = row_offset(g.out, (int)m, MODE == MODE_CONVT2 ? phase : 0) + col_offset(g.out, n);
+      float4* dst = reinterpret_cast<float4*>(g.C + ooff);
+      if (MODE != MODE_WGRAD && g.pmode == 1) {
+        const float4 a = *reinterpret_cast<const float4*>(g.px + ooff);
+        o.x *= act_grad_from_out(a.x, g.pact, g.palpha);
+        o.y *= act_grad_from_out(a.y, g.pact, g.palpha);
+        o.z *= act_grad_from_out(a.z, g.pact, g.palpha);
+        o.w *= act_grad_from_out(a.w, g.pact, g.palpha);
+      }
       if (g.accum) {
         const float4 q = *dst;
         *dst = make_float4(q.x + o.x, q.y + o.y, q.z + o.z, q.w + o.w);
@@ -1101,8 +1190,10 @@ __global__ __launch_bounds__(256) void splitk_reduce(GemmArgs g, FastDiv fdiv, u
       const int n = (int)(idx - m * fdiv.d);
       float v[1];
       red_sum<1>(base + (size_t)m * g.N + n, MN, g.splits, v);
-      float* dst = g.C + row_offset(g.out, (int)m, MODE == MODE_CONVT2 ? phase : 0) + col_offset(g.out, n);
-      const float o = red_epi(g, v[0], wsc, n);
+      const long long ooff = row_offset(g.out, (int)m, MODE == MODE_CONVT2 ? phase : 0) + col_offset(g.out, n);
+      float* dst = g.C + ooff;
+      float o = red_epi(g, v[0], wsc, n);
+      if (MODE != MODE_WGRAD && g.pmode == 1) o *= act_grad_from_out(g.px[ooff], g.pact, g.palpha);
       *dst = g.accum ? *dst + o : o;
     }
   }
@@ -1119,6 +1210,10 @@ __global__ __launch_bounds__(256) void splitk_reduce(GemmArgs g, FastDiv fdiv, u
 // by a fixed LDS tree (deterministic).  grid = (segments * column chunks, phases).
 constexpr int REDBN_QB = 8;
 
+// BWD (pmode 2, the producer's BatchNorm backward sums -- see GemmArgs::pmode): the rows
+// written are g = v * act'(y al + be) and the segment sums are (sum g, sum g (y - mean)),
+// y read at the rows' own offsets; the same block / tree structure.
+template <bool BWD>
 __global__ __launch_bounds__(256) void splitk_reduce_bn(GemmArgs g, int mode_t2, int qb) {
   __shared__ double sh[2][256][4];
   const int phase = blockIdx.y;
@@ -1132,6 +1227,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_bn(GemmArgs g, int mode_t2,
   if (q < Q) {
     const int n = 4 * q;
     const long long noff = col_offset(g.out, n);
+    float p_al[4], p_be[4], p_mu[4];
+    if constexpr (BWD) {
+      const int k = post_seg(g, segm * 64);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) post_consts(g, k, n + i, p_al[i], p_be[i], p_mu[i]);
+    }
     for (int r0 = rl; r0 < 64; r0 += 2 * RL) {  // RL <= 32: two rows per pass
       const int m0 = segm * 64 + r0, m1 = m0 + RL;
       const float* p0 = base + (size_t)m0 * g.N + n;
@@ -1147,17 +1248,33 @@ __global__ __launch_bounds__(256) void splitk_reduce_bn(GemmArgs g, int mode_t2,
                                     red_epi(g, v0.z, wsc, n + 2), red_epi(g, v0.w, wsc, n + 3));
       const float4 o1 = make_float4(red_epi(g, v1.x, wsc, n), red_epi(g, v1.y, wsc, n + 1),
                                     red_epi(g, v1.z, wsc, n + 2), red_epi(g, v1.w, wsc, n + 3));
-      *reinterpret_cast<float4*>(g.C + row_offset(g.out, m0, mode_t2 ? phase : 0) + noff) = o0;
-      *reinterpret_cast<float4*>(g.C + row_offset(g.out, m1, mode_t2 ? phase : 0) + noff) = o1;
-      const float a[2][4] = {{o0.x, o0.y, o0.z, o0.w}, {o1.x, o1.y, o1.z, o1.w}};
+      const long long off0 = row_offset(g.out, m0, mode_t2 ? phase : 0) + noff;
+      const long long off1 = row_offset(g.out, m1, mode_t2 ? phase : 0) + noff;
+      float a[2][4] = {{o0.x, o0.y, o0.z, o0.w}, {o1.x, o1.y, o1.z, o1.w}};
+      if constexpr (BWD) {
+        const float4 y0 = *reinterpret_cast<const float4*>(g.px + off0);
+        const float4 y1 = *reinterpret_cast<const float4*>(g.px + off1);
+        const float yy[2][4] = {{y0.x, y0.y, y0.z, y0.w}, {y1.x, y1.y, y1.z, y1.w}};
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const double d = (double)a[h][i];
-          s1[i] += d;
-          s2[i] += d * d;
-        }
+          for (int i = 0; i < 4; ++i) {
+            a[h][i] *= act_grad_from_in(yy[h][i] * p_al[i] + p_be[i], g.pact, g.palpha);
+            s1[i] += (double)a[h][i];
+            s2[i] += (double)a[h][i] * (double)(yy[h][i] - p_mu[i]);
+          }
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const double d = (double)a[h][i];
+            s1[i] += d;
+            s2[i] += d * d;
+          }
+      }
+      *reinterpret_cast<float4*>(g.C + off0) = make_float4(a[0][0], a[0][1], a[0][2], a[0][3]);
+      *reinterpret_cast<float4*>(g.C + off1) = make_float4(a[1][0], a[1][1], a[1][2], a[1][3]);
     }
   }
 #pragma unroll
@@ -1175,10 +1292,11 @@ __global__ __launch_bounds__(256) void splitk_reduce_bn(GemmArgs g, int mode_t2,
   }
   if (rl == 0 && q < Q) {
     const size_t seg = (size_t)phase * (uint32_t)(g.M >> 6) + (uint32_t)segm;
+    double* out = BWD ? g.ppart : g.bnp;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      g.bnp[(seg * 2) * g.N + 4 * q + i] = sh[0][tid][i];
-      g.bnp[(seg * 2 + 1) * g.N + 4 * q + i] = sh[1][tid][i];
+      out[(seg * 2) * g.N + 4 * q + i] = sh[0][tid][i];
+      out[(seg * 2 + 1) * g.N + 4 * q + i] = sh[1][tid][i];
     }
   }
 }
@@ -2348,6 +2466,9 @@ struct Plan {
   double* bn_part = nullptr;
   int bn_segs = 1;
   bool bn_fused = false;
+  // producer post-op (rgan_conv_post): requested, and whether this plan applies it
+  const RganPost* post = nullptr;
+  bool post_fused = false;
 };
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
@@ -2369,7 +2490,7 @@ static void choose_tiling(Plan& p) {
   int splits = 1;
   // two resident 256-thread blocks per CU on 256 CUs (round-1 sweep of this target: 256 / 384 / 768 /
   // 1024 all lost to 512, profiles/round1_splitk_target_sweep.txt)
-  constexpr long long target = 512;
+  constexpr long long target = RGAN_SPLIT_TARGET;
   if (tiles < target) {
     splits = (int)((target + tiles - 1) / tiles);
     splits = std::min(splits, std::max(1, nk / 4));
@@ -3007,6 +3128,21 @@ static bool bn_reduce_ok(const Plan& p, bool check_ptr) {
 
 static long long bn_epilogue_segments(const Plan& p) { return (long long)p.phases * (p.g.M / 64); }
 
+// producer post-op (GemmArgs::pmode).  Mode 1: every CONV / CONVT2 GEMM epilogue and reduce
+// (vector or scalar) except the tap-staged / accumulating ones.  Mode 2: the vector epilogue
+// of unsplit FAST 128x128 tiles or the BN reduce of split tiles, n = channel, 64-row
+// segments that never straddle a phase or a batch segment.  Call after vec_out is set.
+static bool post_ok(const Plan& p, int mode, int nseg, bool check_ptr) {
+  const GemmArgs& g = p.g;
+  if (p.mode != MODE_CONV && p.mode != MODE_CONVT2) return false;
+  if (p.tap_stage || g.accum || g.bias || g.act != RGAN_ACT_NONE) return false;
+  if (mode == 1) return true;
+  if (mode != 2 || nseg < 1 || g.out.fnc.d != (uint32_t)g.N || g.M % 64 != 0) return false;
+  if (nseg > 1 && (g.M % nseg != 0 || (g.M / nseg) % 64 != 0)) return false;
+  if (g.splits == 1) return p.fast && p.cfg == CFG_L && g.vec_out;
+  return red_vec_ok(p, check_ptr) && g.N >= 4 * REDBN_QB;
+}
+
 static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   if (ws_bytes < plan_ws_bytes(p)) return RGAN_EINVAL;
   if (p.mode == MODE_NARROW_T || p.mode == MODE_NARROW_IN || p.mode == MODE_DENSE1) {
@@ -3070,6 +3206,15 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   }
   p.bn_fused = p.bn_part && (bn_epilogue_ok(p) || bn_reduce_ok(p, true));
   p.g.bnp = p.bn_fused ? p.bn_part : nullptr;
+  p.post_fused = p.post && !p.bn_fused && post_ok(p, p.post->mode, p.post->nseg, true) &&
+                 (p.post->mode != 2 || bn_epilogue_segments(p) <= p.post->part_segments);
+  if (p.post_fused) {
+    const RganPost& q = *p.post;
+    p.g.pmode = q.mode; p.g.pact = q.act; p.g.palpha = q.alpha; p.g.pnseg = q.nseg;
+    p.g.px = q.x; p.g.pst = q.stats; p.g.pgam = q.gamma; p.g.pbet = q.beta; p.g.ppart = q.part;
+  } else {
+    p.g.pmode = 0;
+  }
   int bm, bn;
   tile_dims(p.cfg, bm, bn);
   const int tiles_m = ceil_div(p.g.M, bm);
@@ -3120,12 +3265,13 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
       per /= 4;
       d = o.fnc.d;
     }
-    if (p.bn_fused) {  // bn_reduce_ok: the RED_VEC shape with segment moments
+    if (p.bn_fused || g.pmode == 2) {  // the RED_VEC shape with segment moments / backward sums
       const int Q = g.N / 4;
       int qb = 1;  // quads per block: 8 (32 channels, 128-B row pieces), fewer for narrow N
       while (qb * 2 <= std::min(Q, REDBN_QB)) qb *= 2;
       const dim3 bgrid((unsigned)((g.M / 64) * ceil_div(Q, qb)), p.phases);
-      splitk_reduce_bn<<<bgrid, 256, 0, s>>>(g, p.mode == MODE_CONVT2, qb);
+      if (g.pmode == 2) splitk_reduce_bn<true><<<bgrid, 256, 0, s>>>(g, p.mode == MODE_CONVT2, qb);
+      else splitk_reduce_bn<false><<<bgrid, 256, 0, s>>>(g, p.mode == MODE_CONVT2, qb);
       RGAN_CHECK_LAUNCH();
       return 0;
     }
@@ -3401,6 +3547,41 @@ extern "C" int rgan_conv_dgrad(const RganConv* d, const float* dy, const float* 
   if (!p.pack && !w) return RGAN_EINVAL;  // kernels that read the torch layout
   p.prepacked = wpacked;
   return run_plan(p, ws, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" long long rgan_conv_post_segments(const RganConv* d, int which, int mode, int nseg, int* phases) {
+  Plan p;
+  alignas(16) static const float dummy[4] = {0, 0, 0, 0};
+  int rc = which == 0 ? plan_fwd(d, dummy, dummy, nullptr, nullptr, (float*)dummy, 0, 0.f, p)
+                      : plan_dgrad(d, dummy, dummy, nullptr, (float*)dummy, p);
+  if (rc || (which != 0 && which != 1) || mode != 2) return 0;
+  const OutMap& o = p.g.out;
+  auto al4 = [](long long v) { return (v & 3) == 0; };
+  p.g.vec_out = p.mode != MODE_WGRAD && o.tc == 1 && o.fnc.d % 4 == 0 && p.g.N % 4 == 0 && al4(o.th) &&
+                al4(o.tw) && al4(o.sb) && al4(o.sh) && al4(o.sw);
+  if (phases) *phases = p.phases;
+  return post_ok(p, mode, nseg, false) ? bn_epilogue_segments(p) : 0;
+}
+
+extern "C" int rgan_conv_post(const RganConv* d, int which, const float* in, const float* w, const float* wpacked,
+                              const float* wscale, float* out, void* ws, size_t ws_bytes, const RganPost* post,
+                              int* fused, void* stream) {
+  if (!in || (!w && !wpacked) || !out || !fused || !post || (which != 0 && which != 1)) return RGAN_EINVAL;
+  if (!post->x || (post->mode != 1 && post->mode != 2)) return RGAN_EINVAL;
+  if (post->mode == 2 && (!post->stats || !post->part || post->nseg < 1)) return RGAN_EINVAL;
+  *fused = 0;
+  g_cur_flops = conv_flops(d);
+  Plan p;
+  int rc = which == 0 ? plan_fwd(d, in, w, wscale, nullptr, out, RGAN_ACT_NONE, 0.f, p)
+                      : plan_dgrad(d, in, w, wscale, out, p);
+  if (rc) return rc;
+  if (!p.pack && !w) return RGAN_EINVAL;
+  p.prepacked = wpacked;
+  p.post = post;
+  rc = run_plan(p, ws, ws_bytes, (hipStream_t)stream);
+  if (rc) return rc;
+  *fused = p.post_fused ? 1 : 0;
+  return 0;
 }
 
 extern "C" int rgan_conv_wgrad(const RganConv* d, const float* x, const float* dy, float* dw,

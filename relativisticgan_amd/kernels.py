@@ -274,18 +274,20 @@ def nn_unfold_grad(dwt, w_shape):
     return dw
 
 
-def conv_fwd(x, w, geom, bias=None, act="none", alpha=0.0, wscale=None, out=None, nchw_out=False, cache=False):
+def conv_fwd(x, w, geom, bias=None, act="none", alpha=0.0, wscale=None, out=None, nchw_out=False, cache=False,
+             post=None):
     """y = act(conv(x, w)*wscale + bias); x [B,Cin,H,W] any strides; w torch layout.
 
     ``cache=True`` (module parameters only) reuses a packed weight while its version is
-    unchanged."""
+    unchanged.  ``post`` (no bias / act): a Post for the producer of ... (see conv_dgrad) --
+    used when this conv computes a gradient (G's image-layer data gradient as a 1x1 GEMM)."""
     L.require_cuda(x, w, bias, wscale)
     _f32(x, w, bias)
     if geom.upsample != 1:
         _nn_check(geom)
         wt = FOLDS.get(w) if cache else nn_fold(w)
         return conv_fwd(x, wt, NN_T, bias=bias, act=act, alpha=alpha, wscale=wscale, out=out, nchw_out=nchw_out,
-                        cache=cache)
+                        cache=cache, post=post)
     B, cin, H, W = x.shape
     cout = w.shape[1] if geom.transposed else w.shape[0]
     Ho, Wo = geom.out_hw(H, W)
@@ -299,6 +301,10 @@ def conv_fwd(x, w, geom, bias=None, act="none", alpha=0.0, wscale=None, out=None
     if nbytes == 0:
         raise L.RganError(f"unsupported conv {geom} for input {tuple(x.shape)}")
     ws = L.workspace(nbytes, x.device)
+    if post is not None:
+        post.fused = False
+        if bias is None and act == "none" and _conv_post(0, d, x, w, packed, wscale, out, ws, post) is not False:
+            return out
     L.check(lib.rgan_conv_fwd(ctypes.byref(d), L.ptr(x), L.ptr(w), L.ptr(packed), L.ptr(wscale), L.ptr(bias),
                               L.ptr(out), L.ACT[act], float(alpha), L.ptr(ws), ws.numel(), L.stream()),
             "rgan_conv_fwd")
@@ -356,14 +362,58 @@ def bn_segment_moments(part, s0, s1, C):
     return mom
 
 
-def conv_dgrad(dy, w, geom, x_shape, wscale=None, out=None, like=None, cache=False):
-    """dx of the conv (input grad), NHWC unless `like` (a tensor whose strides to copy) is given."""
+class Post:
+    """Producer post-op of rgan_conv_post (include/rgan.h RganPost): the backward pass of the
+    layer that produced this GEMM's output operand, applied in the GEMM's epilogue / split-K
+    reduce.  mode 1: out *= act'(x) (x = its activation output); mode 2: out = g = out *
+    act'(BN(x)) and the BatchNorm backward sums per 64-row segment (x = its BN input y; finish
+    with bn_backward_parts).  After the call ``fused`` says whether the GEMM applied it
+    (else the output is the plain gradient) and, for mode 2, ``part`` / ``S`` / ``phases``
+    hold the sums."""
+
+    __slots__ = ("mode", "act", "alpha", "x", "stats", "gamma", "beta", "nseg", "fused", "part", "S", "phases")
+
+    def __init__(self, mode, act, alpha, x, stats=None, gamma=None, beta=None, nseg=1):
+        self.mode, self.act, self.alpha, self.x = mode, act, float(alpha), x
+        self.stats, self.gamma, self.beta, self.nseg = stats, gamma, beta, nseg
+        self.fused, self.part, self.S, self.phases = False, None, 0, 1
+
+
+def _conv_post(which, d, inp, w, packed, wscale, out, ws, post):
+    """rgan_conv_post for ``post`` (see Post); returns False when the GEMM cannot apply it."""
+    if (tuple(post.x.shape) != tuple(out.shape) or post.x.stride() != out.stride()
+            or post.x.data_ptr() % 16 or out.data_ptr() % 16):
+        return False
+    lib = L.lib()
+    part, S = None, 0
+    if post.mode == 2:
+        ph = L.c_int(1)
+        S = lib.rgan_conv_post_segments(ctypes.byref(d), which, 2, int(post.nseg), ctypes.byref(ph))
+        post.phases = ph.value
+        if S <= 0:
+            return False
+        part = torch.empty((S, 2, out.shape[1]), dtype=torch.float64, device=out.device)
+    rp = L.RganPost(int(post.mode), L.ACT[post.act], float(post.alpha), int(post.nseg), post.x.data_ptr(),
+                    L.ptr(post.stats), L.ptr(post.gamma), L.ptr(post.beta), L.ptr(part), int(S))
+    fused = L.c_int(0)
+    L.check(lib.rgan_conv_post(ctypes.byref(d), which, L.ptr(inp), L.ptr(w), L.ptr(packed), L.ptr(wscale),
+                               L.ptr(out), L.ptr(ws), ws.numel(), ctypes.byref(rp), ctypes.byref(fused), L.stream()),
+            "rgan_conv_post")
+    if not fused.value:
+        return None  # the plain result was written
+    post.fused, post.part, post.S = True, part, S
+    return True
+
+
+def conv_dgrad(dy, w, geom, x_shape, wscale=None, out=None, like=None, cache=False, post=None):
+    """dx of the conv (input grad), NHWC unless `like` (a tensor whose strides to copy) is given.
+    ``post``: a Post for the layer that produced x (applied when the GEMM can: post.fused)."""
     L.require_cuda(dy, w, wscale)
     _f32(dy, w)
     if geom.upsample != 1:
         _nn_check(geom)
         wt = FOLDS.get(w) if cache else nn_fold(w)
-        return conv_dgrad(dy, wt, NN_T, x_shape, wscale=wscale, out=out, like=like, cache=cache)
+        return conv_dgrad(dy, wt, NN_T, x_shape, wscale=wscale, out=out, like=like, cache=cache, post=post)
     B, cin, H, W = x_shape
     if out is None:
         if like is not None and not is_nhwc(like):
@@ -377,6 +427,10 @@ def conv_dgrad(dy, w, geom, x_shape, wscale=None, out=None, like=None, cache=Fal
     if nbytes == 0:
         raise L.RganError(f"unsupported conv dgrad {geom} for {tuple(x_shape)}")
     ws = L.workspace(nbytes, dy.device)
+    if post is not None:
+        post.fused = False
+        if _conv_post(1, d, dy, w, packed, wscale, out, ws, post) is not False:
+            return out
     L.check(lib.rgan_conv_dgrad(ctypes.byref(d), L.ptr(dy), L.ptr(w), L.ptr(packed), L.ptr(wscale), L.ptr(out),
                                 L.ptr(ws), ws.numel(), L.stream()), "rgan_conv_dgrad")
     return out
@@ -525,6 +579,24 @@ def bn_backward_segments(da, y, stats, gamma, beta, act, alpha, need_gamma, need
                                           L.ACT[act], float(alpha), L.ptr(out), L.ptr(dgamma), L.ptr(dbeta),
                                           L.ptr(ws), L.stream()), "rgan_bn_backward_segments")
     return out, dgamma, dbeta
+
+
+def bn_backward_parts(g, y, stats, gamma, beta, post, need_gamma, need_beta, out=None):
+    """dy (and dgamma / dbeta summed over the batch segments) from g = da * act' and the
+    segment sums a GEMM's post-op wrote (Post mode 2, post.fused): merge + apply."""
+    P, C, _, _ = _pc(y)
+    nseg = post.nseg
+    if stats.dim() == 1:
+        stats = stats.view(1, -1)
+    dy = torch.empty_like(y) if out is None else out
+    dgamma = torch.empty(C, dtype=torch.float32, device=y.device) if need_gamma and gamma is not None else None
+    dbeta = torch.empty(C, dtype=torch.float32, device=y.device) if need_beta and beta is not None else None
+    sums = torch.empty((nseg, 2, C), dtype=torch.float64, device=y.device)
+    L.check(L.lib().rgan_bn_backward_parts(L.ptr(g), L.ptr(y), P, C, nseg, L.ptr(stats), L.ptr(gamma), L.ptr(beta),
+                                           L.ptr(post.part), int(post.S), int(post.phases), L.ptr(dy),
+                                           L.ptr(dgamma), L.ptr(dbeta), L.ptr(sums), L.stream()),
+            "rgan_bn_backward_parts")
+    return dy, dgamma, dbeta
 
 
 def bn_apply(y, stats, gamma, beta, act="none", alpha=0.0, out=None):
@@ -697,8 +769,9 @@ def loss_head_dist(kind, side, phase, r, f, n_global, gsum=None, need_dr=True, n
     return sums, loss, dr, df
 
 
-def scale(t, s):
-    out = torch.empty_like(t)
+def scale(t, s, out=None):
+    if out is None:
+        out = torch.empty_like(t)
     L.check(L.lib().rgan_scale(L.ptr(t), L.ptr(s), t.numel(), L.ptr(out), L.stream()), "rgan_scale")
     return out
 

@@ -15,6 +15,29 @@ from . import dp
 from . import kernels as K
 
 
+_UNIT_SEEDS = {}  # data_ptr -> tensor: device scalars 1.0 used as backward seeds (Trainer._backward)
+
+
+def unit_seed(device, dtype=torch.float32):
+    """A device scalar 1.0 for ``loss.backward(seed)``: the heads' backward recognises it and
+    hands its saved gradients on as they are (x * 1.0 == x: no scale launch)."""
+    one = torch.ones((), dtype=dtype, device=device)
+    _UNIT_SEEDS[one.data_ptr()] = one
+    return one
+
+
+def _is_unit(g):
+    u = _UNIT_SEEDS.get(g.data_ptr())
+    return u is not None and g.numel() == 1 and g.dtype == u.dtype and g.device == u.device
+
+
+def _times(t, g):
+    """t * g (g the upstream scalar gradient)."""
+    if t is None:
+        return None
+    return t if _is_unit(g) else K.scale(t, g.contiguous())
+
+
 class _Head(torch.autograd.Function):
     @staticmethod
     def forward(ctx, r, f, kind, side):
@@ -30,9 +53,7 @@ class _Head(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         dr, df = ctx.saved_tensors
-        g = g.contiguous()
-        return (K.scale(dr, g) if dr is not None else None,
-                K.scale(df, g) if df is not None else None, None, None)
+        return _times(dr, g), _times(df, g), None, None
 
 
 def _head_dist(kind, side, r, f, need_r, need_f):
@@ -83,9 +104,7 @@ class _HeadPair(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g, _g3):
         dr, df = ctx.saved_tensors
-        g = g.contiguous()
-        return (K.scale(dr, g) if dr is not None else None,
-                K.scale(df, g) if df is not None else None, None)
+        return _times(dr, g), _times(df, g), None
 
 
 def loss_D_pair(kind, y_pred, y_pred_fake):
@@ -120,7 +139,7 @@ class _HeadCat(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         dy, = ctx.saved_tensors
-        return K.scale(dy, g.contiguous()), None
+        return _times(dy, g), None
 
 
 def loss_D_cat(kind, y):
@@ -129,6 +148,41 @@ def loss_D_cat(kind, y):
         B = y.numel() // 2
         return (loss_D_pair(kind, y[:B], y[B:])[0] if kind <= 4 else loss_D(kind, y[:B], y[B:]))
     return _HeadCat.apply(y, kind)
+
+
+class _HeadCatG(torch.autograd.Function):
+    """errG of heads 5-8 (GLI:695-707) on the G step's batched output y = [D(G(z)); D(x)]:
+    the gradient is written for the fake half only (D(x) is a constant there); the rows of
+    the real half are left unwritten -- the batched pass's backward reads the fake rows
+    only (ConvLayerFn ``gsegs``)."""
+
+    @staticmethod
+    def forward(ctx, y, kind):
+        B = y.numel() // 2
+        if dp.active():
+            loss, _, df = _head_dist(kind, 2, y[B:], y[:B], False, True)
+        else:
+            df = torch.empty_like(y)  # the fake rows' gradient in the first half
+            loss, _, _ = K.loss_head(kind, 2, y[B:], y[:B], need_dr=False, df=df[:B])
+        ctx.save_for_backward(df)
+        ctx.B = B
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        df, = ctx.saved_tensors
+        B = ctx.B
+        if df.numel() == 2 * B and _is_unit(g):
+            return df, None
+        out = torch.empty(2 * B, dtype=df.dtype, device=df.device)
+        K.scale(df[:B], g.contiguous(), out=out[:B])
+        return out, None
+
+
+def loss_G_cat(kind, y):
+    """errG (heads 5-8) from the G step's joint [D(G(z)); D(x)] output."""
+    assert 5 <= kind <= 8
+    return _HeadCatG.apply(y, kind)
 
 
 def loss_D(kind, y_pred, y_pred_fake):

@@ -169,9 +169,11 @@ class _Layer:
         w = conv.w if isinstance(conv, _ConvBase) else conv.weight
         return w.view(*self.w_view) if self.w_view is not None else w
 
-    def run(self, h, training, segs=1, out=None, sn=None):
+    def run(self, h, training, segs=1, out=None, sn=None, gsegs=None, link_in=None, link_out=None):
         """``sn``: this call's (u, v, inv_sigma) when the net already ran the power
-        iteration of all its spectral layers (_Net._spectral)."""
+        iteration of all its spectral layers (_Net._spectral); ``gsegs``: leading segments
+        that carry an output gradient (ConvLayerFn); ``link_in`` / ``link_out``: the
+        autograd.LayerLink to the layer below / above in the same chain call."""
         conv, bn = self.conv, self.bn
         w = self.weight()
         if self.in_view is not None:
@@ -185,7 +187,8 @@ class _Layer:
         if out is not None and self.out_view is not None:
             raise ValueError("an output buffer for a reshaped layer")
         res = ConvLayerFn.apply(h, w, conv.bias, bn.weight if bn is not None else None,
-                                bn.bias if bn is not None else None, self.spec, bufs, sn, segs, out)
+                                bn.bias if bn is not None else None, self.spec, bufs, sn, segs, out, gsegs,
+                                link_in, link_out)
         if self.out_view is not None:
             res = res.reshape(res.shape[0], *self.out_view)
         return res
@@ -214,15 +217,26 @@ class _Net(nn.Module):
                                          for li in idx])
         return dict(zip(idx, outs))
 
+    def _links(self):
+        """One autograd.LayerLink per boundary between consecutive layers whose output feeds
+        the next layer directly (no reshape between them), else None: the upper layer's
+        data-gradient GEMM then applies the lower layer's activation / BatchNorm backward pass
+        in its epilogue."""
+        plan = self._plan
+        return [AG.LayerLink() if plan[i].out_view is None and plan[i + 1].in_view is None else None
+                for i in range(len(plan) - 1)] + [None]
+
     def _run(self, x, out=None):
         """``out``: a buffer for the last layer's output (e.g. half of a batched D input)."""
         AG.TRACE_NET = self._tag
         h = x
         last = len(self._plan) - 1
         sns = self._spectral()
+        links = self._links()
         for li, layer in enumerate(self._plan):
             AG.TRACE_LAYER = li
-            h = layer.run(h, self.training, out=out if li == last else None, sn=sns.get(li))
+            h = layer.run(h, self.training, out=out if li == last else None, sn=sns.get(li),
+                          link_in=links[li - 1] if li else None, link_out=links[li])
         return h
 
     @property
@@ -231,12 +245,15 @@ class _Net(nn.Module):
         reference runs one power iteration per call, so each call has its own sigma)."""
         return not any(layer.spec is not None and layer.spec.spectral for layer in self._plan)
 
-    def forward_segments(self, xs, cat=None, flat=False):
+    def forward_segments(self, xs, cat=None, flat=False, grad_segs=None):
         """``[self(x) for x in xs]`` as ONE pass over the concatenated batch: every layer's
         GEMMs run once over all segments, BatchNorm normalises (and updates its running
         statistics) per segment in list order, exactly as the separate calls would.
-        ``cat``: the segments already laid out back to back in one tensor (no copy);
-        ``flat``: return the joint output (segments back to back) instead of a list."""
+        ``cat``: the segments already laid out back to back in one tensor (no copy; inputs
+        that require grad get it back through _Joined);
+        ``flat``: return the joint output (segments back to back) instead of a list;
+        ``grad_segs``: only the leading segments' outputs get a gradient (the rest is used
+        as a constant, e.g. the G step's no-graph D(x)): the backward runs over their rows."""
         if not self.segmentable:
             raise ValueError("forward_segments: a spectral-norm layer needs one call per forward")
         n = len(xs)
@@ -245,10 +262,19 @@ class _Net(nn.Module):
             raise ValueError("forward_segments: segments must have equal shapes")
         trace0 = len(AG.ACT_TRACE) if AG.ACT_TRACE is not None else 0
         AG.TRACE_NET = self._tag
-        h = cat if cat is not None else torch.cat(xs)
+        if grad_segs is not None and any(x.requires_grad for x in xs[grad_segs:]):
+            raise ValueError("forward_segments: an input past grad_segs requires grad")
+        if cat is None:
+            h = torch.cat(xs)
+        elif any(x.requires_grad for x in xs):
+            h = _Joined.apply(cat, *xs)
+        else:
+            h = cat
+        links = self._links()
         for li, layer in enumerate(self._plan):
             AG.TRACE_LAYER = li
-            h = layer.run(h, self.training, n)
+            h = layer.run(h, self.training, n, gsegs=grad_segs, link_in=links[li - 1] if li else None,
+                          link_out=links[li])
         if AG.ACT_TRACE is not None:  # activation masks in the separate calls' order
             masks = AG.ACT_TRACE[trace0:]
             layers = AG.ACT_LAYERS[trace0:]
@@ -260,6 +286,29 @@ class _Net(nn.Module):
                 AG.ACT_TAGS.extend(self._tag for _ in masks)
                 AG.ACT_LAYERS.extend(layers)
         return h if flat else list(h.split(B))
+
+    def forward_pair_G(self, fake, x, cat=None):
+        """[D(G(z)); D(x)] of the G step (GLI:674, 695-707) as one batched pass: BatchNorm
+        per call in the reference's call order (fake first), gradient through the fake half
+        only (the reference's D(x) there has no graph: D's parameters are frozen, x is data)."""
+        return self.forward_segments([fake, x], cat, flat=True, grad_segs=1).reshape(-1)
+
+
+class _Joined(torch.autograd.Function):
+    """The segments ``xs`` already written back to back into ``cat`` (e.g. G's output
+    written into the first half of the batched D input): a view of ``cat`` whose gradient
+    goes back to each segment's producer as its rows (no concatenation either way)."""
+
+    @staticmethod
+    def forward(ctx, cat, *xs):
+        ctx.B = xs[0].shape[0]
+        ctx.need = [x.requires_grad for x in xs]
+        return cat.view_as(cat)
+
+    @staticmethod
+    def backward(ctx, g):
+        B = ctx.B
+        return (None,) + tuple(g[k * B:(k + 1) * B] if need else None for k, need in enumerate(ctx.need))
 
 
 # ---------------------------------------------------------------- arch 0 (DCGAN)

@@ -21,7 +21,7 @@ import torch
 from . import autograd, dp
 from .config import TITLES, parse
 from .kernels import DeviceRNG
-from .losses import gradient_penalty, loss_D, loss_D_cat, loss_D_fake, loss_D_real, loss_G
+from .losses import gradient_penalty, loss_D, loss_D_cat, loss_D_fake, loss_D_real, loss_G, loss_G_cat, unit_seed
 from .nets import DCGAN_D, DCGAN_G, weights_init
 from .optim import Adam
 
@@ -100,6 +100,10 @@ class Trainer:
         bd = getattr(p, "rgan_batch_D", None)
         bd = (self.world == 1) if bd is None else bool(bd)
         self.batch_D = bd and self.pac == 1 and self.D.segmentable
+        # the G step's D(G(z)) and D(x) (heads 5-8) as one batched pass (--rgan_batch_G,
+        # default on, under data parallelism too: nothing overlaps with its D(x) forward)
+        bg = getattr(p, "rgan_batch_G", None)
+        self.batch_G = (True if bg is None else bool(bg)) and self.pac == 1 and self.D.segmentable
         self._fake_D = None
         self._one = None
         self.errD = self.errG = None
@@ -172,8 +176,8 @@ class Trainer:
         """loss.backward() (GLI:605/624/644/658/710) with a cached device 1.0 as the seed
         gradient (autograd would fill a fresh ones tensor on every call)."""
         one = self._one
-        if one is None or one.device != loss.device:
-            one = self._one = torch.ones((), dtype=loss.dtype, device=loss.device)
+        if one is None or one.device != loss.device or one.dtype != loss.dtype:
+            one = self._one = unit_seed(loss.device, loss.dtype)
         with autograd.owning_grads():  # the fused layers write their weight .grad directly
             loss.backward(one)
 
@@ -263,7 +267,14 @@ class Trainer:
             self.flush()
             G.zero_grad()
             z = self._normal(feed, "z_G", zshape)
-            if self.pac == 1:
+            pair_G = None
+            if self.batch_G and kind > 4:
+                # D(G(z)) and the fresh real batch's D(x) as one batched pass: G writes its
+                # output and the gather its images into one buffer, back to back
+                pair_G = torch.empty((2 * self.B, p.n_colors, p.image_size, p.image_size), dtype=torch.float32,
+                                     device=self.device)
+                fake = G(z, out=pair_G[:self.B])
+            elif self.pac == 1:
                 fake = G(z)
             else:
                 # PAC:673-674: the G step reuses the D step's G(z) (graph kept; G's weights
@@ -272,15 +283,26 @@ class Trainer:
                 # a version bump: the first layer's weight gradient reads the NEW z.
                 self._zbuf.data.copy_(z)
                 fake, self._fake_D = self._pack(self._fake_D), None
-            y_pred_fake = D(fake)
-            y_pred = None
             recG = {"z": z}
-            if kind > 4:
-                x = self._real(feed, "x_G")
-                with torch.no_grad():
-                    y_pred = D(x)
+            if pair_G is not None:
+                # GLI:674 then GLI:677-682 + 695-707: the draw order (z, then the real batch)
+                # and the BN call order (D(fake), then D(x)) are the reference's
+                x = self._real(feed, "x_G", out=pair_G[self.B:])
+                laid_out = (fake.data_ptr() == pair_G.data_ptr()
+                            and x.data_ptr() == pair_G[self.B:].data_ptr())
+                y_all = D.forward_pair_G(fake, x, cat=pair_G if laid_out else None)
+                y_pred_fake, y_pred = y_all[:self.B], y_all[self.B:].detach()
                 recG.update(x=x, y_pred=y_pred)
-            errG = loss_G(kind, y_pred_fake, y_pred)
+                errG = loss_G_cat(kind, y_all)
+            else:
+                y_pred_fake = D(fake)
+                y_pred = None
+                if kind > 4:
+                    x = self._real(feed, "x_G")
+                    with torch.no_grad():
+                        y_pred = D(x)
+                    recG.update(x=x, y_pred=y_pred)
+                errG = loss_G(kind, y_pred_fake, y_pred)
             self._arm(self.redG)
             self._backward(errG)
             recG.update(y_pred_fake=y_pred_fake.detach(), errG=errG.detach())

@@ -913,3 +913,58 @@ def test_bn_backward_two_segments(K):
                                    dbeta=db1, accumulate_affine=k > 0)
         dy2, dg2, db2 = K.bn_backward_segments(da, y, stats, gamma, beta, act, 0.2, True, True, torch.empty_like(y))
         assert torch.equal(dy1, dy2) and torch.equal(dg1, dg2) and torch.equal(db1, db2), act
+
+
+# (B, cin, cout, H, transposed): the data gradient of a k4 s2 p1 conv of this shape, whose
+# output x (cin channels) a lower layer produced.  Conv: CONVT2 (4 phases); ConvT: CONV.
+# Large M -> unsplit vector epilogue; small M -> split-K reduce.
+POST_CASES = [
+    (64, 128, 256, 32, False),   # CONVT2, M = 64*16*16 per phase: 512 unsplit 128x128 tiles
+    (4, 128, 256, 16, False),    # CONVT2, split-K
+    (8, 256, 128, 16, True),     # CONV (ConvT dgrad), M = 8*16*16 = 2048: split-K
+    (64, 128, 64, 32, True),     # CONV, M = 65536: unsplit
+]
+
+
+@pytest.mark.parametrize("case", POST_CASES)
+@pytest.mark.parametrize("mode", [1, 2])
+def test_dgrad_post_op(K, case, mode):
+    """rgan_conv_post (the layer below's first backward pass in the data-gradient GEMM's
+    epilogue / split-K reduce) == conv_dgrad followed by that pass: mode 1 = act_backward
+    (LeakyReLU, Tanh), mode 2 = bn_backward (g = da * act', the BatchNorm sums, then
+    bn_backward_parts) with 1 and 2 batch segments."""
+    from relativisticgan_amd.kernels import ConvGeom, Post
+    B, cin, cout, H, tr = case
+    torch.manual_seed(23)
+    g = ConvGeom(4, 2, 1, tr)
+    Ho = H // 2 if not tr else H * 2
+    w = (torch.randn(cin, cout, 4, 4, device=DEV) if tr else torch.randn(cout, cin, 4, 4, device=DEV)) * 0.05
+    dy = _nhwc(torch.randn(B, cout, Ho, Ho, device=DEV))
+    xs = (B, cin, H, H)
+    ref_da = K.conv_dgrad(dy, w, g, xs)
+    for act in ("lrelu", "tanh"):
+        if mode == 1:
+            a = _nhwc(torch.tanh(torch.randn(xs, device=DEV))) if act == "tanh" else \
+                _nhwc(F.leaky_relu(torch.randn(xs, device=DEV), 0.2))
+            post = Post(1, act, 0.2, a)
+            got = K.conv_dgrad(dy, w, g, xs, post=post)
+            assert post.fused, (case, act)
+            want = K.act_backward(ref_da, a, act, 0.2)
+            assert _rel(got, want) < 1e-6, (case, act, _rel(got, want))
+            continue
+        y = _nhwc(torch.randn(xs, device=DEV) * 2 + 0.3)
+        gamma, beta = torch.rand(cin, device=DEV) + 0.5, torch.randn(cin, device=DEV)
+        for nseg in (1, 2):
+            stats = torch.cat([torch.randn(nseg, cin, device=DEV) * 0.1 + 0.3,
+                               torch.rand(nseg, cin, device=DEV) + 0.5], 1)
+            post = Post(2, act, 0.2, y, stats=stats, gamma=gamma, beta=beta, nseg=nseg)
+            gz = K.conv_dgrad(dy, w, g, xs, post=post)
+            assert post.fused, (case, act, nseg)
+            dyb, dgb, dbb = K.bn_backward_parts(gz, y, stats, gamma, beta, post, True, True)
+            if nseg == 1:
+                dyw, dgw, dbw = K.bn_backward(ref_da, y, stats[0], gamma, beta, act, 0.2)
+            else:
+                dyw, dgw, dbw = K.bn_backward_segments(ref_da, y, stats, gamma, beta, act, 0.2, True, True,
+                                                       torch.empty_like(y))
+            for k, (u, v) in {"dy": (dyb, dyw), "dgamma": (dgb, dgw), "dbeta": (dbb, dbw)}.items():
+                assert _rel(u, v) < 1e-5, (case, act, nseg, k, _rel(u, v))

@@ -1,0 +1,38 @@
+"""A/B of the layer hand-offs (autograd.LayerLink: the lower layer's activation / BatchNorm
+backward pass fused into the upper layer's data-gradient GEMM) in one process on one box:
+bench.py's timed graph replays of a workload, alternating LINKS on / off.
+
+usage: python tools/ab_links.py [workload=C1] [rounds=3] [steps=20]
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from relativisticgan_amd import autograd as AG  # noqa: E402
+from relativisticgan_amd import kernels as K  # noqa: E402
+
+
+def main():
+    name = sys.argv[1] if len(sys.argv) > 1 else "C1"
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    args = argparse.Namespace(batch_d="auto", graph="auto", sync_bn=False)
+    res = {True: [], False: []}
+    for r in range(rounds):
+        for on in (True, False) if r % 2 == 0 else (False, True):
+            AG.LINKS = on
+            out = bench.run_workload(name, steps, 5, 1, args, K)
+            res[on].append(out["value"])
+            print(f"{name} links={'on ' if on else 'off'} {out['value']:9.1f} img/s  {out['ms_per_step']:.3f} ms/step",
+                  flush=True)
+    for on in (True, False):
+        v = sorted(res[on])
+        print(f"{name} links={'on ' if on else 'off'} median {v[len(v) // 2]:.1f} img/s  all {[round(x, 1) for x in v]}")
+
+
+if __name__ == "__main__":
+    main()
