@@ -129,6 +129,20 @@ int rgan_conv_post(const RganConv* d, int which, const float* in, const float* w
                    const float* wscale, float* out, void* ws, size_t ws_bytes, const RganPost* post,
                    int* fused, void* stream);
 
+/* G's first layer on its 1x1 input (GLI:334-345: ConvTranspose2d(z, Cout, 4, 1, 0) + train-
+ * mode BatchNorm2d + activation) in one launch: y[b][t][c] = sum_ci z[b][ci] W[ci][c][t]
+ * (t = 4 kh + kw; y, a NHWC [B][4][4][Cout]), the BatchNorm batch statistics of each channel
+ * over its B x 16 values (exact two-pass, double), running statistics + num_batches_tracked
+ * updated as torch does, stats = (mean, invstd) [2][Cout], a = act(BN(y)).  z [B][Cin]
+ * contiguous, 16-B aligned; B in {32, 64}; Cin % 4 == 0; Cout % 16 == 0.
+ * rgan_g1_wgrad: its weight gradient dW[ci][c][t] (+)= sum_b z[b][ci] dy[b][t][c] (dy NHWC). */
+int rgan_g1_fwd_bn(const float* z, int B, int Cin, const float* w, int Cout, const float* gamma,
+                   const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                   long long* num_batches_tracked, int act, float act_alpha, float* y, float* a, float* stats,
+                   void* stream);
+int rgan_g1_wgrad(const float* z, int B, int Cin, const float* dy, int Cout, float* dw, int accumulate,
+                  void* stream);
+
 /* dw = d conv / d w applied to dy (aten convolution_backward, grad_weight), written
  * in torch weight layout; dbias (nullable) = per-output-channel sum of dy.
  * accumulate != 0: dw += ..., dbias += ... (autograd's gradient accumulation into an

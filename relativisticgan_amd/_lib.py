@@ -62,6 +62,9 @@ _SIGS = {
                                ctypes.POINTER(RganPost), ctypes.POINTER(c_int), c_vp]),
     "rgan_bn_backward_parts": (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_ll, c_int, c_vp,
                                        c_vp, c_vp, c_vp, c_vp]),
+    "rgan_g1_fwd_bn": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_f, c_f, c_vp, c_vp, c_vp, c_int, c_f,
+                               c_vp, c_vp, c_vp, c_vp]),
+    "rgan_g1_wgrad": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp]),
     "rgan_conv_dgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "rgan_conv_wgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_sz, c_vp]),
     "rgan_nn_fold_weight": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),

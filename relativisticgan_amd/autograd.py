@@ -236,14 +236,23 @@ class ConvLayerFn(torch.autograd.Function):
         # sn   = (u, v, inv_sigma) clones for spectral layers, else None
         wscale = sn[2] if spec.spectral else None
         stats_eval = None
+        g1 = False
         if spec.bn:
             rm, rv, nbt, training = bufs
-            if training:
+            g1 = (training and segs == 1 and bias is None and wscale is None and not dp.sync_bn()
+                  and K.g1_ok(x, w, spec.geom))
+            if g1:
+                # G's first layer on its 1x1 input: conv + BatchNorm + act in one launch
+                y, a, stats = K.g1_fwd_bn(x, w, gamma, beta, spec.eps, spec.momentum, rm, rv, nbt, spec.act,
+                                          spec.alpha, out=out)
+            elif training:
                 y, part, S = K.conv_fwd_bn(x, w, spec.geom, bias=bias, wscale=wscale, cache=True, segs=segs)
             else:
                 y, part, S = K.conv_fwd(x, w, spec.geom, bias=bias, wscale=wscale, cache=True), None, 0
             C = y.shape[1]
-            if training and segs > 1:
+            if g1:
+                pass
+            elif training and segs > 1:
                 Bs = y.shape[0] // segs
                 a = torch.empty_like(y) if out is None else out
                 stats = torch.empty((segs, 2 * C), dtype=torch.float32, device=y.device)
@@ -279,6 +288,7 @@ class ConvLayerFn(torch.autograd.Function):
         ctx.stats_eval = stats_eval
         ctx.training = bufs[3] if bufs is not None else True
         ctx.segs = segs
+        ctx.g1 = g1
         ctx.gsegs = segs if gsegs is None else gsegs
         ctx.link_in, ctx.link_out = link_in, link_out
         if link_out is not None and LINKS:
@@ -401,6 +411,8 @@ class ConvLayerFn(torch.autograd.Function):
                     u, v, inv_sigma = sn
                     dwe, _ = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape))
                     g = K.spectral_backward(w, dwe, u, v, inv_sigma, spec.geom.transposed, out=acc)
+                elif ctx.g1:
+                    g = K.g1_wgrad(x, dy, tuple(w.shape), out=acc)
                 else:
                     g, _ = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), out=acc)
                 if acc is None:
@@ -413,7 +425,11 @@ class ConvLayerFn(torch.autograd.Function):
                 # (dp.grad_view), which autograd then adopts as .grad (no bucket copy)
                 into = (dp.grad_view(w) if nw and not (bias is not None and nb) and not spec.spectral
                         and spec.geom.upsample == 1 else None)
-                dw, db = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), with_bias=bias is not None and nb, into=into)
+                if ctx.g1 and nw:
+                    dw, db = K.g1_wgrad(x, dy, tuple(w.shape), into=into), None
+                else:
+                    dw, db = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), with_bias=bias is not None and nb,
+                                          into=into)
         if nw or nb:
             if spec.spectral and nw:
                 u, v, inv_sigma = sn

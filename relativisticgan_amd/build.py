@@ -19,7 +19,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I" + os.path.join(ROOT, "include"),
          "-Wno-unused-result", "-munsafe-fp-atomics"]
 SOURCES = ["conv_gemm.hip", "bn_act.hip", "heads_optim.hip", "upsample.hip", "images.hip", "patches.hip",
-           "sampling.hip"]
+           "sampling.hip", "first_layer.hip"]
 
 
 def _stale(obj, src):

@@ -165,7 +165,7 @@ __device__ __forceinline__ long long col_offset(const OutMap& o, int n) {
 // WGRAD: the gradient rows are pixel-contiguous (offset = p * pixel stride: scalar
 // advance) and the im2col operand reads one tap per block tile (Cin % BN == 0) through
 // a per-tile table of pixel offsets built by one wave into LDS two tiles ahead.
-template <int MODE, int BM, int BN, int WM, int WN, bool AV, bool BV, bool FAST, bool EMU>
+template <int MODE, int BM, int BN, int WM, int WN, bool AV, bool BV, bool FAST, bool EMU, bool POST = false>
 __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   constexpr int TM = BM / WM / 32, TN = BN / WN / 32;
   static_assert(TM >= 1 && TN >= 1 && WM * WN == 4, "tile config");
@@ -921,7 +921,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
       const long long noff = (slab_out || n >= g.N) ? 0 : col_offset(g.out, n);
       // producer post-op (unsplit only; the reduce applies it to split tiles).  pmode 2: the
       // wave's 64 rows are one 64-row segment of one batch segment (host: bn_post_ok)
-      const int pmode = slab_out ? 0 : g.pmode;
+      const int pmode = (!POST || slab_out) ? 0 : g.pmode;
       float p_al[4], p_be[4], p_mu[4];
       double p1[4] = {0.0, 0.0, 0.0, 0.0}, p2[4] = {0.0, 0.0, 0.0, 0.0};
       if (pmode == 2) {
@@ -952,30 +952,43 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
             s2 += d * d;
           }
         }
-        if (n < g.N) {
+        if (n < g.N && pmode) {
+          // producer post-op: the wave's 16 rows of px first (independent loads in flight
+          // together -- one latency, not one per row), then the rows
+          float4 ax[EPR / 4];
+#pragma unroll
+          for (int s4 = 0; s4 < EPR / 4; ++s4) {
+            const int rl = 4 * s4 + (lane >> 4), m = m0 + wm + EPR * pp + rl;
+            ax[s4] = m < g.M ? *reinterpret_cast<const float4*>(g.px + emoff[wm + EPR * pp + rl] + noff)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
 #pragma unroll
           for (int s4 = 0; s4 < EPR / 4; ++s4) {
             const int rl = 4 * s4 + (lane >> 4), m = m0 + wm + EPR * pp + rl;
             if (m < g.M) {
-              float4 v = *reinterpret_cast<const float4*>(T + rl * EP_LD + 4 * q);
-              const long long ooff = slab_out ? 0 : emoff[wm + EPR * pp + rl] + noff;
-              float* dst = slab_out ? slab + (size_t)m * g.N + n : g.C + ooff;
-              if (pmode) {
-                const float4 a = *reinterpret_cast<const float4*>(g.px + ooff);
-                float vv[4] = {v.x, v.y, v.z, v.w};
-                const float aa[4] = {a.x, a.y, a.z, a.w};
+              const float4 v = *reinterpret_cast<const float4*>(T + rl * EP_LD + 4 * q);
+              float vv[4] = {v.x, v.y, v.z, v.w};
+              const float aa[4] = {ax[s4].x, ax[s4].y, ax[s4].z, ax[s4].w};
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                  if (pmode == 1) {
-                    vv[i] *= act_grad_from_out(aa[i], g.pact, g.palpha);
-                  } else {
-                    vv[i] *= act_grad_from_in(aa[i] * p_al[i] + p_be[i], g.pact, g.palpha);
-                    p1[i] += (double)vv[i];
-                    p2[i] += (double)vv[i] * (double)(aa[i] - p_mu[i]);
-                  }
+              for (int i = 0; i < 4; ++i) {
+                if (pmode == 1) {
+                  vv[i] *= act_grad_from_out(aa[i], g.pact, g.palpha);
+                } else {
+                  vv[i] *= act_grad_from_in(aa[i] * p_al[i] + p_be[i], g.pact, g.palpha);
+                  p1[i] += (double)vv[i];
+                  p2[i] += (double)vv[i] * (double)(aa[i] - p_mu[i]);
                 }
-                v = make_float4(vv[0], vv[1], vv[2], vv[3]);
               }
+              *reinterpret_cast<float4*>(g.C + emoff[wm + EPR * pp + rl] + noff) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+            }
+          }
+        } else if (n < g.N) {
+#pragma unroll
+          for (int s4 = 0; s4 < EPR / 4; ++s4) {
+            const int rl = 4 * s4 + (lane >> 4), m = m0 + wm + EPR * pp + rl;
+            if (m < g.M) {
+              const float4 v = *reinterpret_cast<const float4*>(T + rl * EP_LD + 4 * q);
+              float* dst = slab_out ? slab + (size_t)m * g.N + n : g.C + emoff[wm + EPR * pp + rl] + noff;
 #if RGAN_EXP_NOSTORE
               if (v.x == 1234.5f)
 #endif
@@ -1063,7 +1076,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
             {
               float* dst = g.C + moff[rl] + noff[cl];
               v = actf(v);
-              if (MODE != MODE_WGRAD && g.pmode == 1) v *= act_grad_from_out(g.px[moff[rl] + noff[cl]], g.pact, g.palpha);
               *dst = (MODE == MODE_WGRAD && g.accum) ? *dst + v : v;
             }
           }
@@ -1081,6 +1093,14 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
 template <int MODE, int BM, int BN, int WM, int WN, bool AV, bool BV, bool FAST>
 __global__ __launch_bounds__(256, RGAN_GEMM_SB ? 4 : 2) void gemm_kernel(GemmArgs g) {
   gemm_body<MODE, BM, BN, WM, WN, AV, BV, FAST, false>(g);
+}
+
+// The FAST 128 x 128 CONV / CONVT2 GEMM with a producer post-op in its vector epilogue
+// (GemmArgs::pmode, rgan_conv_post): its own instantiation, so the plain GEMMs' registers and
+// schedule stay those of the post-free epilogue.
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void gemm_post(GemmArgs g) {
+  gemm_body<MODE, 128, 128, 2, 2, true, true, true, false, true>(g);
 }
 
 // Opt-in (rgan_set_gemm_emulation): the FAST 128 x 128 CONV / CONVT2 GEMM with fp32 products
@@ -2941,6 +2961,10 @@ static bool plan_emu(const Plan& p) {
 template <int MODE>
 static void launch_mode(const Plan& p, dim3 grid, hipStream_t s) {
   if constexpr (MODE == MODE_CONV || MODE == MODE_CONVT2) {
+    if (p.g.pmode && p.g.splits == 1) {  // post_ok: FAST 128x128 (the post-op in the epilogue)
+      gemm_post<MODE><<<grid, 256, 0, s>>>(p.g);
+      return;
+    }
     if (plan_emu(p)) {
       gemm_bf16x6<MODE><<<grid, 256, 0, s>>>(p.g);
       return;
@@ -2970,7 +2994,7 @@ static std::vector<ProfRec> g_recs;
 static std::vector<std::string> g_kernel_names;
 static double g_cur_flops = 0.0;
 
-constexpr int N_KERNEL_IDS = 53;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in + 2 bf16x6
+constexpr int N_KERNEL_IDS = 55;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in + 2 bf16x6 + 2 post
 
 static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
   const int id = mode == MODE_NARROW_T ? 45
@@ -3005,6 +3029,8 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
     g_kernel_names[50] = "void rgan::conv_img_in<CI, WT, ACT>(rgan::NarrowArgs)";
     g_kernel_names[51] = "void rgan::gemm_bf16x6<0>(rgan::GemmArgs)";
     g_kernel_names[52] = "void rgan::gemm_bf16x6<1>(rgan::GemmArgs)";
+    g_kernel_names[53] = "void rgan::gemm_post<0>(rgan::GemmArgs)";
+    g_kernel_names[54] = "void rgan::gemm_post<1>(rgan::GemmArgs)";
   }
   return id;
 }
@@ -3128,14 +3154,15 @@ static bool bn_reduce_ok(const Plan& p, bool check_ptr) {
 
 static long long bn_epilogue_segments(const Plan& p) { return (long long)p.phases * (p.g.M / 64); }
 
-// producer post-op (GemmArgs::pmode).  Mode 1: every CONV / CONVT2 GEMM epilogue and reduce
-// (vector or scalar) except the tap-staged / accumulating ones.  Mode 2: the vector epilogue
-// of unsplit FAST 128x128 tiles or the BN reduce of split tiles, n = channel, 64-row
-// segments that never straddle a phase or a batch segment.  Call after vec_out is set.
+// producer post-op (GemmArgs::pmode): unsplit FAST 128x128 tiles (gemm_post's vector
+// epilogue) or split tiles (mode 1: every reduce shape of CONV / CONVT2; mode 2: the BN
+// reduce); mode 2 also needs n = channel and 64-row segments that never straddle a phase or
+// a batch segment.  Call after vec_out is set.
 static bool post_ok(const Plan& p, int mode, int nseg, bool check_ptr) {
   const GemmArgs& g = p.g;
   if (p.mode != MODE_CONV && p.mode != MODE_CONVT2) return false;
   if (p.tap_stage || g.accum || g.bias || g.act != RGAN_ACT_NONE) return false;
+  if (g.splits == 1 && !(p.fast && p.cfg == CFG_L && g.vec_out)) return false;  // gemm_post's epilogue
   if (mode == 1) return true;
   if (mode != 2 || nseg < 1 || g.out.fnc.d != (uint32_t)g.N || g.M % 64 != 0) return false;
   if (nseg > 1 && (g.M % nseg != 0 || (g.M / nseg) % 64 != 0)) return false;
@@ -3230,6 +3257,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     rec.flops = g_cur_flops;
     rec.kid = kernel_id(p.mode, p.cfg, p.av, p.bv, p.fast);
     if (plan_emu(p)) rec.kid = 51 + p.mode;
+    if (p.g.pmode && p.g.splits == 1) rec.kid = 53 + p.mode;
     hipEventRecord(rec.a, s);
   }
   switch (p.mode) {

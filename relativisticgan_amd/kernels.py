@@ -436,6 +436,44 @@ def conv_dgrad(dy, w, geom, x_shape, wscale=None, out=None, like=None, cache=Fal
     return out
 
 
+def g1_ok(x, w, geom):
+    """G's first layer on its 1x1 input can run as rgan_g1_fwd_bn / rgan_g1_wgrad."""
+    return (geom.transposed and geom.k == 4 and geom.stride == 1 and geom.pad == 0 and geom.upsample == 1
+            and x.dim() == 4 and tuple(x.shape[2:]) == (1, 1) and x.shape[0] in (32, 64) and x.shape[1] % 4 == 0
+            and w.shape[1] % 16 == 0 and w.is_contiguous() and x.is_contiguous() and x.data_ptr() % 16 == 0
+            and x.shape[0] * x.shape[1] * 4 + 32 * 256 * 4 <= 64 * 1024)
+
+
+def g1_fwd_bn(x, w, gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked, act, alpha,
+              out=None):
+    """(y, a, stats) of G's first layer + BatchNorm + act in one launch (rgan_g1_fwd_bn)."""
+    L.require_cuda(x, w)
+    B, cin = x.shape[0], x.shape[1]
+    cout = w.shape[1]
+    y = empty_nhwc(B, cout, 4, 4, x.device)
+    a = empty_nhwc(B, cout, 4, 4, x.device) if out is None else out
+    if not is_nhwc(a):
+        raise L.RganError("g1_fwd_bn: out must be NHWC")
+    stats = torch.empty(2 * cout, dtype=torch.float32, device=x.device)
+    L.check(L.lib().rgan_g1_fwd_bn(L.ptr(x), B, cin, L.ptr(w), cout, L.ptr(gamma), L.ptr(beta), float(eps),
+                                   float(momentum), L.ptr(running_mean), L.ptr(running_var),
+                                   L.ptr(num_batches_tracked), L.ACT[act], float(alpha), L.ptr(y), L.ptr(a),
+                                   L.ptr(stats), L.stream()), "rgan_g1_fwd_bn")
+    return y, a, stats
+
+
+def g1_wgrad(x, dy, w_shape, out=None, into=None):
+    """dW of G's first layer (rgan_g1_wgrad); ``out``: add into it, ``into``: write into it."""
+    L.require_cuda(x, dy)
+    if not is_nhwc(dy):
+        dy = dy.contiguous(memory_format=torch.channels_last)
+    dw = out if out is not None else (into if into is not None else
+                                      torch.empty(w_shape, dtype=torch.float32, device=x.device))
+    L.check(L.lib().rgan_g1_wgrad(L.ptr(x), x.shape[0], x.shape[1], L.ptr(dy), w_shape[1], L.ptr(dw),
+                                  int(out is not None), L.stream()), "rgan_g1_wgrad")
+    return dw
+
+
 def conv_wgrad(x, dy, geom, w_shape, with_bias=False, out=None, out_bias=None, into=None):
     """(dw in torch layout, dbias or None).  ``out`` / ``out_bias`` given: the gradients are
     ADDED into them in the GEMM epilogue (autograd accumulation without an add pass);

@@ -968,3 +968,45 @@ def test_dgrad_post_op(K, case, mode):
                                                        torch.empty_like(y))
             for k, (u, v) in {"dy": (dyb, dyw), "dgamma": (dgb, dgw), "dbeta": (dbb, dbw)}.items():
                 assert _rel(u, v) < 1e-5, (case, act, nseg, k, _rel(u, v))
+
+
+@pytest.mark.parametrize("B,cin,cout,act", [(32, 128, 1024, "relu"), (64, 128, 512, "tanh"), (32, 100, 256, "relu")])
+def test_first_layer_fused(K, B, cin, cout, act):
+    """rgan_g1_fwd_bn (G's 1x1 -> 4x4 ConvTranspose2d + train-mode BatchNorm2d + act in one
+    launch) and rgan_g1_wgrad vs torch fp64: y, a, batch statistics, running statistics and
+    num_batches_tracked, and the weight gradient (written and accumulated).  Cin = 100 (not a
+    multiple of 4) must be refused by g1_ok (the GEMM path runs)."""
+    from relativisticgan_amd.kernels import ConvGeom
+    torch.manual_seed(29)
+    g = ConvGeom(4, 1, 0, True)
+    z = torch.randn(B, cin, 1, 1, device=DEV)
+    w = torch.randn(cin, cout, 4, 4, device=DEV) * 0.05
+    if cin % 4:
+        assert not K.g1_ok(z, w, g)
+        return
+    assert K.g1_ok(z, w, g)
+    gamma, beta = torch.rand(cout, device=DEV) + 0.5, torch.randn(cout, device=DEV) * 0.1
+    rm, rv = torch.randn(cout, device=DEV) * 0.1, torch.rand(cout, device=DEV) + 0.5
+    nbt = torch.zeros((), dtype=torch.long, device=DEV)
+    rm0, rv0 = rm.clone(), rv.clone()
+    y, a, stats = K.g1_fwd_bn(z, w, gamma, beta, 1e-5, 0.1, rm, rv, nbt, act, 0.0)
+    y64 = F.conv_transpose2d(z.double().cpu(), w.double().cpu())
+    mean = y64.mean((0, 2, 3))
+    var = y64.var((0, 2, 3), unbiased=False)
+    a64 = F.batch_norm(y64, None, None, gamma.double().cpu(), beta.double().cpu(), training=True, eps=1e-5)
+    a64 = torch.relu(a64) if act == "relu" else torch.tanh(a64)
+    assert K.is_nhwc(y) and K.is_nhwc(a)
+    assert _rel(y, y64) < 1e-6 and _rel(a, a64) < 1e-5
+    assert _rel(stats[:cout], mean) < 1e-6 and _rel(stats[cout:], 1 / torch.sqrt(var + 1e-5)) < 1e-6
+    n = B * 16
+    assert _rel(rm, 0.9 * rm0.double().cpu() + 0.1 * mean) < 1e-6
+    assert _rel(rv, 0.9 * rv0.double().cpu() + 0.1 * var * n / (n - 1)) < 1e-6
+    assert int(nbt.item()) == 1
+    dy = _nhwc(torch.randn(B, cout, 4, 4, device=DEV))
+    dw = K.g1_wgrad(z, dy, tuple(w.shape))
+    dw64 = torch.einsum("bi,bohw->iohw", z.double().cpu().flatten(1), dy.double().cpu())
+    assert _rel(dw, dw64) < 1e-6
+    base = torch.randn_like(dw)
+    acc = base.clone()
+    K.g1_wgrad(z, dy, tuple(w.shape), out=acc)
+    assert _rel(acc - base, dw64) < 1e-5
