@@ -134,7 +134,8 @@ int rgan_conv_post(const RganConv* d, int which, const float* in, const float* w
  * (t = 4 kh + kw; y, a NHWC [B][4][4][Cout]), the BatchNorm batch statistics of each channel
  * over its B x 16 values (exact two-pass, double), running statistics + num_batches_tracked
  * updated as torch does, stats = (mean, invstd) [2][Cout], a = act(BN(y)).  z [B][Cin]
- * contiguous, 16-B aligned; B in {32, 64}; Cin % 4 == 0; Cout % 16 == 0.
+ * contiguous, 16-B aligned; B in {32, 64} (the batch sizes of BASELINE's configs); Cin (z size)
+ * in {64, 128}; Cout % 16 == 0 (other shapes run the GEMM + BatchNorm entry points).
  * rgan_g1_wgrad: its weight gradient dW[ci][c][t] (+)= sum_b z[b][ci] dy[b][t][c] (dy NHWC). */
 int rgan_g1_fwd_bn(const float* z, int B, int Cin, const float* w, int Cout, const float* gamma,
                    const float* beta, float eps, float momentum, float* running_mean, float* running_var,

@@ -6,79 +6,84 @@
 // W[ci][co][t] (t = 4 kh + kw) with M = B rows only: as an implicit GEMM it is one 128-row m
 // tile (B = 32 uses a quarter) over 4 k tiles, latency-bound (17 us at C1, 7 TF/s) and
 // followed by three BatchNorm launches.  Here ONE launch does all of it: a block owns 16
-// output channels x 16 taps = 256 columns (thread = column) and the whole batch, so each
-// channel's B x 16 BatchNorm population is inside the block:
-//   1. y columns by fp32 FMA over ci (z staged in LDS, read as broadcasts; W rows of the
-//      block's 256 columns are contiguous in torch layout [ci][co][t]);
-//   2. per channel: exact two-pass mean / variance in double over the block-resident values
-//      (the 16 tap lanes of a channel are 16 consecutive lanes: fixed xor-butterfly), running
-//      statistics updated as torch does (unbiased variance), (mean, invstd) written;
+// output channels x 16 taps and the whole batch (1024 threads: a thread = one column x a
+// quarter of the batch rows), so each channel's B x 16 BatchNorm population is one wave's:
+//   1. y by fp32 FMA over ci in order (z staged in LDS, read as float4 broadcasts; a thread's
+//      W column read 64 entries at a time into registers -- one load latency per chunk);
+//   2. per channel: exact two-pass mean / variance in double over the wave's registers
+//      (fixed xor-butterfly), running statistics updated as torch does (unbiased
+//      variance), (mean, invstd) written;
 //   3. a = act(y * al + be) with al = gamma * invstd, be = beta - mean * al (bn_apply's form);
 //      y (for the backward) and a written NHWC through an LDS transpose (64-B channel runs).
 // The block's columns stay in registers for the whole batch (B <= 64): W is read once.
-// rgan_g1_wgrad: dW[ci][co][t] (+)= sum_b z[b][ci] * dy[b][t][co], thread = column, the
-// column's B gradient values in registers, z broadcast from LDS.
+// rgan_g1_wgrad: dW[ci][co][t] (+)= sum_b z[b][ci] * dy[b][t][co], thread = column x a quarter
+// of the ci range, the column's B gradient values in registers, z broadcast from LDS.
 #include "common.h"
 
 namespace rgan {
 
-constexpr int G1_CB = 16;   // channels per block (x 16 taps = 256 threads)
-// batch sizes with an instantiation (the column's B values live in registers): 32, 64
+constexpr int G1_CB = 16;   // channels per block (x 16 taps x 4 batch / ci groups = 1024 threads)
+constexpr int G1_WCH = 32;  // W entries of a thread's column held in registers at a time
+// instantiated for B (batch: a thread's rows live in registers) in {32, 64} and CIN (z size)
+// in {64, 128}
 
-template <int B>
-__global__ __launch_bounds__(256) void g1_fwd_bn_kernel(const float* __restrict__ z, int Cin,
-                                                        const float* __restrict__ w, int Cout,
-                                                        const float* __restrict__ gamma,
-                                                        const float* __restrict__ beta, float eps, float momentum,
-                                                        float* running_mean, float* running_var, long long* nbt,
-                                                        int act, float alpha, float* __restrict__ y,
-                                                        float* __restrict__ a, float* __restrict__ stats) {
+// thread = (channel c_l, group q, tap t): tid = 64 c_l + 16 q + t -- a channel's 64 threads are
+// one wave (its BatchNorm population B x 16 sits in that wave's registers)
+template <int B, int Cin>
+__global__ __launch_bounds__(1024) void g1_fwd_bn_kernel(const float* __restrict__ z,
+                                                         const float* __restrict__ w, int Cout,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float eps, float momentum,
+                                                         float* running_mean, float* running_var, long long* nbt,
+                                                         int act, float alpha, float* __restrict__ y,
+                                                         float* __restrict__ a, float* __restrict__ stats) {
+  constexpr int R = B / 4;                // batch rows per thread: q R .. q R + R - 1
   extern __shared__ float lds[];
   float* zs = lds;                        // [B][Cin]
   float* ys = lds + (size_t)B * Cin;      // [32][16 taps][16 channels]: output staging
   __shared__ float alv[G1_CB], bev[G1_CB];
-  const int tid = threadIdx.x;
-  const int co0 = blockIdx.x * G1_CB;
-  for (int i = tid; i < B * Cin; i += 256) zs[i] = z[i];
+  const int tid = threadIdx.x, c_l = tid >> 6, q = (tid >> 4) & 3, t_l = tid & 15;
+  const int co0 = blockIdx.x * G1_CB, co = co0 + c_l;
+  for (int i = tid; i < B * Cin; i += 1024) zs[i] = z[i];
   __syncthreads();
-  // thread t computes column (channel co0 + (t >> 4), tap t & 15) for the whole batch: its W
-  // entries W[ci][co][tap] are contiguous in t
-  const int c_l = tid >> 4, t_l = tid & 15;
-  const float* wp = w + (size_t)(co0 + c_l) * 16 + t_l;
+  const float* wp = w + (size_t)co * 16 + t_l;  // W[ci][co][t]: the 16 taps contiguous
   const size_t wstride = (size_t)Cout * 16;
-  float acc[B];
+  float acc[R];
 #pragma unroll
-  for (int b = 0; b < B; ++b) acc[b] = 0.f;
-  // ci in order; z rows read as float4 broadcasts (4 ci per LDS read)
-  for (int ci = 0; ci < Cin; ci += 4) {
-    const float w0 = wp[(size_t)ci * wstride], w1 = wp[(size_t)(ci + 1) * wstride];
-    const float w2 = wp[(size_t)(ci + 2) * wstride], w3 = wp[(size_t)(ci + 3) * wstride];
+  for (int j = 0; j < R; ++j) acc[j] = 0.f;
 #pragma unroll
-    for (int b = 0; b < B; ++b) {
-      const float4 zz = *reinterpret_cast<const float4*>(zs + b * Cin + ci);
-      acc[b] = fmaf(zz.w, w3, fmaf(zz.z, w2, fmaf(zz.y, w1, fmaf(zz.x, w0, acc[b]))));
+  for (int c0 = 0; c0 < Cin; c0 += G1_WCH) {
+    // the next G1_WCH entries of the column in flight together (one latency per chunk)
+    float wv[G1_WCH];
+#pragma unroll
+    for (int k = 0; k < G1_WCH; ++k) wv[k] = wp[(size_t)(c0 + k) * wstride];
+#pragma unroll
+    for (int k = 0; k < G1_WCH; k += 4) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) {  // ci in order per output
+        const float4 zz = *reinterpret_cast<const float4*>(zs + (q * R + j) * Cin + c0 + k);
+        acc[j] = fmaf(zz.w, wv[k + 3], fmaf(zz.z, wv[k + 2], fmaf(zz.y, wv[k + 1], fmaf(zz.x, wv[k], acc[j]))));
+      }
     }
   }
-  // channel statistics, exact two-pass in double: the channel's 16 taps are lanes
-  // 16 c_l .. 16 c_l + 15 of one wave (fixed xor-butterfly)
+  // channel statistics, exact two-pass in double over the wave (fixed xor-butterfly)
   double s1 = 0.0;
 #pragma unroll
-  for (int b = 0; b < B; ++b) s1 += (double)acc[b];
+  for (int j = 0; j < R; ++j) s1 += (double)acc[j];
 #pragma unroll
-  for (int o = 1; o < 16; o <<= 1) s1 += __shfl_xor(s1, o);
+  for (int o = 1; o < 64; o <<= 1) s1 += __shfl_xor(s1, o);
   const double n = (double)B * 16.0, mean = s1 / n;
   double s2 = 0.0;
 #pragma unroll
-  for (int b = 0; b < B; ++b) {
-    const double d = (double)acc[b] - mean;
+  for (int j = 0; j < R; ++j) {
+    const double d = (double)acc[j] - mean;
     s2 += d * d;
   }
 #pragma unroll
-  for (int o = 1; o < 16; o <<= 1) s2 += __shfl_xor(s2, o);
-  const int co = co0 + c_l;
+  for (int o = 1; o < 64; o <<= 1) s2 += __shfl_xor(s2, o);
   const double var = s2 / n;
   const float st_mean = (float)mean, st_inv = (float)(1.0 / sqrt(var + (double)eps));
-  if (t_l == 0) {
+  if ((tid & 63) == 0) {
     stats[co] = st_mean;
     stats[Cout + co] = st_inv;
     if (running_mean) running_mean[co] = (1.f - momentum) * running_mean[co] + momentum * st_mean;
@@ -91,55 +96,63 @@ __global__ __launch_bounds__(256) void g1_fwd_bn_kernel(const float* __restrict_
     bev[c_l] = (beta ? beta[co] : 0.f) - st_mean * al;
   }
   if (blockIdx.x == 0 && tid == 0 && nbt) nbt[0] += 1;
-  // y and a NHWC, 32 rows at a time through LDS: thread = (tap, channel) with the channel
-  // fastest (64-B runs of the 16 channels)
-  const int wc = tid & 15, wt = tid >> 4;
+  // y and a NHWC, 32 rows at a time through LDS: out thread = (row, tap, channel) with the
+  // channel fastest (64-B runs of the 16 channels)
+  const int wc = tid & 15, wt = (tid >> 4) & 15, wr = tid >> 8;
 #pragma unroll
-  for (int h = 0; h < B / 32; ++h) {  // unrolled: acc indices stay compile-time (registers)
-    const int b0 = 32 * h;
+  for (int h = 0; h < B / 32; ++h) {  // rows 32 h .. 32 h + 31: those of groups 4 h / (B / 32) ...
     __syncthreads();  // alv / bev written; the previous chunk's reads done
 #pragma unroll
-    for (int b = 0; b < 32; ++b) ys[(b * 16 + t_l) * 16 + c_l] = acc[b0 + b];
+    for (int j = 0; j < R; ++j) {
+      const int b = q * R + j;
+      if (b >= 32 * h && b < 32 * h + 32) ys[((b - 32 * h) * 16 + t_l) * 16 + c_l] = acc[j];
+    }
     __syncthreads();
     const float al = alv[wc], be = bev[wc];
-    for (int b = 0; b < 32; ++b) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int b = wr + 4 * i;
       const float v = ys[(b * 16 + wt) * 16 + wc];
-      const size_t o = ((size_t)(b0 + b) * 16 + wt) * Cout + co0 + wc;
+      const size_t o = ((size_t)(32 * h + b) * 16 + wt) * Cout + co0 + wc;
       y[o] = v;
       a[o] = act_fwd(v * al + be, act, alpha);
     }
   }
 }
 
-template <int B>
-__global__ __launch_bounds__(256) void g1_wgrad_kernel(const float* __restrict__ z, int Cin,
-                                                       const float* __restrict__ dy, int Cout, float* dw,
-                                                       int accumulate) {
-  extern __shared__ float zs[];  // [B][Cin]
-  const int tid = threadIdx.x, c_l = tid >> 4, t_l = tid & 15;
-  const int co0 = blockIdx.x * G1_CB, co = co0 + c_l;
-  for (int i = tid; i < B * Cin; i += 256) zs[i] = z[i];
-  float g[B];
-#pragma unroll
-  for (int b = 0; b < B; ++b) g[b] = dy[((size_t)b * 16 + t_l) * Cout + co];
+// thread = (channel c_l, ci quarter q, tap t): the quarter's Cin/4 outputs dW[ci][co][t] in
+// registers, b in order (each output's sum as the GEMM's K loop), z rows broadcast from LDS
+template <int B, int Cin>
+__global__ __launch_bounds__(1024) void g1_wgrad_kernel(const float* __restrict__ z, const float* __restrict__ dy,
+                                                        int Cout, float* dw, int accumulate) {
+  constexpr int PER = Cin / 4;
+  __shared__ __attribute__((aligned(16))) float zs[B * Cin];
+  const int tid = threadIdx.x, c_l = tid >> 6, q = (tid >> 4) & 3, t_l = tid & 15;
+  const int co = blockIdx.x * G1_CB + c_l;
+  for (int i = tid; i < B * Cin; i += 1024) zs[i] = z[i];
   __syncthreads();
+  const float* gp = dy + (size_t)t_l * Cout + co;  // dy[b][t][co], b stride 16 Cout
+  float s[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) s[k] = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float gb = gp[(size_t)b * 16 * Cout];
+    const float* zr = zs + b * Cin + q * PER;
+#pragma unroll
+    for (int k = 0; k < PER; k += 4) {
+      const float4 zz = *reinterpret_cast<const float4*>(zr + k);
+      s[k] = fmaf(zz.x, gb, s[k]);
+      s[k + 1] = fmaf(zz.y, gb, s[k + 1]);
+      s[k + 2] = fmaf(zz.z, gb, s[k + 2]);
+      s[k + 3] = fmaf(zz.w, gb, s[k + 3]);
+    }
+  }
   float* wp = dw + (size_t)co * 16 + t_l;
   const size_t wstride = (size_t)Cout * 16;
-  for (int ci = 0; ci < Cin; ci += 4) {  // b in order per output, as the GEMM's K loop
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int b = 0; b < B; ++b) {
-      const float4 zz = *reinterpret_cast<const float4*>(zs + b * Cin + ci);
-      s[0] = fmaf(zz.x, g[b], s[0]);
-      s[1] = fmaf(zz.y, g[b], s[1]);
-      s[2] = fmaf(zz.z, g[b], s[2]);
-      s[3] = fmaf(zz.w, g[b], s[3]);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float* d = wp + (size_t)(ci + k) * wstride;
-      *d = accumulate ? *d + s[k] : s[k];
-    }
+  for (int k = 0; k < PER; ++k) {
+    float* d = wp + (size_t)(q * PER + k) * wstride;
+    *d = accumulate ? *d + s[k] : s[k];
   }
 }
 
@@ -147,34 +160,42 @@ __global__ __launch_bounds__(256) void g1_wgrad_kernel(const float* __restrict__
 
 using namespace rgan;
 
+template <int B, int Cin>
+static void g1_fwd_launch(int Cout, const float* z, const float* w, const float* gamma, const float* beta, float eps,
+                          float momentum, float* rm, float* rv, long long* nbt, int act, float alpha, float* y,
+                          float* a, float* stats, hipStream_t s) {
+  const size_t lds = ((size_t)B * Cin + 32 * 256) * sizeof(float);
+  g1_fwd_bn_kernel<B, Cin><<<Cout / G1_CB, 1024, lds, s>>>(z, w, Cout, gamma, beta, eps, momentum, rm, rv, nbt, act,
+                                                           alpha, y, a, stats);
+}
+
 extern "C" int rgan_g1_fwd_bn(const float* z, int B, int Cin, const float* w, int Cout, const float* gamma,
                               const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                               long long* num_batches_tracked, int act, float act_alpha, float* y, float* a,
                               float* stats, void* stream) {
-  RGAN_REQUIRE(z && w && y && a && stats && (B == 32 || B == 64) && Cin >= 4 && Cin % 4 == 0 &&
+  RGAN_REQUIRE(z && w && y && a && stats && (B == 32 || B == 64) && (Cin == 64 || Cin == 128) &&
                Cout >= G1_CB && Cout % G1_CB == 0 && ((uintptr_t)z & 15) == 0);
-  const size_t lds = ((size_t)B * Cin + 32 * 256) * sizeof(float);
-  RGAN_REQUIRE(lds <= 64 * 1024);
   const hipStream_t s = (hipStream_t)stream;
-  if (B == 32)
-    g1_fwd_bn_kernel<32><<<Cout / G1_CB, 256, lds, s>>>(z, Cin, w, Cout, gamma, beta, eps, momentum, running_mean,
-                                                        running_var, num_batches_tracked, act, act_alpha, y, a, stats);
-  else
-    g1_fwd_bn_kernel<64><<<Cout / G1_CB, 256, lds, s>>>(z, Cin, w, Cout, gamma, beta, eps, momentum, running_mean,
-                                                        running_var, num_batches_tracked, act, act_alpha, y, a, stats);
+#define RGAN_G1F(BB, CC)                                                                                     \
+  g1_fwd_launch<BB, CC>(Cout, z, w, gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked, \
+                        act, act_alpha, y, a, stats, s)
+  if (B == 32) { if (Cin == 64) RGAN_G1F(32, 64); else RGAN_G1F(32, 128); }
+  else { if (Cin == 64) RGAN_G1F(64, 64); else RGAN_G1F(64, 128); }
+#undef RGAN_G1F
   RGAN_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int rgan_g1_wgrad(const float* z, int B, int Cin, const float* dy, int Cout, float* dw, int accumulate,
                              void* stream) {
-  RGAN_REQUIRE(z && dy && dw && (B == 32 || B == 64) && Cin >= 4 && Cin % 4 == 0 && Cout >= G1_CB &&
+  RGAN_REQUIRE(z && dy && dw && (B == 32 || B == 64) && (Cin == 64 || Cin == 128) && Cout >= G1_CB &&
                Cout % G1_CB == 0 && ((uintptr_t)z & 15) == 0);
-  const size_t lds = (size_t)B * Cin * sizeof(float);
-  RGAN_REQUIRE(lds <= 64 * 1024);
   const hipStream_t s = (hipStream_t)stream;
-  if (B == 32) g1_wgrad_kernel<32><<<Cout / G1_CB, 256, lds, s>>>(z, Cin, dy, Cout, dw, accumulate);
-  else g1_wgrad_kernel<64><<<Cout / G1_CB, 256, lds, s>>>(z, Cin, dy, Cout, dw, accumulate);
+  const dim3 grid(Cout / G1_CB);
+  if (B == 32 && Cin == 64) g1_wgrad_kernel<32, 64><<<grid, 1024, 0, s>>>(z, dy, Cout, dw, accumulate);
+  else if (B == 32) g1_wgrad_kernel<32, 128><<<grid, 1024, 0, s>>>(z, dy, Cout, dw, accumulate);
+  else if (Cin == 64) g1_wgrad_kernel<64, 64><<<grid, 1024, 0, s>>>(z, dy, Cout, dw, accumulate);
+  else g1_wgrad_kernel<64, 128><<<grid, 1024, 0, s>>>(z, dy, Cout, dw, accumulate);
   RGAN_CHECK_LAUNCH();
   return 0;
 }

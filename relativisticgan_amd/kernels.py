@@ -439,9 +439,8 @@ def conv_dgrad(dy, w, geom, x_shape, wscale=None, out=None, like=None, cache=Fal
 def g1_ok(x, w, geom):
     """G's first layer on its 1x1 input can run as rgan_g1_fwd_bn / rgan_g1_wgrad."""
     return (geom.transposed and geom.k == 4 and geom.stride == 1 and geom.pad == 0 and geom.upsample == 1
-            and x.dim() == 4 and tuple(x.shape[2:]) == (1, 1) and x.shape[0] in (32, 64) and x.shape[1] % 4 == 0
-            and w.shape[1] % 16 == 0 and w.is_contiguous() and x.is_contiguous() and x.data_ptr() % 16 == 0
-            and x.shape[0] * x.shape[1] * 4 + 32 * 256 * 4 <= 64 * 1024)
+            and x.dim() == 4 and tuple(x.shape[2:]) == (1, 1) and x.shape[0] in (32, 64) and x.shape[1] in (64, 128)
+            and w.shape[1] % 16 == 0 and w.is_contiguous() and x.is_contiguous() and x.data_ptr() % 16 == 0)
 
 
 def g1_fwd_bn(x, w, gamma, beta, eps, momentum, running_mean, running_var, num_batches_tracked, act, alpha,

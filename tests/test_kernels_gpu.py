@@ -970,7 +970,8 @@ def test_dgrad_post_op(K, case, mode):
                 assert _rel(u, v) < 1e-5, (case, act, nseg, k, _rel(u, v))
 
 
-@pytest.mark.parametrize("B,cin,cout,act", [(32, 128, 1024, "relu"), (64, 128, 512, "tanh"), (32, 100, 256, "relu")])
+@pytest.mark.parametrize("B,cin,cout,act", [(32, 128, 1024, "relu"), (64, 128, 512, "tanh"), (64, 64, 256, "relu"),
+                                         (32, 100, 256, "relu")])
 def test_first_layer_fused(K, B, cin, cout, act):
     """rgan_g1_fwd_bn (G's 1x1 -> 4x4 ConvTranspose2d + train-mode BatchNorm2d + act in one
     launch) and rgan_g1_wgrad vs torch fp64: y, a, batch statistics, running statistics and
