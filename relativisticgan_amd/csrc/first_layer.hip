@@ -5,8 +5,8 @@
 // On a 1x1 input the transposed conv is a plain product y[b][t][co] = sum_ci z[b][ci] *
 // W[ci][co][t] (t = 4 kh + kw) with M = B rows only: as an implicit GEMM it is one 128-row m
 // tile (B = 32 uses a quarter) over 4 k tiles, latency-bound (17 us at C1, 7 TF/s) and
-// followed by three BatchNorm launches.  Here ONE launch does all of it: a block owns 16
-// output channels x 16 taps and the whole batch (1024 threads: a thread = one column x a
+// followed by three BatchNorm launches.  Here ONE launch does all of it: a block owns 4
+// output channels x 16 taps and the whole batch (256 threads: a thread = one column x a
 // quarter of the batch rows), so each channel's B x 16 BatchNorm population is one wave's:
 //   1. y by fp32 FMA over ci in order (z staged in LDS, read as float4 broadcasts; a thread's
 //      W column read 64 entries at a time into registers -- one load latency per chunk);
@@ -22,7 +22,9 @@
 
 namespace rgan {
 
-constexpr int G1_CB = 16;   // channels per block (x 16 taps x 4 batch / ci groups = 1024 threads)
+constexpr int G1_CB = 4;    // channels per block (x 16 taps x 4 batch / ci groups = 256 threads):
+                            // Cout / 4 blocks, so even C1's 1024 channels spread over all CUs
+constexpr int G1_T = G1_CB * 64;
 constexpr int G1_WCH = 32;  // W entries of a thread's column held in registers at a time
 // instantiated for B (batch: a thread's rows live in registers) in {32, 64} and CIN (z size)
 // in {64, 128}
@@ -30,7 +32,7 @@ constexpr int G1_WCH = 32;  // W entries of a thread's column held in registers 
 // thread = (channel c_l, group q, tap t): tid = 64 c_l + 16 q + t -- a channel's 64 threads are
 // one wave (its BatchNorm population B x 16 sits in that wave's registers)
 template <int B, int Cin>
-__global__ __launch_bounds__(1024) void g1_fwd_bn_kernel(const float* __restrict__ z,
+__global__ __launch_bounds__(G1_T) void g1_fwd_bn_kernel(const float* __restrict__ z,
                                                          const float* __restrict__ w, int Cout,
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, float eps, float momentum,
@@ -40,11 +42,11 @@ __global__ __launch_bounds__(1024) void g1_fwd_bn_kernel(const float* __restrict
   constexpr int R = B / 4;                // batch rows per thread: q R .. q R + R - 1
   extern __shared__ float lds[];
   float* zs = lds;                        // [B][Cin]
-  float* ys = lds + (size_t)B * Cin;      // [32][16 taps][16 channels]: output staging
+  float* ys = lds + (size_t)B * Cin;      // [32][16 taps][G1_CB channels]: output staging
   __shared__ float alv[G1_CB], bev[G1_CB];
   const int tid = threadIdx.x, c_l = tid >> 6, q = (tid >> 4) & 3, t_l = tid & 15;
   const int co0 = blockIdx.x * G1_CB, co = co0 + c_l;
-  for (int i = tid; i < B * Cin; i += 1024) zs[i] = z[i];
+  for (int i = tid; i < B * Cin; i += G1_T) zs[i] = z[i];
   __syncthreads();
   const float* wp = w + (size_t)co * 16 + t_l;  // W[ci][co][t]: the 16 taps contiguous
   const size_t wstride = (size_t)Cout * 16;
@@ -97,22 +99,23 @@ __global__ __launch_bounds__(1024) void g1_fwd_bn_kernel(const float* __restrict
   }
   if (blockIdx.x == 0 && tid == 0 && nbt) nbt[0] += 1;
   // y and a NHWC, 32 rows at a time through LDS: out thread = (row, tap, channel) with the
-  // channel fastest (64-B runs of the 16 channels)
-  const int wc = tid & 15, wt = (tid >> 4) & 15, wr = tid >> 8;
+  // channel fastest (G1_CB-channel runs)
+  const int wc = tid % G1_CB, wt = (tid / G1_CB) & 15, wr = tid / (16 * G1_CB);
+  constexpr int WROWS = G1_T / (16 * G1_CB);  // rows per pass
 #pragma unroll
   for (int h = 0; h < B / 32; ++h) {  // rows 32 h .. 32 h + 31: those of groups 4 h / (B / 32) ...
     __syncthreads();  // alv / bev written; the previous chunk's reads done
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const int b = q * R + j;
-      if (b >= 32 * h && b < 32 * h + 32) ys[((b - 32 * h) * 16 + t_l) * 16 + c_l] = acc[j];
+      if (b >= 32 * h && b < 32 * h + 32) ys[((b - 32 * h) * 16 + t_l) * G1_CB + c_l] = acc[j];
     }
     __syncthreads();
     const float al = alv[wc], be = bev[wc];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int b = wr + 4 * i;
-      const float v = ys[(b * 16 + wt) * 16 + wc];
+    for (int i = 0; i < 32 / WROWS; ++i) {
+      const int b = wr + WROWS * i;
+      const float v = ys[(b * 16 + wt) * G1_CB + wc];
       const size_t o = ((size_t)(32 * h + b) * 16 + wt) * Cout + co0 + wc;
       y[o] = v;
       a[o] = act_fwd(v * al + be, act, alpha);
@@ -123,13 +126,13 @@ __global__ __launch_bounds__(1024) void g1_fwd_bn_kernel(const float* __restrict
 // thread = (channel c_l, ci quarter q, tap t): the quarter's Cin/4 outputs dW[ci][co][t] in
 // registers, b in order (each output's sum as the GEMM's K loop), z rows broadcast from LDS
 template <int B, int Cin>
-__global__ __launch_bounds__(1024) void g1_wgrad_kernel(const float* __restrict__ z, const float* __restrict__ dy,
+__global__ __launch_bounds__(G1_T) void g1_wgrad_kernel(const float* __restrict__ z, const float* __restrict__ dy,
                                                         int Cout, float* dw, int accumulate) {
   constexpr int PER = Cin / 4;
   __shared__ __attribute__((aligned(16))) float zs[B * Cin];
   const int tid = threadIdx.x, c_l = tid >> 6, q = (tid >> 4) & 3, t_l = tid & 15;
   const int co = blockIdx.x * G1_CB + c_l;
-  for (int i = tid; i < B * Cin; i += 1024) zs[i] = z[i];
+  for (int i = tid; i < B * Cin; i += G1_T) zs[i] = z[i];
   __syncthreads();
   const float* gp = dy + (size_t)t_l * Cout + co;  // dy[b][t][co], b stride 16 Cout
   float s[PER];
@@ -164,8 +167,8 @@ template <int B, int Cin>
 static void g1_fwd_launch(int Cout, const float* z, const float* w, const float* gamma, const float* beta, float eps,
                           float momentum, float* rm, float* rv, long long* nbt, int act, float alpha, float* y,
                           float* a, float* stats, hipStream_t s) {
-  const size_t lds = ((size_t)B * Cin + 32 * 256) * sizeof(float);
-  g1_fwd_bn_kernel<B, Cin><<<Cout / G1_CB, 1024, lds, s>>>(z, w, Cout, gamma, beta, eps, momentum, rm, rv, nbt, act,
+  const size_t lds = ((size_t)B * Cin + 32 * 16 * G1_CB) * sizeof(float);
+  g1_fwd_bn_kernel<B, Cin><<<Cout / G1_CB, G1_T, lds, s>>>(z, w, Cout, gamma, beta, eps, momentum, rm, rv, nbt, act,
                                                            alpha, y, a, stats);
 }
 
@@ -192,10 +195,10 @@ extern "C" int rgan_g1_wgrad(const float* z, int B, int Cin, const float* dy, in
                Cout % G1_CB == 0 && ((uintptr_t)z & 15) == 0);
   const hipStream_t s = (hipStream_t)stream;
   const dim3 grid(Cout / G1_CB);
-  if (B == 32 && Cin == 64) g1_wgrad_kernel<32, 64><<<grid, 1024, 0, s>>>(z, dy, Cout, dw, accumulate);
-  else if (B == 32) g1_wgrad_kernel<32, 128><<<grid, 1024, 0, s>>>(z, dy, Cout, dw, accumulate);
-  else if (Cin == 64) g1_wgrad_kernel<64, 64><<<grid, 1024, 0, s>>>(z, dy, Cout, dw, accumulate);
-  else g1_wgrad_kernel<64, 128><<<grid, 1024, 0, s>>>(z, dy, Cout, dw, accumulate);
+  if (B == 32 && Cin == 64) g1_wgrad_kernel<32, 64><<<grid, G1_T, 0, s>>>(z, dy, Cout, dw, accumulate);
+  else if (B == 32) g1_wgrad_kernel<32, 128><<<grid, G1_T, 0, s>>>(z, dy, Cout, dw, accumulate);
+  else if (Cin == 64) g1_wgrad_kernel<64, 64><<<grid, G1_T, 0, s>>>(z, dy, Cout, dw, accumulate);
+  else g1_wgrad_kernel<64, 128><<<grid, G1_T, 0, s>>>(z, dy, Cout, dw, accumulate);
   RGAN_CHECK_LAUNCH();
   return 0;
 }
