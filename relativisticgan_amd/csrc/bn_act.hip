@@ -440,8 +440,14 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
 
 // apply-pass grid: pixel blocks per channel group, each thread at least `min_iter` pixel
 // rows (round-1 sweep with tools/bn_micro.py: 4096 blocks, 4 rows)
+#ifndef RGAN_BN_APPLY_BLOCKS  // (variant builds sweep these: tools/build_variant.py)
+#define RGAN_BN_APPLY_BLOCKS 4096
+#endif
+#ifndef RGAN_BN_APPLY_MIN_ITER
+#define RGAN_BN_APPLY_MIN_ITER 4
+#endif
 static dim3 apply_grid(const BnGeo& g, long long P) {
-  constexpr long long blocks = 4096, min_iter = 4;
+  constexpr long long blocks = RGAN_BN_APPLY_BLOCKS, min_iter = RGAN_BN_APPLY_MIN_ITER;
   const long long rb = std::max<long long>(
       1, std::min<long long>((P + g.rp * min_iter - 1) / (g.rp * min_iter), std::max<long long>(1, blocks / g.cgroups)));
   return dim3(g.cgroups, (unsigned)rb);
