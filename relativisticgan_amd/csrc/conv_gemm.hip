@@ -1102,6 +1102,11 @@ template <int MODE>
 __global__ __launch_bounds__(256, 2) void gemm_post(GemmArgs g) {
   gemm_body<MODE, 128, 128, 2, 2, true, true, true, false, true>(g);
 }
+// ... and with the opt-in fp32-on-bf16x6 products (rgan_set_gemm_emulation)
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void gemm_post_bf16x6(GemmArgs g) {
+  gemm_body<MODE, 128, 128, 2, 2, true, true, true, true, true>(g);
+}
 
 // Opt-in (rgan_set_gemm_emulation): the FAST 128 x 128 CONV / CONVT2 GEMM with fp32 products
 // emulated on the bf16 MFMA (see gemm_body's EMU path).  Its own symbol, reported as such.
@@ -2962,7 +2967,8 @@ template <int MODE>
 static void launch_mode(const Plan& p, dim3 grid, hipStream_t s) {
   if constexpr (MODE == MODE_CONV || MODE == MODE_CONVT2) {
     if (p.g.pmode && p.g.splits == 1) {  // post_ok: FAST 128x128 (the post-op in the epilogue)
-      gemm_post<MODE><<<grid, 256, 0, s>>>(p.g);
+      if (plan_emu(p)) gemm_post_bf16x6<MODE><<<grid, 256, 0, s>>>(p.g);
+      else gemm_post<MODE><<<grid, 256, 0, s>>>(p.g);
       return;
     }
     if (plan_emu(p)) {
@@ -2994,7 +3000,7 @@ static std::vector<ProfRec> g_recs;
 static std::vector<std::string> g_kernel_names;
 static double g_cur_flops = 0.0;
 
-constexpr int N_KERNEL_IDS = 55;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in + 2 bf16x6 + 2 post
+constexpr int N_KERNEL_IDS = 57;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in + 2 bf16x6 + 2 post + 2 post bf16x6
 
 static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
   const int id = mode == MODE_NARROW_T ? 45
@@ -3031,6 +3037,8 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
     g_kernel_names[52] = "void rgan::gemm_bf16x6<1>(rgan::GemmArgs)";
     g_kernel_names[53] = "void rgan::gemm_post<0>(rgan::GemmArgs)";
     g_kernel_names[54] = "void rgan::gemm_post<1>(rgan::GemmArgs)";
+    g_kernel_names[55] = "void rgan::gemm_post_bf16x6<0>(rgan::GemmArgs)";
+    g_kernel_names[56] = "void rgan::gemm_post_bf16x6<1>(rgan::GemmArgs)";
   }
   return id;
 }
@@ -3257,7 +3265,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     rec.flops = g_cur_flops;
     rec.kid = kernel_id(p.mode, p.cfg, p.av, p.bv, p.fast);
     if (plan_emu(p)) rec.kid = 51 + p.mode;
-    if (p.g.pmode && p.g.splits == 1) rec.kid = 53 + p.mode;
+    if (p.g.pmode && p.g.splits == 1) rec.kid = (plan_emu(p) ? 55 : 53) + p.mode;
     hipEventRecord(rec.a, s);
   }
   switch (p.mode) {

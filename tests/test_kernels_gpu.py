@@ -1011,3 +1011,34 @@ def test_first_layer_fused(K, B, cin, cout, act):
     acc = base.clone()
     K.g1_wgrad(z, dy, tuple(w.shape), out=acc)
     assert _rel(acc - base, dw64) < 1e-5
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_dgrad_post_op_emulated(K, mode):
+    """The post-op GEMM on the opt-in fp32-on-bf16x6 products (gemm_post_bf16x6) == the fp32
+    post-op GEMM within the emulation's accuracy (unsplit CONVT2 data gradient)."""
+    from relativisticgan_amd.kernels import ConvGeom, Post
+    torch.manual_seed(31)
+    g = ConvGeom(4, 2, 1, False)
+    B, cin, cout, H = 64, 128, 256, 32
+    w = torch.randn(cout, cin, 4, 4, device=DEV) * 0.05
+    dy = _nhwc(torch.randn(B, cout, H // 2, H // 2, device=DEV))
+    xs = (B, cin, H, H)
+    x = _nhwc(torch.randn(xs, device=DEV))
+    if mode == 1:
+        mk = lambda: Post(1, "lrelu", 0.2, _nhwc(F.leaky_relu(x, 0.2)))  # noqa: E731
+    else:
+        st = torch.cat([torch.full((1, cin), 0.1, device=DEV), torch.full((1, cin), 1.3, device=DEV)], 1)
+        mk = lambda: Post(2, "relu", 0.0, x, stats=st, nseg=1)  # noqa: E731
+    p32 = mk()
+    want = K.conv_dgrad(dy, w, g, xs, post=p32)
+    prev = K.set_gemm_emulation(True)
+    try:
+        pe = mk()
+        got = K.conv_dgrad(dy, w, g, xs, post=pe)
+    finally:
+        K.set_gemm_emulation(prev)
+    assert p32.fused and pe.fused
+    assert _rel(got, want) < 2e-6, _rel(got, want)
+    if mode == 2:
+        assert _rel(pe.part, p32.part) < 2e-6

@@ -1,0 +1,3 @@
+set -o pipefail
+bash tools/gpu_cmd_k.sh || exit 1
+tools/gpu_session.sh r3final prof=C1 prof=C3 prof=C2 prof=C3h32 prof=C4 prof=C4p prof=C5
