@@ -9,13 +9,17 @@ backward only scales them by the upstream gradient.  Under data parallelism the
 batch means are global: the head runs in three phases with two tiny
 all-reduces in between.
 """
+import weakref
+
 import torch
 
 from . import dp
 from . import kernels as K
 
 
-_UNIT_SEEDS = {}  # data_ptr -> tensor: device scalars 1.0 used as backward seeds (Trainer._backward)
+# data_ptr -> tensor: device scalars 1.0 used as backward seeds (Trainer._backward); weak, so a
+# dead seed's entry goes with it (its address may be reused by another tensor)
+_UNIT_SEEDS = weakref.WeakValueDictionary()
 
 
 def unit_seed(device, dtype=torch.float32):

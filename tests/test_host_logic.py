@@ -1,0 +1,61 @@
+"""Host-side logic of the round-3 fusions, on the CPU (no kernel launches).
+
+* loss heads: the unit backward seed registry (a dead seed's address must not stay "unit");
+* autograd.LayerLink: the kernels.Post it builds for the lower layer (rows of the gradient
+  segment, per-segment statistics rows, act-only vs BatchNorm mode);
+* ConvLayerFn: forward inputs == backward outputs (autograd requires one gradient slot per input);
+* --rgan_batch_G is a CLI flag with the reference's argparse bool convention.
+"""
+import gc
+import inspect
+
+import torch
+
+from relativisticgan_amd import autograd as AG
+from relativisticgan_amd import losses
+
+
+def test_unit_seed_registry():
+    one = losses.unit_seed("cpu")
+    assert losses._is_unit(one)
+    other = torch.ones((), dtype=torch.float32)
+    assert not losses._is_unit(other)
+    ptr = one.data_ptr()
+    del one
+    gc.collect()
+    assert ptr not in losses._UNIT_SEEDS
+
+
+def test_layer_link_post_rows_and_segments():
+    link = AG.LayerLink()
+    assert link.post(4, 1) is None  # nothing recorded: no post-op
+    y = torch.randn(8, 16, 4, 4).contiguous(memory_format=torch.channels_last)
+    stats = torch.randn(2, 32)  # two batch segments' (mean, invstd)
+    link.mode, link.act, link.alpha, link.x, link.stats = 2, "lrelu", 0.2, y, stats
+    link.gamma, link.beta, link.segs = torch.ones(16), torch.zeros(16), 2
+    p = link.post(4, 1)  # the G step's restricted backward: first segment only
+    assert p.mode == 2 and p.nseg == 1 and p.x.shape[0] == 4 and p.x.data_ptr() == y.data_ptr()
+    assert torch.equal(p.stats, stats[:1])
+    p2 = link.post(8, 2)  # the batched D step: both segments
+    assert p2.nseg == 2 and torch.equal(p2.stats, stats)
+    link1 = AG.LayerLink()
+    a = torch.randn(8, 16, 4, 4)
+    link1.mode, link1.act, link1.alpha, link1.x = 1, "relu", 0.0, a
+    p3 = link1.post(8, 2)
+    assert p3.mode == 1 and p3.stats is None and p3.x.shape[0] == 8
+
+
+def test_conv_layer_fn_arity():
+    n_in = len(inspect.signature(AG.ConvLayerFn.forward).parameters) - 1  # minus ctx
+    src = inspect.getsource(AG.ConvLayerFn)
+    # every return of backward / _create_graph_backward hands back one slot per forward input
+    assert f"[None] * {n_in}" in src
+    tail = ", ".join(["None"] * (n_in - 5))
+    assert f"return dx, dw, db, dgamma, dbeta, {tail}\n" in src
+
+
+def test_batch_G_flag():
+    from relativisticgan_amd.config import make_param, parse
+    assert make_param().rgan_batch_G is None
+    p = parse(["--rgan_batch_G", "False"])
+    assert p.rgan_batch_G is False
