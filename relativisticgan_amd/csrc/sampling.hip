@@ -3,8 +3,8 @@
 // numpy.random.choice(N, B, replace=False)), as counter-based draws on the GPU.
 //
 // Philox-4x32-10 keyed by the run's seed; the 64-bit counter lives on the device and every
-// call advances it by the numbers it consumed (a trailing one-thread launch after a fill,
-// the sampling wave itself for the indices), so a call
+// call advances it by the numbers it consumed (the one-block fill of a z / u draw or the
+// sampling wave itself; a trailing one-thread launch after a large fill), so a call
 // captured in a HIP graph draws fresh numbers at every replay with no host involvement.
 // Every rank of a data-parallel run holds the same seed and counter and draws the global
 // batch (each keeps its shard), like torch's device generator did here before.
@@ -35,8 +35,10 @@ __device__ __forceinline__ u32x4s philox(unsigned long long ctr, unsigned long l
 __device__ __forceinline__ float u01(uint32_t v) { return ((float)(v >> 8) + 1.f) * (1.f / 16777216.f); }
 
 // kind 0: N(0, 1) (Box-Muller on the four words: two normals per pair); kind 1: U[0, 1)
+// advance != 0 (one-block launches): the block also moves the counter on by `advance`
+// after every thread has read it (the barrier orders the reads before thread 0's store)
 __global__ __launch_bounds__(256) void rng_fill(float* out, long long n, int kind, unsigned long long seed,
-                                                const unsigned long long* counter) {
+                                                unsigned long long* counter, unsigned long long advance) {
   const unsigned long long base = counter[0];
   for (long long q = blockIdx.x * 256LL + threadIdx.x; 4 * q < n; q += (long long)gridDim.x * 256) {
     const u32x4s r = philox(base + (unsigned long long)q, seed);
@@ -54,6 +56,10 @@ __global__ __launch_bounds__(256) void rng_fill(float* out, long long n, int kin
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       if (4 * q + i < n) out[4 * q + i] = v[i];
+  }
+  if (advance) {
+    __syncthreads();
+    if (threadIdx.x == 0) counter[0] = base + advance;
   }
 }
 
@@ -145,7 +151,12 @@ extern "C" int rgan_rng_fill(float* out, long long n, int kind, unsigned long lo
   if (n == 0) return 0;
   hipStream_t s = (hipStream_t)stream;
   const long long quads = (n + 3) / 4;
-  rng_fill<<<(unsigned)std::min<long long>((quads + 255) / 256, 2048), 256, 0, s>>>(out, n, kind, seed, counter);
+  if (quads <= 16 * 256) {  // z / u draws: one block that also advances the counter (one launch)
+    rng_fill<<<1, 256, 0, s>>>(out, n, kind, seed, counter, (unsigned long long)quads);
+    RGAN_CHECK_LAUNCH();
+    return 0;
+  }
+  rng_fill<<<(unsigned)std::min<long long>((quads + 255) / 256, 2048), 256, 0, s>>>(out, n, kind, seed, counter, 0ull);
   RGAN_CHECK_LAUNCH();
   rng_advance<<<1, 1, 0, s>>>(counter, (unsigned long long)quads);
   RGAN_CHECK_LAUNCH();

@@ -838,6 +838,13 @@ def test_device_rng(K):
     assert big.unique().numel() == 300 and big.min().item() >= 0 and big.max().item() < 5000
     assert torch.equal(b.normal((400, 1000)), z)  # same seed, same counter: same draws
     assert not torch.equal(b.normal((400, 1000)), z)  # the counter moved
+    # z-sized draws run as one block that advances the counter itself: the same numbers as
+    # the multi-block fill from the same counter, and the counter moved by the quads consumed
+    c, d = K.DeviceRNG(9, DEV), K.DeviceRNG(9, DEV)
+    small = c.normal((32, 128))
+    assert torch.equal(small.flatten(), d.normal((20000,))[:4096])
+    assert int(c.counter.item()) == 1024 and int(d.counter.item()) == 5000
+    assert not torch.equal(c.normal((32, 128)), small)
     counts = torch.zeros(20, device=DEV)
     for _ in range(200):
         counts.index_add_(0, a.choice(20, 5), torch.ones(5, device=DEV))
