@@ -39,14 +39,16 @@ __global__ __launch_bounds__(G1_T) void g1_fwd_bn_kernel(const float* __restrict
                                                          float* running_mean, float* running_var, long long* nbt,
                                                          int act, float alpha, float* __restrict__ y,
                                                          float* __restrict__ a, float* __restrict__ stats) {
-  constexpr int R = B / 4;                // batch rows per thread: q R .. q R + R - 1
+  constexpr int R = B / 4;                // batch rows per thread: 4 j + q, j < R
+  constexpr int ZS = Cin + 4;             // z row stride in LDS: the 4 groups' rows (consecutive
+                                          // b) sit 16 B apart mod 256 -- conflict-free b128 reads
   extern __shared__ float lds[];
-  float* zs = lds;                        // [B][Cin]
-  float* ys = lds + (size_t)B * Cin;      // [32][16 taps][G1_CB channels]: output staging
+  float* zs = lds;                        // [B][ZS]
+  float* ys = lds + (size_t)B * ZS;       // [32][16 taps][G1_CB channels]: output staging
   __shared__ float alv[G1_CB], bev[G1_CB];
   const int tid = threadIdx.x, c_l = tid >> 6, q = (tid >> 4) & 3, t_l = tid & 15;
   const int co0 = blockIdx.x * G1_CB, co = co0 + c_l;
-  for (int i = tid; i < B * Cin; i += G1_T) zs[i] = z[i];
+  for (int i = tid; i < B * Cin; i += G1_T) zs[(i / Cin) * ZS + i % Cin] = z[i];
   __syncthreads();
   const float* wp = w + (size_t)co * 16 + t_l;  // W[ci][co][t]: the 16 taps contiguous
   const size_t wstride = (size_t)Cout * 16;
@@ -63,7 +65,7 @@ __global__ __launch_bounds__(G1_T) void g1_fwd_bn_kernel(const float* __restrict
     for (int k = 0; k < G1_WCH; k += 4) {
 #pragma unroll
       for (int j = 0; j < R; ++j) {  // ci in order per output
-        const float4 zz = *reinterpret_cast<const float4*>(zs + (q * R + j) * Cin + c0 + k);
+        const float4 zz = *reinterpret_cast<const float4*>(zs + (4 * j + q) * ZS + c0 + k);
         acc[j] = fmaf(zz.w, wv[k + 3], fmaf(zz.z, wv[k + 2], fmaf(zz.y, wv[k + 1], fmaf(zz.x, wv[k], acc[j]))));
       }
     }
@@ -107,7 +109,7 @@ __global__ __launch_bounds__(G1_T) void g1_fwd_bn_kernel(const float* __restrict
     __syncthreads();  // alv / bev written; the previous chunk's reads done
 #pragma unroll
     for (int j = 0; j < R; ++j) {
-      const int b = q * R + j;
+      const int b = 4 * j + q;
       if (b >= 32 * h && b < 32 * h + 32) ys[((b - 32 * h) * 16 + t_l) * G1_CB + c_l] = acc[j];
     }
     __syncthreads();
@@ -123,40 +125,46 @@ __global__ __launch_bounds__(G1_T) void g1_fwd_bn_kernel(const float* __restrict
   }
 }
 
-// thread = (channel c_l, ci quarter q, tap t): the quarter's Cin/4 outputs dW[ci][co][t] in
-// registers, b in order (each output's sum as the GEMM's K loop), z rows broadcast from LDS
+// thread = (channel c_l, ci group q, tap t): the group's Cin/4 outputs dW[ci][co][t] in
+// registers (ci quads q, q + 4, q + 8, ...: the 4 groups read adjacent float4 of a z row, no
+// bank conflict), b in order (each output's sum as the GEMM's K loop)
 template <int B, int Cin>
 __global__ __launch_bounds__(G1_T) void g1_wgrad_kernel(const float* __restrict__ z, const float* __restrict__ dy,
                                                         int Cout, float* dw, int accumulate) {
-  constexpr int PER = Cin / 4;
+  constexpr int NQ = Cin / 16;  // ci quads per group
   __shared__ __attribute__((aligned(16))) float zs[B * Cin];
   const int tid = threadIdx.x, c_l = tid >> 6, q = (tid >> 4) & 3, t_l = tid & 15;
   const int co = blockIdx.x * G1_CB + c_l;
   for (int i = tid; i < B * Cin; i += G1_T) zs[i] = z[i];
   __syncthreads();
   const float* gp = dy + (size_t)t_l * Cout + co;  // dy[b][t][co], b stride 16 Cout
-  float s[PER];
+  float s[NQ][4];
 #pragma unroll
-  for (int k = 0; k < PER; ++k) s[k] = 0.f;
+  for (int k = 0; k < NQ; ++k)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s[k][i] = 0.f;
+#pragma unroll 2
   for (int b = 0; b < B; ++b) {
     const float gb = gp[(size_t)b * 16 * Cout];
-    const float* zr = zs + b * Cin + q * PER;
+    const float* zr = zs + b * Cin + 4 * q;
 #pragma unroll
-    for (int k = 0; k < PER; k += 4) {
-      const float4 zz = *reinterpret_cast<const float4*>(zr + k);
-      s[k] = fmaf(zz.x, gb, s[k]);
-      s[k + 1] = fmaf(zz.y, gb, s[k + 1]);
-      s[k + 2] = fmaf(zz.z, gb, s[k + 2]);
-      s[k + 3] = fmaf(zz.w, gb, s[k + 3]);
+    for (int k = 0; k < NQ; ++k) {
+      const float4 zz = *reinterpret_cast<const float4*>(zr + 16 * k);
+      s[k][0] = fmaf(zz.x, gb, s[k][0]);
+      s[k][1] = fmaf(zz.y, gb, s[k][1]);
+      s[k][2] = fmaf(zz.z, gb, s[k][2]);
+      s[k][3] = fmaf(zz.w, gb, s[k][3]);
     }
   }
   float* wp = dw + (size_t)co * 16 + t_l;
   const size_t wstride = (size_t)Cout * 16;
 #pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    float* d = wp + (size_t)(q * PER + k) * wstride;
-    *d = accumulate ? *d + s[k] : s[k];
-  }
+  for (int k = 0; k < NQ; ++k)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float* d = wp + (size_t)(16 * k + 4 * q + i) * wstride;
+      *d = accumulate ? *d + s[k][i] : s[k][i];
+    }
 }
 
 }  // namespace rgan
@@ -167,7 +175,7 @@ template <int B, int Cin>
 static void g1_fwd_launch(int Cout, const float* z, const float* w, const float* gamma, const float* beta, float eps,
                           float momentum, float* rm, float* rv, long long* nbt, int act, float alpha, float* y,
                           float* a, float* stats, hipStream_t s) {
-  const size_t lds = ((size_t)B * Cin + 32 * 16 * G1_CB) * sizeof(float);
+  const size_t lds = ((size_t)B * (Cin + 4) + 32 * 16 * G1_CB) * sizeof(float);
   g1_fwd_bn_kernel<B, Cin><<<Cout / G1_CB, G1_T, lds, s>>>(z, w, Cout, gamma, beta, eps, momentum, rm, rv, nbt, act,
                                                            alpha, y, a, stats);
 }
