@@ -189,14 +189,18 @@ __device__ __forceinline__ AdamConst adam_const(const double* hyper, const float
   return k;
 }
 
+// Every rounding spelled out (explicit fmaf / _rn intrinsics: no contraction left to the
+// compiler, so every kernel inlining this rounds alike), as torch's CPU kernels round:
+// lerp = fma(w, end - m, m) or fma(w - 1, end - m, end) (ATen lerp_vec), addcmul =
+// fma(value * g, g, v), addcdiv = p + (value * m) / denom (checked elementwise against
+// torch.optim.Adam on the CPU).
 __device__ __forceinline__ void adam_elem(const AdamConst& k, float g, float& p, float& m, float& v) {
-  if (k.has_wd) g = g + k.fwd * p;
-  const float diff = g - m;
-  m = k.w < 0.5f ? m + k.w * diff : g - diff * (1.f - k.w);
-  v = v * k.fb2;
-  v = v + k.f1mb2 * g * g;
-  const float denom = sqrtf(v) / k.bc2s + k.feps;
-  p = p + k.neg_step * (m / denom);
+  if (k.has_wd) g = fmaf(k.fwd, p, g);
+  const float diff = __fsub_rn(g, m);
+  m = k.w < 0.5f ? fmaf(k.w, diff, m) : fmaf(k.w - 1.f, diff, g);
+  v = fmaf(__fmul_rn(k.f1mb2, g), g, __fmul_rn(v, k.fb2));
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), k.bc2s), k.feps);
+  p = __fadd_rn(p, __fdiv_rn(__fmul_rn(k.neg_step, m), denom));
 }
 
 }  // namespace rgan

@@ -1224,6 +1224,50 @@ __global__ __launch_bounds__(256) void splitk_reduce(GemmArgs g, FastDiv fdiv, u
   }
 }
 
+// RED_ANY shape with few outputs and many splits (the 1x1 patch GEMMs' weight gradients: a
+// 128 x 64 output, split-K 512 ways): one thread per output would be a 512-long chain on
+// 32 blocks.  Here a block = 16 outputs x 16 split lanes; lane l sums splits l, l + 16, ...
+// in order (4 loads in flight), then a fixed LDS tree adds the 16 lane sums (deterministic;
+// a different association than red_sum's split order, the same set of fp32 partials).
+constexpr int REDW_OUT = 16, REDW_LANES = 16;
+template <int MODE>
+__global__ __launch_bounds__(256) void splitk_reduce_wide(GemmArgs g, FastDiv fdiv, uint32_t per_phase) {
+  __shared__ float sh[REDW_LANES][REDW_OUT + 1];
+  const int phase = blockIdx.y, ob = threadIdx.x % REDW_OUT, l = threadIdx.x / REDW_OUT;
+  const size_t MN = (size_t)g.M * g.N;
+  const uint32_t idx = blockIdx.x * REDW_OUT + ob;
+  const bool live = idx < per_phase;
+  const float* s = g.slab + (size_t)phase * g.splits * MN + (live ? idx : 0);  // idx = m N + n
+  float acc = 0.f;
+  if (live) {
+    int sp = l;
+    for (; sp + 3 * REDW_LANES < g.splits; sp += 4 * REDW_LANES) {
+      float t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) t[u] = s[(size_t)(sp + u * REDW_LANES) * MN];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc += t[u];
+    }
+    for (; sp < g.splits; sp += REDW_LANES) acc += s[(size_t)sp * MN];
+  }
+  sh[l][ob] = acc;
+  __syncthreads();
+  for (int h = REDW_LANES / 2; h > 0; h >>= 1) {
+    if (l < h) sh[l][ob] += sh[l + h][ob];
+    __syncthreads();
+  }
+  if (l == 0 && live) {
+    const uint32_t m = fdiv.div(idx);  // fdiv = N
+    const int n = (int)(idx - m * fdiv.d);
+    const float wsc = g.wscale ? g.wscale[0] : 1.f;
+    const long long ooff = row_offset(g.out, (int)m, MODE == MODE_CONVT2 ? phase : 0) + col_offset(g.out, n);
+    float* dst = g.C + ooff;
+    float o = red_epi(g, sh[0][ob], wsc, n);
+    if (MODE != MODE_WGRAD && g.pmode == 1) o *= act_grad_from_out(g.px[ooff], g.pact, g.palpha);
+    *dst = g.accum ? *dst + o : o;
+  }
+}
+
 // Split-K reduce of a BatchNorm layer's conv forward with the batch statistics fused in:
 // the same rows the RED_VEC reduce writes (same split order, bitwise the same values), plus
 // the (sum y, sum y^2) of every 64-row segment of every channel in double -- the layout the
@@ -2356,13 +2400,23 @@ __device__ __forceinline__ void apk_scatter(const AdamPackT& t, long long e, flo
   }
 }
 
+__device__ __forceinline__ void adam_pack_flat(const AdamPackBatch& b, const AdamPackTensor& X, const AdamConst& k,
+                                               int local, int tid);
+
+// The call's step-counter increment rides on its last launch: every block computes with
+// step + 1 (read at entry), and the last block to arrive (a device-wide ticket) stores it --
+// after every block of every launch of the call has read the old value (no separate
+// increment launch ahead of the step).
+__device__ unsigned int g_adam_arrive = 0;
+
 __global__ __launch_bounds__(AP_THREADS) void adam_pack_kernel(AdamPackBatch b, const double* __restrict__ hyper,
-                                                               const float* __restrict__ step) {
+                                                               float* step, int bump) {
   __shared__ float T[32 * AP_TLD];  // brick [a][b][tap]: b stride 17, a stride 548 (4 consecutive a: distinct banks)
   int j = 0;
   while (j + 1 < b.cnt && (int)blockIdx.x >= b.first[j + 1]) ++j;
   const AdamPackTensor X = b.t[j];
-  const AdamConst k = adam_const(hyper, step);
+  const float st1 = step[0] + 1.f;
+  const AdamConst k = adam_const(hyper, &st1);
   const int local = (int)blockIdx.x - b.first[j], tid = threadIdx.x;
   if (X.brick) {
     const AdamPackT& t0 = b.pk[X.pk0];
@@ -2413,8 +2467,20 @@ __global__ __launch_bounds__(AP_THREADS) void adam_pack_kernel(AdamPackBatch b, 
         *reinterpret_cast<float4*>(t.out + dst) = v4;
       }
     }
-    return;
+  } else {
+    adam_pack_flat(b, X, k, local, tid);
   }
+  if (bump) {
+    __syncthreads();  // every wave of this block has read step[0]
+    if (threadIdx.x == 0 && atomicAdd(&g_adam_arrive, 1u) == gridDim.x - 1) {
+      step[0] = st1;
+      atomicExch(&g_adam_arrive, 0u);
+    }
+  }
+}
+
+__device__ __forceinline__ void adam_pack_flat(const AdamPackBatch& b, const AdamPackTensor& X, const AdamConst& k,
+                                               int local, int tid) {
   const long long e0 = (long long)local * AP_FLAT, e1 = min(X.n, e0 + AP_FLAT);
   const bool vec = (X.n & 3) == 0 && ((((uintptr_t)X.p | (uintptr_t)X.g | (uintptr_t)X.m | (uintptr_t)X.v) & 15) == 0);
   if (vec) {
@@ -3311,8 +3377,18 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
       RGAN_CHECK_LAUNCH();
       return 0;
     }
-    const dim3 rgrid((unsigned)std::min<uint32_t>((per + 255) / 256, 8192), p.phases);
     const FastDiv fd(d);
+    if (kind == RED_ANY && g.splits >= 4 * REDW_LANES && per <= 65536) {  // few outputs, long chains
+      const dim3 wgrid((unsigned)ceil_div((long long)per, REDW_OUT), p.phases);
+      switch (p.mode) {
+        case MODE_CONV: splitk_reduce_wide<MODE_CONV><<<wgrid, 256, 0, s>>>(g, fd, per); break;
+        case MODE_CONVT2: splitk_reduce_wide<MODE_CONVT2><<<wgrid, 256, 0, s>>>(g, fd, per); break;
+        default: splitk_reduce_wide<MODE_WGRAD><<<wgrid, 256, 0, s>>>(g, fd, per); break;
+      }
+      RGAN_CHECK_LAUNCH();
+      return 0;
+    }
+    const dim3 rgrid((unsigned)std::min<uint32_t>((per + 255) / 256, 8192), p.phases);
 #define RGAN_RED(MD)                                                                   \
   switch (kind) {                                                                      \
     case RED_VEC: splitk_reduce<MD, RED_VEC><<<rgrid, 256, 0, s>>>(g, fd, per); break;  \
@@ -3472,15 +3548,17 @@ extern "C" int rgan_adam_packed(int ntensors, float* const* params, const float*
     }
   }
   RGAN_CHECK_LAUNCH();
-  const int rs = rgan_adam_step_inc(step, stream);
-  if (rs) return rs;
   AdamPackBatch b{};
   long long blocks = 0;
   int np = 0;
-  auto flush = [&]() -> int {
+  bool bumped = false;
+  auto flush = [&](bool last) -> int {
     if (b.cnt == 0) return 0;
     b.first[b.cnt] = (int)blocks;
-    if (blocks > 0) adam_pack_kernel<<<(unsigned)blocks, AP_THREADS, 0, s>>>(b, hyper, step);
+    if (blocks > 0) {
+      adam_pack_kernel<<<(unsigned)blocks, AP_THREADS, 0, s>>>(b, hyper, step, last ? 1 : 0);
+      bumped = last;
+    }
     RGAN_CHECK_LAUNCH();
     b = AdamPackBatch{};
     blocks = 0;
@@ -3492,7 +3570,7 @@ extern "C" int rgan_adam_packed(int ntensors, float* const* params, const float*
     const int nt = (int)L.size();
     RGAN_REQUIRE(nt <= AP_MAXP);
     if (b.cnt == AP_MAXT || np + nt > AP_MAXP) {
-      const int rc = flush();
+      const int rc = flush(false);
       if (rc) return rc;
     }
     AdamPackTensor X{params[j], grads[j], exp_avg[j], exp_avg_sq[j], numel[j], 0, 0, np, nt};
@@ -3512,8 +3590,12 @@ extern "C" int rgan_adam_packed(int ntensors, float* const* params, const float*
     RGAN_REQUIRE(blocks < (1LL << 30));
     ++b.cnt;
   }
-  int rc = flush();
+  int rc = flush(true);
   if (rc) return rc;
+  if (!bumped) {  // no block ran the last launch's ticket: a separate increment
+    rc = rgan_adam_step_inc(step, stream);
+    if (rc) return rc;
+  }
   for (size_t i = 0; i < later.size(); ++i) {  // layouts the kernel does not write: repack
     launch_pack_plan(later[i], later_out[i], s);
     RGAN_CHECK_LAUNCH();

@@ -204,6 +204,28 @@ def test_image_layer_patches(K, C, layout):
     assert _rel(K.unpatch_grad(g1, 40, C, 64, 1), wr.grad) < 2e-6
 
 
+@pytest.mark.parametrize("B", [32, 64])
+def test_image_layer_wgrad_full_size(K, B):
+    """The image layers' weight gradients at the C1 shapes (64x64 RGB, 128 channels): a
+    128 x 64 patch-GEMM output split-K hundreds of ways, reduced by the 16-lane split reduce
+    (splitk_reduce_wide) -- vs torch fp64."""
+    torch.manual_seed(B)
+    img = _nhwc(torch.randn(B, 3, 64, 64, device=DEV))
+    dy = _nhwc(torch.randn(B, 128, 32, 32, device=DEV))
+    X = K.patches_k4s2(img)
+    g1, _ = K.conv_wgrad(X, dy, K.G1X1, (128, 64, 1, 1))
+    w64 = torch.zeros(128, 3, 4, 4, dtype=torch.float64, requires_grad=True)
+    F.conv2d(img.double().cpu(), w64, stride=2, padding=1).backward(dy.double().cpu())
+    assert _rel(K.unpatch_grad(g1, 128, 3, 64, 1), w64.grad) < 2e-6
+    # G's last ConvTranspose2d (128 -> 3, 32x32 -> 64x64): dW over the image gradient's patches
+    x = _nhwc(torch.randn(B, 128, 32, 32, device=DEV))
+    dimg = torch.randn(B, 3, 64, 64, device=DEV)
+    g1, _ = K.conv_wgrad(K.patches_k4s2(dimg), x, K.G1X1, (128, 64, 1, 1))
+    wr = torch.zeros(128, 3, 4, 4, dtype=torch.float64, requires_grad=True)
+    F.conv_transpose2d(x.double().cpu(), wr, stride=2, padding=1).backward(dimg.double().cpu())
+    assert _rel(K.unpatch_grad(g1, 128, 3, 64, 1), wr.grad) < 2e-6
+
+
 @pytest.mark.parametrize("nc", [1, 2, 3, 4])
 def test_conv_narrow_paths(K, nc):
     """Narrow kernels: ConvT k4s2p1 with nc outputs (and the Conv2d dgrad of that shape),
@@ -609,6 +631,28 @@ def test_adam_matches_torch(K):
     assert step.item() == 3
 
 
+def test_adam_packed_step_counter_many_tensors(K):
+    """optim.Adam over more tensors than one packed launch holds (two launches, the step
+    counter stored by the second one's last block) == torch.optim.Adam, the device step
+    counter at the step count."""
+    from relativisticgan_amd.optim import Adam
+    torch.manual_seed(6)
+    shapes = [(33,), (4096 * 3 + 8,), (5, 7)] * 11
+    params = [torch.nn.Parameter(torch.randn(s, device=DEV)) for s in shapes]
+    ref = [torch.nn.Parameter(p.detach().cpu().clone()) for p in params]
+    opt = Adam(params, lr=1e-3, betas=(0.5, 0.999))
+    topt = torch.optim.Adam(ref, lr=1e-3, betas=(0.5, 0.999))
+    for it in range(3):
+        for p, r in zip(params, ref):
+            p.grad = torch.randn_like(p)
+            r.grad = p.grad.cpu()
+        opt.step()
+        topt.step()
+        assert opt._dev[0][2].item() == it + 1
+    for p, r in zip(params, ref):
+        assert torch.allclose(p.detach().cpu(), r.detach(), rtol=1e-6, atol=1e-7)
+
+
 def test_gather(K):
     imgs = torch.randn(10, 3, 4, 4, device=DEV)
     idx = torch.tensor([3, 0, 9], dtype=torch.long, device=DEV)
@@ -806,6 +850,8 @@ def test_adam_writes_packed_layouts(K):
         for q in twins:
             ref.state[q]["step"] += 1
         torch.cuda.synchronize()
+        # the packed kernel's last block stores step + 1 (no separate increment launch)
+        assert opt._dev[0][2].item() == dstep.item() == step + 1
         for p, q in zip(params, twins):
             assert torch.equal(p.detach(), q.detach())
             assert torch.equal(opt.state[p]["exp_avg"], ref.state[q]["exp_avg"])
