@@ -2006,6 +2006,9 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
 // staged through LDS 16 channels at a time (pixel stride 20 dwords: ds_read_b128 of 4
 // channels), weights [co][c][tap] staged beside it; per 4 channels a wave reads 18 + 16
 // ds_read_b128 and issues 128 MFMAs.
+#ifndef RGAN_NARROW_MAX_SPLITS
+#define RGAN_NARROW_MAX_SPLITS 8  // input-channel splits of convt2_narrow_mfma on small grids
+#endif
 constexpr int NM_TR = 16, NM_TC = 32, NM_HR = NM_TR + 2, NM_HC = NM_TC + 2, NM_CH = 16, NM_LD = NM_CH + 4;
 constexpr int NM_XQ = NM_HR * NM_HC * (NM_CH / 4);  // float4 slots of one staged chunk
 constexpr int NM_XPT = (NM_XQ + 255) / 256;         // ... per thread
@@ -2726,7 +2729,8 @@ static bool plan_narrow_t(Plan& p, int batch, const float* x, const long long* x
   const int chunks = ceil_div(C, NM_CH);
   int splits = 1;
   if (ntiles < 256)
-    splits = (int)std::min<long long>(std::min(chunks, 8), ceil_div(512, (int)std::max<long long>(ntiles, 1)));
+    splits = (int)std::min<long long>(std::min(chunks, RGAN_NARROW_MAX_SPLITS),
+                                      ceil_div(512, (int)std::max<long long>(ntiles, 1)));
   a.cps = ceil_div(chunks, std::max(splits, 1)) * NM_CH;
   a.splits = ceil_div(C, a.cps);
   a.slab = nullptr;

@@ -1,46 +1,49 @@
-"""Image-layer (narrow) kernel micro-benchmark at the C3 shard's shapes (diagnostic; GPU).
+"""Narrow ConvTranspose2d micro-benchmark (diagnostic; GPU): G's image layer (128 -> 3,
+32x32 -> 64x64, tanh) and D's image-layer data gradient (the same ConvT shape, no act) at
+C1 / C2 batch sizes, each launch sequence (narrow kernel + split reduce) timed alone with
+HIP events.  Run against variant builds (RGAN_LIB=..., RGAN_NARROW_MAX_SPLITS=...).
 
-D's image conv (3 -> 128, k4 s2 p1, 256^2 -> 128^2, conv_narrow_in_mfma), G's image convT
-(128 -> 3, 128^2 -> 256^2, convt2_narrow_mfma) and their data gradients, B = 32.  Prints
-time per launch (library HIP events) and HBM-side algorithmic GB/s (image + 128-channel side
-once each).  usage: python tools/narrow_micro.py [reps] [B]
+usage: python tools/narrow_micro.py [reps]
 """
 import os
 import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 from relativisticgan_amd import kernels as K  # noqa: E402
 
+SHAPES = [(32, 128, 32, 32), (64, 128, 32, 32), (64, 128, 64, 64), (32, 64, 32, 32)]
 
-def run(name, fn, reps, nbytes):
+
+def one(fn, reps):
     fn()
     torch.cuda.synchronize()
-    K.profile_begin(reps + 8)
+    tot = 0.0
     for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
         fn()
-    pr = K.profile_end()
-    us = pr["ms"] / reps * 1000
-    print(f"{name:28s} {us:8.1f} us  {nbytes / us / 1e3:7.1f} GB/s  {pr['flops'] / pr['ms'] / 1e9:6.1f} TF/s",
-          flush=True)
+        b.record()
+        torch.cuda.synchronize()
+        tot += a.elapsed_time(b)
+    return tot / reps * 1000.0
 
 
 def main():
-    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
-    B = int(sys.argv[2]) if len(sys.argv) > 2 else 32
-    S, C = 256, 128
-    g = K.ConvGeom(4, 2, 1, False)
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
     gt = K.ConvGeom(4, 2, 1, True)
-    img = torch.rand(B, 3, S, S, device="cuda") * 2 - 1
-    wd = torch.nn.Parameter(torch.randn(C, 3, 4, 4, device="cuda") * 0.02)
-    wg = torch.nn.Parameter(torch.randn(C, 3, 4, 4, device="cuda") * 0.02)
-    h = torch.randn(B, C, S // 2, S // 2, device="cuda").contiguous(memory_format=torch.channels_last)
-    nb = 4 * (B * 3 * S * S + B * C * (S // 2) ** 2)
-    run("D image conv fwd", lambda: K.conv_fwd(img, wd, g, act="lrelu", alpha=0.2, cache=True), reps, nb)
-    run("D image conv dgrad", lambda: K.conv_dgrad(h, wd, g, tuple(img.shape), like=img, cache=True), reps, nb)
-    run("G image convT fwd", lambda: K.conv_fwd(h, wg, gt, act="tanh", nchw_out=True, cache=True), reps, nb)
-    run("G image convT dgrad", lambda: K.conv_dgrad(img, wg, gt, tuple(h.shape), cache=True), reps, nb)
+    tot = 0.0
+    for B, C, H, W in SHAPES:
+        x = K.empty_nhwc(B, C, H, W, "cuda").normal_()
+        w = torch.randn(C, 3, 4, 4, device="cuda") * 0.05
+        t1 = one(lambda: K.conv_fwd(x, w, gt, act="tanh", cache=True), reps)
+        ref = torch.nn.functional.conv_transpose2d(x.double(), w.double(), stride=2, padding=1).tanh()
+        err = (K.conv_fwd(x, w, gt, act="tanh", cache=True).double() - ref).abs().max().item()
+        tot += t1
+        print(f"{str((B, C, H, W)):20s} convT->3 {t1:6.1f} us  max err {err:.2e}", flush=True)
+    print(f"sum {tot:.1f} us")
 
 
 if __name__ == "__main__":
