@@ -646,6 +646,131 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ da
   }
 }
 
+// Small-P BatchNorm backward (the 4x4 layer under D's closing dense layer: 512 rows per
+// call at B = 32): the sums, their merge and the apply in one launch instead of three.
+// Block = 4 channels (one float4 quad) x 256 row lanes; lane r sums rows r, r + 256, ... of
+// each segment in double (bn_bwd_partial's terms), a fixed LDS tree adds the 256 lanes, then
+// every lane applies its rows with bn_bwd_apply's constants and formula (row loads issued 4
+// ahead in both passes).  NSEG 2: rows [0, Ps) use stats / sums row 0, [Ps, 2 Ps) row 1; the
+// affine gradients are the segments' sum.
+constexpr int BNS_LANES = 256, BNS_CH = 4;
+constexpr long long BNS_MAX_ROWS = 2048;  // rows per segment: <= 8 per lane
+template <int NSEG>
+__global__ __launch_bounds__(256) void bn_bwd_small(const float* __restrict__ da, const float* __restrict__ y,
+                                                    long long Ps, int C, const float* __restrict__ stats,
+                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                    int act, float alpha, float* __restrict__ dy, float* dgamma,
+                                                    float* dbeta) {
+  __shared__ double sh[2][NSEG][BNS_LANES][BNS_CH];
+  const int r = threadIdx.x, c0 = blockIdx.x * BNS_CH;
+  float mean[NSEG][4], al[NSEG][4], be[NSEG][4], inv[NSEG][4];
+#pragma unroll
+  for (int sg = 0; sg < NSEG; ++sg)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float* st = stats + (size_t)sg * 2 * C;
+      const int c = c0 + q;
+      inv[sg][q] = st[C + c];
+      mean[sg][q] = st[c];
+      al[sg][q] = (gamma ? gamma[c] : 1.f) * inv[sg][q];
+      be[sg][q] = (beta ? beta[c] : 0.f) - mean[sg][q] * al[sg][q];
+    }
+#pragma unroll
+  for (int sg = 0; sg < NSEG; ++sg) {
+    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+    const long long rb = (long long)sg * Ps;
+    for (long long p = r; p < Ps; p += 4 * BNS_LANES) {
+      float4 v[4], g[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long pp = p + u * BNS_LANES;
+        if (pp < Ps) {
+          v[u] = *reinterpret_cast<const float4*>(y + (rb + pp) * C + c0);
+          g[u] = *reinterpret_cast<const float4*>(da + (rb + pp) * C + c0);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (p + u * BNS_LANES < Ps) {
+          const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w}, gg[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const double gz = (double)(gg[q] * act_grad_from_in(vv[q] * al[sg][q] + be[sg][q], act, alpha));
+            s1[q] += gz;
+            s2[q] += gz * (double)(vv[q] - mean[sg][q]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      sh[0][sg][r][q] = s1[q];
+      sh[1][sg][r][q] = s2[q];
+    }
+  }
+  __syncthreads();
+  for (int h = BNS_LANES / 2; h > 0; h >>= 1) {
+    if (r < h) {
+#pragma unroll
+      for (int sg = 0; sg < NSEG; ++sg)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          sh[0][sg][r][q] += sh[0][sg][r + h][q];
+          sh[1][sg][r][q] += sh[1][sg][r + h][q];
+        }
+    }
+    __syncthreads();
+  }
+  const double inv_pg = 1.0 / (double)Ps;
+  float k1[NSEG][4], k2[NSEG][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float db = 0.f, dg = 0.f;
+#pragma unroll
+    for (int sg = 0; sg < NSEG; ++sg) {
+      const double S1 = sh[0][sg][0][q], S2 = sh[1][sg][0][q], iv = (double)inv[sg][q];
+      k1[sg][q] = (float)(S1 * inv_pg);
+      k2[sg][q] = (float)(S2 * iv * iv * inv_pg);
+      const float dbs = (float)S1, dgs = (float)(S2 * iv);
+      db = sg == 0 ? dbs : db + dbs;
+      dg = sg == 0 ? dgs : dg + dgs;
+    }
+    if (r == 0) {
+      if (dbeta) dbeta[c0 + q] = db;
+      if (dgamma) dgamma[c0 + q] = dg;
+    }
+  }
+#pragma unroll
+  for (int sg = 0; sg < NSEG; ++sg) {
+    const long long rb = (long long)sg * Ps;
+    for (long long p = r; p < Ps; p += 4 * BNS_LANES) {
+      float4 v[4], g[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long pp = p + u * BNS_LANES;
+        if (pp < Ps) {
+          v[u] = *reinterpret_cast<const float4*>(y + (rb + pp) * C + c0);
+          g[u] = *reinterpret_cast<const float4*>(da + (rb + pp) * C + c0);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long pp = p + u * BNS_LANES;
+        if (pp < Ps) {
+          float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+          const float gg[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float gz = gg[q] * act_grad_from_in(vv[q] * al[sg][q] + be[sg][q], act, alpha);
+            vv[q] = al[sg][q] * (gz - k1[sg][q] - (vv[q] - mean[sg][q]) * k2[sg][q]);
+          }
+          *reinterpret_cast<float4*>(dy + (rb + pp) * C + c0) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+        }
+      }
+    }
+  }
+}
+
 static bool dense_nhwc(long long sp, long long sc, int C, const void* p) {
   return sc == 1 && sp == C && ((uintptr_t)p & 15) == 0;
 }
@@ -716,6 +841,15 @@ extern "C" int rgan_bn_backward_segments(const float* da, const float* y, long l
   RGAN_REQUIRE(da && y && stats && dy && partial && P > 0 && C > 0 && (nseg == 1 || nseg == 2) && P % nseg == 0);
   hipStream_t s = (hipStream_t)stream;
   const long long Ps = P / nseg;
+  if (Ps <= BNS_MAX_ROWS && C % BNS_CH == 0 && dense_nhwc(C, 1, C, y) && dense_nhwc(C, 1, C, da) &&
+      dense_nhwc(C, 1, C, dy)) {  // small layers: one launch
+    if (nseg == 1)
+      bn_bwd_small<1><<<C / BNS_CH, 256, 0, s>>>(da, y, Ps, C, stats, gamma, beta, act, act_alpha, dy, dgamma, dbeta);
+    else
+      bn_bwd_small<2><<<C / BNS_CH, 256, 0, s>>>(da, y, Ps, C, stats, gamma, beta, act, act_alpha, dy, dgamma, dbeta);
+    RGAN_CHECK_LAUNCH();
+    return 0;
+  }
   BnGeo g = bn_geo(Ps, C, C, 1);
   RGAN_REQUIRE(g.vec && dense_nhwc(C, 1, C, y) && dense_nhwc(C, 1, C, da) && dense_nhwc(C, 1, C, dy));
   double* part = (double*)partial;
@@ -809,6 +943,13 @@ extern "C" int rgan_bn_backward(const float* da, long long dsp, long long dsc, c
                                 const float* beta, int act, float act_alpha, float* dy, long long ysp,
                                 long long ysc, float* dgamma, float* dbeta, void* partial, void* stream) {
   RGAN_REQUIRE(partial && P > 0 && C > 0);
+  if (P <= BNS_MAX_ROWS && C % BNS_CH == 0 && dense_nhwc(sp, sc, C, y) && dense_nhwc(dsp, dsc, C, da) &&
+      dense_nhwc(ysp, ysc, C, dy) && stats && dy) {  // small layers: one launch
+    bn_bwd_small<1><<<C / BNS_CH, 256, 0, (hipStream_t)stream>>>(da, y, P, C, stats, gamma, beta, act, act_alpha, dy,
+                                                                 dgamma, dbeta);
+    RGAN_CHECK_LAUNCH();
+    return 0;
+  }
   double* sums = (double*)partial + (size_t)max_chunks(P, C) * 2 * C;
   int rc = rgan_bn_backward_sums(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, sums,
                                  partial, stream);
