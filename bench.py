@@ -251,6 +251,7 @@ def _run_workload(name, steps, warmup, world, args, K, dp_path=False):
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=side):
                 t.iteration(it)
+        t.graph_captured = True  # host mirrors (Adam step, LR) freeze from here: no checkpoints
         it += 1
         graph_segments = getattr(graph, "n_segments", 1)
         graph.replay()  # one untimed replay

@@ -330,6 +330,10 @@ int rgan_loss_head(int kind, int side, const float* r, const float* f, int n,
  * and both gradients (nullable) -- the batched D step's pair of losses. */
 int rgan_loss_head_pair(int kind, const float* r, const float* f, int n, float* loss3, float* dr,
                         float* df, void* stream);
+/* Heads 5-8, G side, on the G step's batched output y = [D(G(z)); D(x)] (2n values): loss
+ * and dy[0..n) = d loss / d D(G(z)), dy[n..2n) = 0 (D(x) is a no-grad forward, GLI:681),
+ * in one launch. */
+int rgan_loss_head_joint(int kind, const float* y, int n, float* loss, float* dy, void* stream);
 /* Distributed form: the three phases of the same head with the cross-rank sums done by
  * the caller between them.  phase 0: sums[0..1] = (sum r, sum f) local;
  * phase 1: given global means in gsum[0..1] (sum r, sum f over n_global), sums[0..3] =
@@ -400,7 +404,8 @@ int rgan_adam_step_inc(float* step, void* stream);
  * repack pass reading every weight again after the step.  packs[i].tensor indexes the
  * params arrays; layouts the Adam kernel cannot write (non-contiguous weights, generic
  * packs) are repacked by their own launch after it, so every listed layout is current
- * when the call's work completes. */
+ * when the call's work completes.  step = device float[2]: step[0] the count (as rgan_adam),
+ * step[1] the call's arrival ticket (a uint32, 0 before the first call; left 0). */
 typedef struct RganAdamPack {
   int tensor;
   int which;               /* 0 forward layout, 1 data-gradient layout (rgan_conv_pack) */

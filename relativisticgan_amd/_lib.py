@@ -102,6 +102,7 @@ _SIGS = {
     "rgan_channel_sum": (c_int, [c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_int, c_vp, c_vp]),
     "rgan_loss_head": (c_int, [c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
     "rgan_loss_head_pair": (c_int, [c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "rgan_loss_head_joint": (c_int, [c_int, c_vp, c_int, c_vp, c_vp, c_vp]),
     "rgan_loss_head_dist": (c_int, [c_int, c_int, c_int, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                                     c_vp]),
     "rgan_scale": (c_int, [c_vp, c_vp, c_ll, c_vp, c_vp]),

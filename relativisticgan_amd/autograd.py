@@ -329,15 +329,27 @@ class ConvLayerFn(torch.autograd.Function):
             if stats is not None and stats.dim() == 2:
                 stats = stats[0] if ctx.gsegs == 1 else stats[:ctx.gsegs]
             if nx:
+                # rows of the trailing (no-grad) segments are never read by the batched pass's
+                # consumer and stay unwritten; zeroed only under anomaly detection, which
+                # inspects every backward output
                 dx_full = torch.empty_like(saved[0])
                 dx_out = dx_full[:Bg]
+                if torch.is_anomaly_enabled():
+                    dx_full[Bg:].zero_()
         # this layer's output gradient may arrive with its first backward pass already applied
         # by the layer above (LayerLink): g = da * act' (+ BN sums), or da * act'
         done = ctx.link_out.done if ctx.link_out is not None else None
         if done is not None:
             ctx.link_out.done = None
-            if done[0] != da.data_ptr() or not done[1].fused:
-                done = None
+            if not done[1].fused:
+                done = None  # the GEMM above wrote the plain gradient
+            elif done[0] != da.data_ptr():
+                # the layer above applied this layer's act' / BatchNorm sums to the gradient it
+                # produced, but a different tensor arrived here (a cast, a hook, a second
+                # consumer re-materialised it): running the first pass again would be silently
+                # wrong, so refuse
+                raise RuntimeError("LayerLink: the fused output gradient was replaced before this layer's "
+                                   "backward (hook / cast / second consumer of the activation)")
         # ... and this layer's data gradient may carry the layer below's first pass
         # (the two layers ran in one chain call: same batch segments, same gradient rows)
         post = ctx.link_in.post(Bg, ctx.gsegs) if nx and ctx.link_in is not None else None

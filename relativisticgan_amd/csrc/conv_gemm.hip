@@ -2407,10 +2407,10 @@ __device__ __forceinline__ void adam_pack_flat(const AdamPackBatch& b, const Ada
                                                int local, int tid);
 
 // The call's step-counter increment rides on its last launch: every block computes with
-// step + 1 (read at entry), and the last block to arrive (a device-wide ticket) stores it --
-// after every block of every launch of the call has read the old value (no separate
-// increment launch ahead of the step).
-__device__ unsigned int g_adam_arrive = 0;
+// step + 1 (read at entry), and the last block to arrive stores it -- after every block of
+// every launch of the call has read the old value (no separate increment launch ahead of the
+// step).  The arrival ticket is the group's own word next to its counter (step[1], 0 between
+// calls), so optimizer steps of different groups / optimizers / streams never share one.
 
 __global__ __launch_bounds__(AP_THREADS) void adam_pack_kernel(AdamPackBatch b, const double* __restrict__ hyper,
                                                                float* step, int bump) {
@@ -2475,9 +2475,10 @@ __global__ __launch_bounds__(AP_THREADS) void adam_pack_kernel(AdamPackBatch b, 
   }
   if (bump) {
     __syncthreads();  // every wave of this block has read step[0]
-    if (threadIdx.x == 0 && atomicAdd(&g_adam_arrive, 1u) == gridDim.x - 1) {
+    unsigned int* ticket = reinterpret_cast<unsigned int*>(step + 1);
+    if (threadIdx.x == 0 && atomicAdd(ticket, 1u) == gridDim.x - 1) {
       step[0] = st1;
-      atomicExch(&g_adam_arrive, 0u);
+      atomicExch(ticket, 0u);
     }
   }
 }

@@ -68,10 +68,12 @@ __device__ __forceinline__ float single_term(int kind, int side, float t, float&
 __global__ __launch_bounds__(1024) void loss_head_kernel(int kind, int side, int phase, const float* r,
                                                          const float* f, int n, int n_global,
                                                          const float* gsum, float* sums, float* loss,
-                                                         float* dr, float* df) {
+                                                         float* dr, float* df, float* zr = nullptr) {
   __shared__ float red[16];
   const int tid = threadIdx.x;
   const float ng = (float)n_global;
+  if (zr)  // rgan_loss_head_joint: the joint gradient's no-grad half is zero
+    for (int i = tid; i < n; i += blockDim.x) zr[i] = 0.f;
   if (kind <= 4) {
     const float* t = side == 0 ? r : f;
     float* dt = side == 0 ? dr : df;
@@ -209,6 +211,17 @@ extern "C" int rgan_loss_head(int kind, int side, const float* r, const float* f
   RGAN_REQUIRE(head_args_ok(kind, side, r, f, n) && loss);
   loss_head_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(kind, side, -1, r, f, n, n, nullptr, nullptr, loss,
                                                        dr, df);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
+// Heads 5-8, G side, on the G step's joint output y = [D(G(z)); D(x)] (2n values, the batched
+// pass of GLI:673-707): loss and dy = [d loss / d D(G(z)); 0] -- D(x) is a no-grad forward in
+// the reference (GLI:681), so the second half of the joint gradient is zero, in the same launch.
+extern "C" int rgan_loss_head_joint(int kind, const float* y, int n, float* loss, float* dy, void* stream) {
+  RGAN_REQUIRE(kind >= 5 && kind <= 8 && y && dy && head_args_ok(kind, 2, y + n, y, n) && loss);
+  loss_head_kernel<<<1, 1024, 0, (hipStream_t)stream>>>(kind, 2, -1, y + n, y, n, n, nullptr, nullptr, loss,
+                                                       nullptr, dy, dy + n);
   RGAN_CHECK_LAUNCH();
   return 0;
 }

@@ -120,7 +120,10 @@ class PiecewiseGraph:
     counter, the device RNG's Philox offsets) as eager iterations, with the ~10-20 us of
     Python + ctypes per launch gone from everything between the collectives.  All segments
     share one memory pool and replay in capture order, so a tensor produced in one segment
-    and consumed in a later one keeps its address."""
+    and consumed in a later one keeps its address.  Host-side state advances only at capture
+    (Adam's ``state['step']`` mirror, the LR schedulers, a deferred G decay): after replays the
+    optimizer state_dict / checkpoint would be stale, so the caller sets
+    ``Trainer.graph_captured`` and ``Trainer.state()`` refuses to checkpoint."""
 
     def __init__(self, stream):
         self.stream = stream

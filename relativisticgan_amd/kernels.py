@@ -793,6 +793,17 @@ def loss_head_pair(kind, r, f, need_dr=True, need_df=True, dr=None, df=None):
     return loss3, dr, df
 
 
+def loss_head_joint(kind, y):
+    """Heads 5-8, G side, on the joint [D(G(z)); D(x)] output: (loss, dy) with dy's second
+    half zero (rgan_loss_head_joint)."""
+    n = y.numel() // 2
+    loss = torch.empty((), dtype=torch.float32, device=y.device)
+    dy = torch.empty_like(y)
+    L.check(L.lib().rgan_loss_head_joint(int(kind), L.ptr(y), n, L.ptr(loss), L.ptr(dy), L.stream()),
+            "rgan_loss_head_joint")
+    return loss, dy
+
+
 def loss_head_dist(kind, side, phase, r, f, n_global, gsum=None, need_dr=True, need_df=True):
     t = r if r is not None else f
     n = t.numel()
@@ -956,7 +967,10 @@ def adam(params, grads, exp_avgs, exp_avg_sqs, hyper, step):
 
 def adam_packed(params, grads, exp_avgs, exp_avg_sqs, hyper, step, layouts):
     """``adam`` that also writes the cached GEMM layouts ``layouts`` ([(param index, key,
-    pack-cache entry)], _PackCache.layouts_of) from the updated values (rgan_adam_packed)."""
+    pack-cache entry)], _PackCache.layouts_of) from the updated values (rgan_adam_packed).
+    ``step``: the count, a view whose next float is the group's arrival ticket (optim.Adam)."""
+    if step.untyped_storage().nbytes() < 4 * (step.storage_offset() + 2):
+        raise L.RganError("adam_packed: step must be followed by its arrival-ticket word (float[2] storage)")
     n = len(params)
     arr = ctypes.c_void_p * max(n, 1)
     P = arr(*[p.data_ptr() for p in params])

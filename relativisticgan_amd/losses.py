@@ -156,9 +156,9 @@ def loss_D_cat(kind, y):
 
 class _HeadCatG(torch.autograd.Function):
     """errG of heads 5-8 (GLI:695-707) on the G step's batched output y = [D(G(z)); D(x)]:
-    the gradient is written for the fake half only (D(x) is a constant there); the rows of
-    the real half are left unwritten -- the batched pass's backward reads the fake rows
-    only (ConvLayerFn ``gsegs``)."""
+    the gradient of the fake half, and zeros for the real half (D(x) is a no-grad constant
+    there, GLI:681) -- written by the head's own launch; the batched pass's backward reads the
+    fake rows only (ConvLayerFn ``gsegs``)."""
 
     @staticmethod
     def forward(ctx, y, kind):
@@ -166,8 +166,7 @@ class _HeadCatG(torch.autograd.Function):
         if dp.active():
             loss, _, df = _head_dist(kind, 2, y[B:], y[:B], False, True)
         else:
-            df = torch.empty_like(y)  # the fake rows' gradient in the first half
-            loss, _, _ = K.loss_head(kind, 2, y[B:], y[:B], need_dr=False, df=df[:B])
+            loss, df = K.loss_head_joint(kind, y)  # [d errG / d D(G(z)); 0]
         ctx.save_for_backward(df)
         ctx.B = B
         return loss
@@ -178,7 +177,7 @@ class _HeadCatG(torch.autograd.Function):
         B = ctx.B
         if df.numel() == 2 * B and _is_unit(g):
             return df, None
-        out = torch.empty(2 * B, dtype=df.dtype, device=df.device)
+        out = torch.zeros(2 * B, dtype=df.dtype, device=df.device)
         K.scale(df[:B], g.contiguous(), out=out[:B])
         return out, None
 

@@ -34,7 +34,8 @@ class Adam(torch.optim.Optimizer):
         if cur is None or cur[0].device != device:
             hyper = torch.tensor(list(key) + [0.0, 0.0, 0.0], dtype=torch.float64).to(device, non_blocking=True)
             step0 = float(first_state["step"]) if first_state is not None and "step" in first_state else 0.0
-            step = torch.full((1,), step0, dtype=torch.float32, device=device)
+            # [count, arrival ticket] (rgan_adam_packed); the count is the 1-element view
+            step = torch.tensor([step0, 0.0], dtype=torch.float32).to(device)[:1]
             cur = (hyper, key, step)
             self._dev[gi] = cur
         elif cur[1] != key:

@@ -108,6 +108,10 @@ class Trainer:
         self._one = None
         self.errD = self.errG = None
         self.last = {}
+        # set by whoever captures iterations into HIP graphs (bench.py, dp.PiecewiseGraph users):
+        # replays advance the device-side state only (Adam's device step counters, the device
+        # LR), while the host mirrors (state['step'], the schedulers) froze at capture time
+        self.graph_captured = False
 
     # -- inputs (host order = reference order; device = throughput mode)
     def _shard(self, t):
@@ -342,6 +346,10 @@ class Trainer:
 
     # -- checkpoint (GLI:536-552, 733-747): same dict keys as the reference
     def state(self, i, current_set_images=0):
+        if self.graph_captured:
+            raise RuntimeError("Trainer.state(): iterations were replayed from a captured HIP graph, so the "
+                               "host-side Adam step counts and LR schedulers are stale; checkpoint an eagerly "
+                               "stepped trainer")
         self.flush()
         return {"i": i, "current_set_images": current_set_images, "G_state": self.G.state_dict(),
                 "D_state": self.D.state_dict(), "G_optimizer": self.optG.state_dict(),

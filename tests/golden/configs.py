@@ -79,10 +79,24 @@ CONFIGS = {
     "rahinge_spectral_c5": {"args": {"image_size": 128, "batch_size": 32, "z_size": 128, "G_h_size": 128,
                                      "D_h_size": 128, "loss_D": 8, "spectral": "True", "n_iter": 2},
                             "seed": 1, "n_images": 64, "threads": 8},
+    # C3 = the per-GPU shard of configs[2] (the bench's headline workload): RaLSGAN DCGAN
+    # 256x256, batch 32, h = z = 128 (GLI:329 mult = S/8 -> 5 middle layers per net; heads
+    # GLI:639, 705).  ~2.5 min of reference CPU time per iteration at 8 threads.
+    "ralsgan_c3": {"args": {"image_size": 256, "batch_size": 32, "z_size": 128, "G_h_size": 128,
+                            "D_h_size": 128, "loss_D": 7, "n_iter": 2}, "seed": 1, "n_images": 64,
+                   "threads": 8},
 }
 
 # full-size configs: minutes of CPU oracle time each (GPU parity runs them with all host cores)
-FULL_SIZE = ("ralsgan_c1", "rasgan_c2", "wgangp_c4p", "rahinge_spectral_c5")
+FULL_SIZE = ("ralsgan_c1", "rasgan_c2", "wgangp_c4p", "rahinge_spectral_c5", "ralsgan_c3")
+# configs too slow for the default CPU suite's bitwise oracle pin (RGAN_SLOW=1 runs them)
+SLOW_PIN = ("ralsgan_c3",)
+
+# 100-iteration scalar trajectories of the unmodified reference at several thread counts
+# (SURVEY §8(c)(iii)): the spread between thread counts is the drift envelope.  Keys of
+# TRAJECTORIES name a config of CONFIGS whose args are used with n_iter = TRAJ_ITERS.
+TRAJ_ITERS = 100
+TRAJECTORIES = {"ralsgan_c1": (1, 2, 4, 8)}
 
 
 # configs with a reference fixture (tests/golden/<name>.npz) pinning the oracle bitwise

@@ -203,7 +203,88 @@ def run_config(name, cfg):
     return out
 
 
+TRAJ_KEYS = ("errD", "errG", "D.y_pred", "D.y_pred_fake", "G.y_pred", "G.y_pred_fake",
+             "D.x", "D.z", "G.z", "G.x", "D.wsum", "G.wsum")
+
+
+def run_trajectory(name, threads, n_iter):
+    """Scalar trajectory of the unmodified reference: per iteration the
+    losses, the means of D's outputs in both steps, the sums of the drawn inputs (draw order)
+    and the sums of each net's parameters after its step, at ``threads`` intra-op threads.
+    Written to tests/golden/traj_<name>_t<threads>.npz."""
+    cfg = CONFIGS[name]
+    torch.set_num_threads(threads)
+    args = dict(cfg["args"])
+    S = args.get("image_size", 64)
+    install_stubs(synthetic_dataset(cfg.get("n_images", 64), S))
+    out = {k: np.full(n_iter, np.nan) for k in TRAJ_KEYS}
+    orig_step = torch.optim.Adam.step
+
+    def wsum(net):
+        return float(sum(p.detach().double().sum() for p in net.parameters()))
+
+    def step_hook(self, *a, **k):
+        g = _script_globals()
+        i = g["i"]
+        side = "D" if self is g["optimizerD"] else "G"
+        res = orig_step(self, *a, **k)
+        if side == "D":
+            out["errD"][i] = float(g["errD"])
+            out["D.y_pred"][i] = float(g["y_pred"].detach().double().mean())
+            out["D.y_pred_fake"][i] = float(g["y_pred_fake"].detach().double().mean())
+            out["D.x"][i] = float(g["x"].double().sum())
+            out["D.z"][i] = float(g["z"].double().sum())
+        else:
+            out["errG"][i] = float(g["errG"])
+            if g["param"].loss_D not in (1, 2, 3, 4):
+                out["G.y_pred"][i] = float(g["y_pred"].detach().double().mean())
+                out["G.x"][i] = float(g["x"].double().sum())
+            out["G.y_pred_fake"][i] = float(g["y_pred_fake"].detach().double().mean())
+            out["G.z"][i] = float(g["z"].double().sum())
+        out[side + ".wsum"][i] = wsum(g[side])
+        return res
+
+    torch.optim.Adam.step = step_hook
+    tmp = tempfile.mkdtemp(prefix="rgan_traj_")
+    os.makedirs(os.path.join(tmp, "extra"))
+    argv = [REF_SCRIPT, "--cuda", "False", "--seed", str(cfg.get("seed", 1)), "--n_iter", str(n_iter),
+            "--gen_extra_images", "0", "--print_every", "1000", "--output_folder", tmp,
+            "--extra_folder", tmp + "/extra", "--input_folder", tmp]
+    for k, v in args.items():
+        if k != "n_iter":
+            argv += ["--" + k, str(v)]
+    old_argv, old_cwd = sys.argv, os.getcwd()
+    sys.argv = argv
+    os.chdir(tmp)
+    try:
+        runpy.run_path(REF_SCRIPT, run_name="__main__")
+    finally:
+        sys.argv = old_argv
+        os.chdir(old_cwd)
+        torch.optim.Adam.step = orig_step
+    out["meta.json"] = np.frombuffer(json.dumps({
+        "config": name, "args": args, "seed": cfg.get("seed", 1), "n_iter": n_iter, "threads": threads,
+        "n_images": cfg.get("n_images", 64), "torch": torch.__version__}).encode(), dtype=np.uint8).copy()
+    path = os.path.join(HERE, f"traj_{name}_t{threads}.npz")
+    np.savez_compressed(path, **out)
+    return path
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "--trajectory":
+        # --trajectory NAME [THREADS ...]: one fresh interpreter per thread count
+        from tests.golden.configs import TRAJ_ITERS, TRAJECTORIES
+        name = sys.argv[2]
+        threads = [int(t) for t in sys.argv[3:]] or list(TRAJECTORIES[name])
+        if len(threads) == 1:
+            print(name, threads[0], "->", run_trajectory(name, threads[0], TRAJ_ITERS), flush=True)
+        else:
+            import subprocess
+            for th in threads:
+                r = subprocess.run([sys.executable, os.path.abspath(__file__), "--trajectory", name, str(th)],
+                                   capture_output=True, text=True)
+                print(name, th, "ok" if r.returncode == 0 else "FAILED\n" + r.stderr[-2000:], flush=True)
+        sys.exit(0)
     names = sys.argv[1:] or PINNED
     if len(names) == 1:
         print(names[0], "->", run_config(names[0], CONFIGS[names[0]]), flush=True)

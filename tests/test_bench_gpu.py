@@ -1,5 +1,5 @@
 """bench.py's driver contract on the GPU box: the N=1 JSON line, and the N>1 path (torchrun,
-one process per rank, max-over-ranks timing) rehearsed with 2 gloo ranks on the one GPU
+one process per rank, max-over-ranks timing) rehearsed with 2 and 4 gloo ranks on the one GPU
 (RGAN_BENCH_BACKEND=gloo: RCCL refuses two ranks on one device).  Small workload (C1),
 few steps: this checks the code path and the line's keys, not the numbers."""
 import json
@@ -44,18 +44,35 @@ def test_bench_one_gpu_line():
     assert dpp["value"] > 0 and dpp["batched_D_step"] is True and dpp["launch_mode"] == "piecewise"
 
 
-def test_bench_two_rank_rehearsal():
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_multi_rank_rehearsal(world):
     env = _env()
     env["RGAN_BENCH_BACKEND"] = "gloo"
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                        "--master-addr", "127.0.0.1", "--master-port", "29613", "bench.py", "--gpus", "2",
-                        "--workload", "C1", "--extra=", "--steps", "2", "--warmup", "1"], cwd=ROOT, env=env,
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+                        "--master-addr", "127.0.0.1", "--master-port", str(29613 + world), "bench.py", "--gpus",
+                        str(world), "--workload", "C1", "--extra=", "--steps", "2", "--warmup", "1"], cwd=ROOT, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _line(r.stdout)  # rank 0 only prints
     assert KEYS <= set(d)
-    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 64
+    assert d["n_gpus"] == world and d["config"]["parallelism"] == f"dp{world}"
+    assert d["config"]["global_batch"] == 32 * world
     # C1 (24M parameters) under DP: HIP graphs cut at the collectives
     assert d["config"]["batched_D_step"] is True and d["config"]["launch_mode"] == "piecewise"
     assert d["config"]["graph_segments"] > 4
     assert "cpu_baseline" not in d and d["value"] > 0
+
+
+def test_bench_headline_two_rank_rehearsal():
+    """The headline C3 shard (366M parameters) under DP: eager launches with the gradient
+    buckets all-reduced asynchronously from the backward's hooks (gloo here, RCCL on the node)."""
+    env = _env()
+    env["RGAN_BENCH_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29640", "bench.py", "--gpus", "2",
+                        "--workload", "C3", "--extra=", "--steps", "2", "--warmup", "1"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 64 and d["config"]["launch_mode"] == "eager"
+    assert d["value"] > 0

@@ -1,4 +1,4 @@
-"""Data parallelism end to end on the HIP kernels: 2 ranks (gloo) sharing cuda:0.
+"""Data parallelism end to end on the HIP kernels: 2 and 4 ranks (gloo) sharing cuda:0.
 
 Each rank runs the real training step on its half of the global batch with SyncBN,
 distributed loss heads and the bucketed gradient all-reduce; the result must match the
@@ -53,12 +53,14 @@ def _capture(t, store):
 N_ITER = {"ralsgan_pac2": 1}
 
 
-def _run(name, world, rank, n_iter=None, device="cuda:0", batch_D=None):
+def _run(name, world, rank, n_iter=None, device="cuda:0", batch_D=None, batch_G=None):
     n_iter = n_iter or N_ITER.get(name, 2)
     from relativisticgan_amd.train import Trainer
     p = param_for(name)
     p.rgan_rng = "host"
     p.rgan_batch_D = batch_D
+    if batch_G is not None:
+        p.rgan_batch_G = batch_G
     t = Trainer(p, dataset_for(name).to(device))
     out = []
     for i in range(n_iter):
@@ -71,7 +73,7 @@ def _run(name, world, rank, n_iter=None, device="cuda:0", batch_D=None):
     return out
 
 
-def _worker(rank, world, port, name, path, sync_bn=True, n_iter=None, backend="gloo", batch_D=None):
+def _worker(rank, world, port, name, path, sync_bn=True, n_iter=None, backend="gloo", batch_D=None, batch_G=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dev = rank if backend == "nccl" else 0  # RCCL: one GPU per rank; gloo: both ranks on cuda:0
@@ -80,7 +82,7 @@ def _worker(rank, world, port, name, path, sync_bn=True, n_iter=None, backend="g
     from relativisticgan_amd import dp
     dp.setup(sync_bn=sync_bn)
     try:
-        res = _run(name, world, rank, n_iter, device=f"cuda:{dev}", batch_D=batch_D)
+        res = _run(name, world, rank, n_iter, device=f"cuda:{dev}", batch_D=batch_D, batch_G=batch_G)
         # gather the per-rank D outputs so rank 0 holds the global vectors
         for st in res:
             for k in ("y_pred", "y_pred_fake"):
@@ -99,12 +101,12 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-def _spawn(name, sync_bn=True, n_iter=None, backend="gloo", batch_D=None):
+def _spawn(name, sync_bn=True, n_iter=None, backend="gloo", batch_D=None, world=2, batch_G=None):
     path = os.path.join(tempfile.mkdtemp(), "dp.pt")
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, path, sync_bn, n_iter, backend, batch_D))
-             for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, name, path, sync_bn, n_iter, backend, batch_D, batch_G))
+             for r in range(world)]
     for pr in procs:
         pr.start()
     for pr in procs:
@@ -178,6 +180,37 @@ def test_dp2_per_shard_bn_matches_reference_data_parallel(name):
     slot, DataParallel would chunk the 2B z rows."""
     dpres = _spawn(name, sync_bn=False, n_iter=1)
     ref = _oracle_data_parallel(name, 2)
+    _compare(name, dpres, ref)
+
+
+@pytest.mark.parametrize("name", ["ralsgan", "wgangp", "rahinge_spectral"])
+def test_dp4_matches_single_process(name):
+    """4 ranks (2 samples each of the global batch of 8) with SyncBN: the rank-ordered merge
+    of 4 ranks' BatchNorm moments (dp.py all-gather + rgan_bn_finalize), bucket sequencing
+    across 4 ranks and the 4-way distributed heads == the single-process global-batch step."""
+    single = _run(name, 1, 0)
+    dpres = _spawn(name, world=4)
+    _compare(name, dpres, single)
+
+
+@pytest.mark.parametrize("name", ["ralsgan", "rasgan"])
+def test_dp4_per_shard_bn_matches_reference_data_parallel(name):
+    """Per-shard BatchNorm over 4 ranks vs the oracle's data_parallel over 4 replicas
+    (DataParallel's scatter of the batch into 4 chunks, GLI:393-394, 455-456)."""
+    dpres = _spawn(name, sync_bn=False, n_iter=1, world=4)
+    ref = _oracle_data_parallel(name, 4)
+    _compare(name, dpres, ref)
+
+
+@pytest.mark.parametrize("sync_bn", [True, False])
+def test_dp2_unbatched_G_step(sync_bn):
+    """--rgan_batch_G False under data parallelism (the G step's D(G(z)) and D(x) as separate
+    calls, heads 5-8) against the same references as the batched default: the single process
+    (SyncBN) or the oracle's data_parallel (per-shard BN).  With the batched default covered by
+    the tests above, both G-step forms are pinned under DP, with and without SyncBN."""
+    name = "ralsgan"
+    dpres = _spawn(name, sync_bn=sync_bn, n_iter=None if sync_bn else 1, batch_G=False)
+    ref = _run(name, 1, 0) if sync_bn else _oracle_data_parallel(name, 2)
     _compare(name, dpres, ref)
 
 
