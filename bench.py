@@ -176,6 +176,22 @@ def cpu_baseline(loss_D, size, batch, h, spectral, seconds_hint, arch=0, min_ite
                       f"torch {torch.__version__} CPU fp32, {threads} threads on {cpus['model']}"}
 
 
+def restatement_check():
+    """the oracle timed against the unmodified reference script on the same host
+    (tests/golden/time_reference.py, run in the build container -- the reference does not
+    travel to the GPU box): the committed result files, oracle / reference seconds per
+    iteration within +-10 %."""
+    import glob
+    out = []
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "round*_cpu_reference_vs_oracle_*.json"))):
+        with open(f) as fh:
+            d = json.load(fh)
+        out.append({k: d.get(k) for k in ("config", "threads", "reference_s_per_iter", "oracle_s_per_iter",
+                                           "oracle_over_reference", "within_10pct")}
+                   | {"source": os.path.relpath(f, ROOT)})
+    return out
+
+
 def run_workload(name, steps, warmup, world, args, K, emu=False, dp_path=False):
     """Train `steps` timed iterations of workload `name` (after `warmup`); returns the
     measurement (max over ranks).  emu: forward / data-gradient GEMMs on bf16x6.  dp_path:
@@ -322,6 +338,85 @@ def roofline_of(res, workload):
                             "kernels": prof["kernels"]}}
 
 
+HBM_PEAK = 8.0e12  # MI355X_MICROARCH.md: HBM3E peak (spec)
+
+
+def hbm_kernels(name, K, reps=10):
+    """achieved HBM GB/s of the HBM-bound kernels of the step (BatchNorm
+    apply / backward, the one-launch small-layer BN backward, Adam, activation backward) at
+    the workload's own layer shapes: algorithmic bytes per launch (BN apply
+    8 B/elem, BN backward 8 + 12 B/elem, Adam 28 B/param, act' 12 B/elem) / the launch's
+    average duration (torch.cuda.Event pairs on the launch stream, reps launches after 2)."""
+    loss_D, size, bpg, h = WORKLOADS[name]
+    if ARCH.get(name, 0) != 0:
+        return None
+    torch.manual_seed(0)
+    dev = "cuda"
+    B2 = 2 * bpg  # the batched D pass: both calls' halves in one launch
+    c_big, hw_big = 2 * h, size // 4  # D's first BatchNorm layer (the largest)
+    c_small = h * (size // 8)  # D's last BatchNorm layer (4 x 4): h * S / 8 channels
+
+    def nhwc(B, C, H):
+        return K.empty_nhwc(B, C, H, H, dev).normal_()
+
+    def timed(fn):
+        for _ in range(2):
+            fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps * 1000.0  # us
+
+    out = []
+
+    def add(kernel, shape, nbytes, us):
+        gbs = nbytes / us / 1e3
+        out.append({"kernel": kernel, "shape": shape, "bytes_per_launch": nbytes, "us": us, "GB_s": gbs,
+                    "frac_of_hbm_peak": gbs * 1e9 / HBM_PEAK})
+
+    y = nhwc(B2, c_big, hw_big)
+    C = c_big
+    gamma, beta = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
+    stats = torch.cat([torch.randn(2, C, device=dev), torch.rand(2, C, device=dev) + 0.5], 1)
+    a = torch.empty_like(y)
+    n = y.numel()
+    add("bn_apply_segments (normalise + LeakyReLU)", list(y.shape), 8 * n,
+        timed(lambda: K.bn_apply_segments(y, stats, gamma, beta, "lrelu", 0.2, out=a)))
+    da = torch.randn_like(y)
+    dy = torch.empty_like(y)
+    add("bn_backward_segments (sums + merge + apply, act')", list(y.shape), 20 * n,
+        timed(lambda: K.bn_backward_segments(da, y, stats, gamma, beta, "lrelu", 0.2, True, True, dy)))
+    add("act_backward (LeakyReLU')", list(y.shape), 12 * n, timed(lambda: K.act_backward(da, a, "lrelu", 0.2)))
+    ys = nhwc(B2, c_small, 4)
+    Cs = c_small
+    gs, bs = torch.rand(Cs, device=dev) + 0.5, torch.randn(Cs, device=dev)
+    sts = torch.cat([torch.randn(2, Cs, device=dev), torch.rand(2, Cs, device=dev) + 0.5], 1)
+    das, dys = torch.randn_like(ys), torch.empty_like(ys)
+    add("bn_bwd_small (4x4 layer under D's dense head, one launch)", list(ys.shape), 20 * ys.numel(),
+        timed(lambda: K.bn_backward_segments(das, ys, sts, gs, bs, "lrelu", 0.2, True, True, dys)))
+    # Adam over a D-sized parameter set (the conv weights of the workload's D)
+    shapes, cin, s = [], 3, size
+    cout = h
+    while s > 4:
+        shapes.append((cout, cin, 4, 4))
+        cin, cout, s = cout, cout * 2, s // 2
+    shapes.append((1, cin, 4, 4))
+    ps = [torch.randn(sh, device=dev) * 0.02 for sh in shapes]
+    gs_ = [torch.randn_like(p) for p in ps]
+    ms, vs = [torch.zeros_like(p) for p in ps], [torch.zeros_like(p) for p in ps]
+    hyper = torch.tensor([1e-4, 0.5, 0.999, 1e-8, 0.0, 0, 0, 0], dtype=torch.float64, device=dev)
+    step = torch.zeros(1, device=dev)
+    npar = sum(p.numel() for p in ps)
+    add("adam (multi-tensor, D's conv weights)", [npar], 28 * npar, timed(lambda: K.adam(ps, gs_, ms, vs, hyper, step)))
+    del y, a, da, dy, ys, das, dys, ps, gs_, ms, vs
+    torch.cuda.empty_cache()
+    return {"peak_GB_s": HBM_PEAK / 1e9, "note": "algorithmic bytes (SURVEY §8(d)) / HIP-event launch time",
+            "kernels": out}
+
+
 def describe(res):
     arch = "arch1 (standard CNN)" if res["arch"] == 1 else "arch0"
     return (f"{res['name']}: loss_D {res['loss_D']} DCGAN {arch} {res['size']}x{res['size']}, h={res['h']}, "
@@ -350,6 +445,7 @@ def main():
     ap.add_argument("--no-dp-path", action="store_true",
                     help="skip the N=1 runs of the data-parallel launch mode (dp_path_n1)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-hbm", action="store_true", help="skip the HBM-bound kernels' GB/s table (hbm_kernels)")
     ap.add_argument("--sync-bn", action="store_true",
                     help="SyncBN over ranks (default: per-shard BN = the reference's DataParallel)")
     args = ap.parse_args()
@@ -420,9 +516,12 @@ def main():
             "gemm_arith": "forward / data-gradient conv GEMMs: fp32 operands split exactly into 3 bf16 "
                           "pieces, 6 bf16 MFMA products accumulated in fp32 (weight gradients: fp32 MFMA)",
             "roofline": roofline_of(emu_res, args.workload)}
+    if world == 1 and not args.no_hbm:
+        out["hbm_kernels"] = hbm_kernels(args.workload, K)
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(res["loss_D"], res["size"], res["bpg"], res["h"], res["spectral"],
                                            args.cpu_seconds, arch=res["arch"])
+        out["cpu_baseline"]["restatement_check"] = restatement_check()
     print(json.dumps(out), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()

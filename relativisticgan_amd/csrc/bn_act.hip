@@ -648,125 +648,140 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ da
 
 // Small-P BatchNorm backward (the 4x4 layer under D's closing dense layer: 512 rows per
 // call at B = 32): the sums, their merge and the apply in one launch instead of three.
-// Block = 4 channels (one float4 quad) x 256 row lanes; lane r sums rows r, r + 256, ... of
-// each segment in double (bn_bwd_partial's terms), a fixed LDS tree adds the 256 lanes, then
-// every lane applies its rows with bn_bwd_apply's constants and formula (row loads issued 4
-// ahead in both passes).  NSEG 2: rows [0, Ps) use stats / sums row 0, [Ps, 2 Ps) row 1; the
-// affine gradients are the segments' sum.
-constexpr int BNS_LANES = 256, BNS_CH = 4;
-constexpr long long BNS_MAX_ROWS = 2048;  // rows per segment: <= 8 per lane
+// Block = 16 channels (one 64-B piece of every NHWC row: four lanes x float4) x 128 row
+// lanes (512 threads); the block holding the other half of those 128-B lines runs on the same
+// XCD (a 4-channel block shared every line with three other blocks, usually on other XCDs).
+// Lane (r, q) reads rows r, r + 128, ... of each segment -- the first BNS_RC rows per
+// segment kept in registers for the apply pass (no second read; rows past them are read
+// again) -- and sums bn_bwd_partial's terms in double; the 16 row lanes of a wave are added
+// by a fixed xor butterfly, the 8 waves by a fixed LDS sum, then every lane applies its rows
+// with bn_bwd_apply's constants and formula.  NSEG 2: rows [0, Ps) use stats / sums row 0,
+// [Ps, 2 Ps) row 1; the affine gradients are the segments' sum.
+constexpr int BNS_LANES = 128, BNS_CH = 16, BNS_THREADS = 512;
+constexpr long long BNS_MAX_ROWS = 2048;  // rows per segment
 template <int NSEG>
-__global__ __launch_bounds__(256) void bn_bwd_small(const float* __restrict__ da, const float* __restrict__ y,
-                                                    long long Ps, int C, const float* __restrict__ stats,
-                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                    int act, float alpha, float* __restrict__ dy, float* dgamma,
-                                                    float* dbeta) {
-  __shared__ double sh[2][NSEG][BNS_LANES][BNS_CH];
-  const int r = threadIdx.x, c0 = blockIdx.x * BNS_CH;
+__global__ __launch_bounds__(BNS_THREADS) void bn_bwd_small(const float* __restrict__ da, const float* __restrict__ y,
+                                                            long long Ps, int C, const float* __restrict__ stats,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, int act, float alpha,
+                                                            float* __restrict__ dy, float* dgamma, float* dbeta) {
+  constexpr int RC = 8 / NSEG;  // rows per segment cached in registers
+  constexpr int NW = BNS_THREADS / 64;
+  __shared__ double sh[2][NSEG][NW][BNS_CH];
+  const int tid = threadIdx.x, q = tid & 3, r = tid >> 2, lane = tid & 63, wv = tid >> 6;
+  // XCD-aware channel groups: blocks are dispatched round-robin over the 8 XCDs, so group
+  // (b % 8) * (nb / 8) + b / 8 puts consecutive 16-channel groups -- the two 64-B halves of
+  // every 128-B line -- on one XCD (one L2 fetch per line)
+  const int nb = gridDim.x;
+  const int grp = (nb % 8 == 0) ? (int)(blockIdx.x % 8) * (nb / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  const int c0 = grp * BNS_CH + 4 * q;
   float mean[NSEG][4], al[NSEG][4], be[NSEG][4], inv[NSEG][4];
 #pragma unroll
   for (int sg = 0; sg < NSEG; ++sg)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int k = 0; k < 4; ++k) {
       const float* st = stats + (size_t)sg * 2 * C;
-      const int c = c0 + q;
-      inv[sg][q] = st[C + c];
-      mean[sg][q] = st[c];
-      al[sg][q] = (gamma ? gamma[c] : 1.f) * inv[sg][q];
-      be[sg][q] = (beta ? beta[c] : 0.f) - mean[sg][q] * al[sg][q];
+      const int c = c0 + k;
+      inv[sg][k] = st[C + c];
+      mean[sg][k] = st[c];
+      al[sg][k] = (gamma ? gamma[c] : 1.f) * inv[sg][k];
+      be[sg][k] = (beta ? beta[c] : 0.f) - mean[sg][k] * al[sg][k];
     }
+  float4 cv[NSEG][RC], cg[NSEG][RC];
+#pragma unroll
+  for (int sg = 0; sg < NSEG; ++sg) {
+    const long long rb = (long long)sg * Ps;
+#pragma unroll
+    for (int j = 0; j < RC; ++j) {  // every cached row's loads in flight together
+      const long long p = r + (long long)j * BNS_LANES;
+      if (p < Ps) {
+        cv[sg][j] = *reinterpret_cast<const float4*>(y + (rb + p) * C + c0);
+        cg[sg][j] = *reinterpret_cast<const float4*>(da + (rb + p) * C + c0);
+      }
+    }
+  }
+  auto terms = [&](int sg, const float4& v4, const float4& g4, double (&s1)[4], double (&s2)[4]) {
+    const float vv[4] = {v4.x, v4.y, v4.z, v4.w}, gg[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double gz = (double)(gg[k] * act_grad_from_in(vv[k] * al[sg][k] + be[sg][k], act, alpha));
+      s1[k] += gz;
+      s2[k] += gz * (double)(vv[k] - mean[sg][k]);
+    }
+  };
 #pragma unroll
   for (int sg = 0; sg < NSEG; ++sg) {
     double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
     const long long rb = (long long)sg * Ps;
-    for (long long p = r; p < Ps; p += 4 * BNS_LANES) {
-      float4 v[4], g[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const long long pp = p + u * BNS_LANES;
-        if (pp < Ps) {
-          v[u] = *reinterpret_cast<const float4*>(y + (rb + pp) * C + c0);
-          g[u] = *reinterpret_cast<const float4*>(da + (rb + pp) * C + c0);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (p + u * BNS_LANES < Ps) {
-          const float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w}, gg[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const double gz = (double)(gg[q] * act_grad_from_in(vv[q] * al[sg][q] + be[sg][q], act, alpha));
-            s1[q] += gz;
-            s2[q] += gz * (double)(vv[q] - mean[sg][q]);
-          }
-        }
-      }
+    for (int j = 0; j < RC; ++j)
+      if (r + (long long)j * BNS_LANES < Ps) terms(sg, cv[sg][j], cg[sg][j], s1, s2);
+    for (long long p = r + (long long)RC * BNS_LANES; p < Ps; p += BNS_LANES) {
+      const float4 v4 = *reinterpret_cast<const float4*>(y + (rb + p) * C + c0);
+      const float4 g4 = *reinterpret_cast<const float4*>(da + (rb + p) * C + c0);
+      terms(sg, v4, g4, s1, s2);
     }
+    // the wave's 16 row lanes of each channel: fixed xor butterfly over lane bits 2..5
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      sh[0][sg][r][q] = s1[q];
-      sh[1][sg][r][q] = s2[q];
-    }
+    for (int o = 4; o < 64; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s1[k] += __shfl_xor(s1[k], o);
+        s2[k] += __shfl_xor(s2[k], o);
+      }
+    if (lane < 4)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        sh[0][sg][wv][4 * q + k] = s1[k];
+        sh[1][sg][wv][4 * q + k] = s2[k];
+      }
   }
   __syncthreads();
-  for (int h = BNS_LANES / 2; h > 0; h >>= 1) {
-    if (r < h) {
-#pragma unroll
-      for (int sg = 0; sg < NSEG; ++sg)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          sh[0][sg][r][q] += sh[0][sg][r + h][q];
-          sh[1][sg][r][q] += sh[1][sg][r + h][q];
-        }
-    }
-    __syncthreads();
-  }
   const double inv_pg = 1.0 / (double)Ps;
   float k1[NSEG][4], k2[NSEG][4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
+  for (int k = 0; k < 4; ++k) {
     float db = 0.f, dg = 0.f;
 #pragma unroll
     for (int sg = 0; sg < NSEG; ++sg) {
-      const double S1 = sh[0][sg][0][q], S2 = sh[1][sg][0][q], iv = (double)inv[sg][q];
-      k1[sg][q] = (float)(S1 * inv_pg);
-      k2[sg][q] = (float)(S2 * iv * iv * inv_pg);
+      double S1 = sh[0][sg][0][4 * q + k], S2 = sh[1][sg][0][4 * q + k];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) {  // waves in order
+        S1 += sh[0][sg][w][4 * q + k];
+        S2 += sh[1][sg][w][4 * q + k];
+      }
+      const double iv = (double)inv[sg][k];
+      k1[sg][k] = (float)(S1 * inv_pg);
+      k2[sg][k] = (float)(S2 * iv * iv * inv_pg);
       const float dbs = (float)S1, dgs = (float)(S2 * iv);
       db = sg == 0 ? dbs : db + dbs;
       dg = sg == 0 ? dgs : dg + dgs;
     }
     if (r == 0) {
-      if (dbeta) dbeta[c0 + q] = db;
-      if (dgamma) dgamma[c0 + q] = dg;
+      if (dbeta) dbeta[c0 + k] = db;
+      if (dgamma) dgamma[c0 + k] = dg;
     }
   }
+  auto apply = [&](int sg, const float4& v4, const float4& g4, long long row) {
+    float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+    const float gg[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float gz = gg[k] * act_grad_from_in(vv[k] * al[sg][k] + be[sg][k], act, alpha);
+      vv[k] = al[sg][k] * (gz - k1[sg][k] - (vv[k] - mean[sg][k]) * k2[sg][k]);
+    }
+    *reinterpret_cast<float4*>(dy + row * C + c0) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+  };
 #pragma unroll
   for (int sg = 0; sg < NSEG; ++sg) {
     const long long rb = (long long)sg * Ps;
-    for (long long p = r; p < Ps; p += 4 * BNS_LANES) {
-      float4 v[4], g[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const long long pp = p + u * BNS_LANES;
-        if (pp < Ps) {
-          v[u] = *reinterpret_cast<const float4*>(y + (rb + pp) * C + c0);
-          g[u] = *reinterpret_cast<const float4*>(da + (rb + pp) * C + c0);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const long long pp = p + u * BNS_LANES;
-        if (pp < Ps) {
-          float vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-          const float gg[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float gz = gg[q] * act_grad_from_in(vv[q] * al[sg][q] + be[sg][q], act, alpha);
-            vv[q] = al[sg][q] * (gz - k1[sg][q] - (vv[q] - mean[sg][q]) * k2[sg][q]);
-          }
-          *reinterpret_cast<float4*>(dy + (rb + pp) * C + c0) = make_float4(vv[0], vv[1], vv[2], vv[3]);
-        }
-      }
+    for (int j = 0; j < RC; ++j)
+      if (r + (long long)j * BNS_LANES < Ps) apply(sg, cv[sg][j], cg[sg][j], rb + r + (long long)j * BNS_LANES);
+    for (long long p = r + (long long)RC * BNS_LANES; p < Ps; p += BNS_LANES) {
+      const float4 v4 = *reinterpret_cast<const float4*>(y + (rb + p) * C + c0);
+      const float4 g4 = *reinterpret_cast<const float4*>(da + (rb + p) * C + c0);
+      apply(sg, v4, g4, rb + p);
     }
   }
 }
@@ -844,9 +859,11 @@ extern "C" int rgan_bn_backward_segments(const float* da, const float* y, long l
   if (Ps <= BNS_MAX_ROWS && C % BNS_CH == 0 && dense_nhwc(C, 1, C, y) && dense_nhwc(C, 1, C, da) &&
       dense_nhwc(C, 1, C, dy)) {  // small layers: one launch
     if (nseg == 1)
-      bn_bwd_small<1><<<C / BNS_CH, 256, 0, s>>>(da, y, Ps, C, stats, gamma, beta, act, act_alpha, dy, dgamma, dbeta);
+      bn_bwd_small<1><<<C / BNS_CH, BNS_THREADS, 0, s>>>(da, y, Ps, C, stats, gamma, beta, act, act_alpha, dy, dgamma,
+                                                         dbeta);
     else
-      bn_bwd_small<2><<<C / BNS_CH, 256, 0, s>>>(da, y, Ps, C, stats, gamma, beta, act, act_alpha, dy, dgamma, dbeta);
+      bn_bwd_small<2><<<C / BNS_CH, BNS_THREADS, 0, s>>>(da, y, Ps, C, stats, gamma, beta, act, act_alpha, dy, dgamma,
+                                                         dbeta);
     RGAN_CHECK_LAUNCH();
     return 0;
   }
@@ -945,8 +962,8 @@ extern "C" int rgan_bn_backward(const float* da, long long dsp, long long dsc, c
   RGAN_REQUIRE(partial && P > 0 && C > 0);
   if (P <= BNS_MAX_ROWS && C % BNS_CH == 0 && dense_nhwc(sp, sc, C, y) && dense_nhwc(dsp, dsc, C, da) &&
       dense_nhwc(ysp, ysc, C, dy) && stats && dy) {  // small layers: one launch
-    bn_bwd_small<1><<<C / BNS_CH, 256, 0, (hipStream_t)stream>>>(da, y, P, C, stats, gamma, beta, act, act_alpha, dy,
-                                                                 dgamma, dbeta);
+    bn_bwd_small<1><<<C / BNS_CH, BNS_THREADS, 0, (hipStream_t)stream>>>(da, y, P, C, stats, gamma, beta, act,
+                                                                         act_alpha, dy, dgamma, dbeta);
     RGAN_CHECK_LAUNCH();
     return 0;
   }

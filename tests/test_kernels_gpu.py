@@ -946,7 +946,7 @@ def test_bn_two_segments_one_launch(K):
     assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2) and int(n2.item()) == 2
 
 
-@pytest.mark.parametrize("C,B,H", [(64, 8, 32), (64, 8, 16), (1024, 64, 4)])
+@pytest.mark.parametrize("C,B,H", [(64, 8, 32), (64, 8, 16), (1024, 64, 4), (4096, 64, 4), (64, 16, 16), (36, 8, 8)])
 def test_bn_backward_two_segments(K, C, B, H):
     """rgan_bn_backward_segments (both calls of the batched pass at once) == the per-call
     backward sums + apply: dy and the summed affine gradients -- bitwise for the three-launch

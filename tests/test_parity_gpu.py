@@ -478,6 +478,7 @@ def test_step_parity_teacher_forced(name, emu):
     from relativisticgan_amd.train import Trainer
     n_iter = CONFIGS[name]["args"].get("n_iter", 3)
     p, init, steps = _oracle_for(name, n_iter)
+    print(f"[parity {name}] oracle fp32 replay done", flush=True)
     p = copy.deepcopy(p)
     p.rgan_rng = "host"
     prev = kernels.set_gemm_emulation(emu)
@@ -493,7 +494,9 @@ def test_step_parity_teacher_forced(name, emu):
         errs, report, flips_all, premise = [], [], [], []
         for st in steps:
             got = gpu_step(t, st)
+            print(f"[parity {name}{'-bf16x6' if emu else ''}] it{st['i']}: GPU step done", flush=True)
             exact = _exact_for(name, st)
+            print(f"[parity {name}] it{st['i']}: exact fp64 step done", flush=True)
             recs, perrs = check_premise(got["masks"], exact)
             premise += [dict(r, it=st["i"]) for r in recs]
             errs += [f"it{st['i']} premise: {e}" for e in perrs]
