@@ -23,6 +23,7 @@ import torch
 import torch.nn as nn
 
 from . import autograd as AG
+from . import ops
 from .autograd import ConvLayerFn, LayerSpec
 from .kernels import ConvGeom, spectral_power, spectral_power_batch
 
@@ -175,9 +176,15 @@ class _Layer:
         that carry an output gradient (ConvLayerFn); ``link_in`` / ``link_out``: the
         autograd.LayerLink to the layer below / above in the same chain call."""
         conv, bn = self.conv, self.bn
-        w = self.weight()
         if self.in_view is not None:
             h = h.reshape(h.shape[0], *self.in_view)
+        if ops.tracing(h):
+            # traced (torch.export / torch.compile): the layer as rgan:: operators (ops.py)
+            if segs != 1 or out is not None:
+                raise NotImplementedError("traced nets: one forward call per net (no batched segments)")
+            res = ops.layer_forward(self, h, training)
+            return res.reshape(res.shape[0], *self.out_view) if self.out_view is not None else res
+        w = self.weight()
         if self.spec.spectral and sn is None:
             with torch.no_grad():
                 inv_sigma = spectral_power(w.detach(), conv.weight_u, conv.weight_v, conv.geom.transposed,
@@ -231,6 +238,10 @@ class _Net(nn.Module):
         AG.TRACE_NET = self._tag
         h = x
         last = len(self._plan) - 1
+        if ops.tracing(x):  # rgan:: operators per layer (ops.layer_forward): no fused hand-offs
+            for layer in self._plan:
+                h = layer.run(h, self.training)
+            return h
         sns = self._spectral()
         links = self._links()
         for li, layer in enumerate(self._plan):
