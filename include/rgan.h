@@ -320,6 +320,13 @@ int rgan_act_backward_ex(const float* da, const float* a, const float* add, long
 int rgan_channel_sum(const float* t, long long P, int C, long long sp, long long sc,
                      float* out, int accumulate, void* partial, void* stream);
 
+/* dgamma (+)= (float)(sums[1][c] * invstd[c]), dbeta (+)= (float)sums[0][c] (accumulate != 0:
+ * added) from [2][C] BatchNorm backward sums (rgan_bn_backward_sums) and stats [mean; invstd]:
+ * the affine gradients from a rank's LOCAL sums under SyncBN, where the normalisation uses the
+ * all-reduced ones (either output nullable). */
+int rgan_bn_affine_grads(const double* sums, const float* stats, int C, float* dgamma, float* dbeta,
+                         int accumulate, void* stream);
+
 /* ---- loss heads (GLI:481-484, 592-644, 686-709) ----
  * kind = --loss_D (1..8); side 0 = D-real (heads 1-4) / D (heads 5-8), 1 = D-fake
  * (heads 1-4), 2 = G.  r, f: [n] (either nullable per head).  loss: device float[1];

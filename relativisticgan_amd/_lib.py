@@ -91,6 +91,7 @@ _SIGS = {
                                  c_vp, c_ll, c_ll, c_vp, c_vp, c_vp, c_vp]),
     "rgan_bn_backward_apply_ex": (c_int, [c_vp, c_ll, c_ll, c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp, c_int,
                                           c_f, c_vp, c_ll, c_vp, c_vp, c_ll, c_ll, c_vp, c_vp, c_int, c_vp]),
+    "rgan_bn_affine_grads": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]),
     "rgan_bn_dd_partial_bytes": (c_sz, [c_ll, c_int]),
     "rgan_bn_dd_sums": (c_int, [c_vp, c_vp, c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp, c_int, c_f, c_int, c_vp,
                                 c_ll, c_vp, c_vp, c_vp]),

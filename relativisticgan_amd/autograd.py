@@ -371,10 +371,9 @@ class ConvLayerFn(torch.autograd.Function):
                 # dgamma/dbeta stay shard-local (from the pre-all-reduce sums): the bucketed
                 # gradient all-reduce sums them like every other parameter gradient
                 C = y.shape[1]
-                if ng and gamma is not None:
-                    dgamma = (sums[C:] * stats[C:2 * C].double()).float()
-                if nbeta and beta is not None:
-                    dbeta = sums[:C].float()
+                dgamma = torch.empty(C, dtype=torch.float32, device=y.device) if ng and gamma is not None else None
+                dbeta = torch.empty(C, dtype=torch.float32, device=y.device) if nbeta and beta is not None else None
+                K.bn_affine_grads(sums, stats, C, dgamma, dbeta)
                 dp.all_reduce_sum(sums)
                 dy, _, _ = K.bn_backward_apply(da_c, y, stats, gamma, beta, spec.act, spec.alpha, sums,
                                                P * dp.world(), need_affine=False)

@@ -839,6 +839,27 @@ extern "C" int rgan_bn_backward_apply_ex(const float* da, long long dsp, long lo
   return 0;
 }
 
+// dgamma (+)= (float)(sum g (y - mean) * invstd), dbeta (+)= (float)sum g from [2][C] sums --
+// the affine gradients bn_bwd_apply writes, from a rank's LOCAL sums under SyncBN (the
+// normalisation uses the all-reduced sums; the bucketed gradient all-reduce sums these)
+__global__ void bn_affine_from_sums(const double* __restrict__ sums, const float* __restrict__ stats, int C,
+                                    float* dgamma, float* dbeta, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float db = (float)sums[c], dg = (float)(sums[C + c] * (double)stats[C + c]);
+  if (dbeta) dbeta[c] = accumulate ? dbeta[c] + db : db;
+  if (dgamma) dgamma[c] = accumulate ? dgamma[c] + dg : dg;
+}
+
+extern "C" int rgan_bn_affine_grads(const double* sums, const float* stats, int C, float* dgamma, float* dbeta,
+                                    int accumulate, void* stream) {
+  RGAN_REQUIRE(sums && stats && C > 0);
+  if (!dgamma && !dbeta) return 0;
+  bn_affine_from_sums<<<ceil_div(C, 256), 256, 0, (hipStream_t)stream>>>(sums, stats, C, dgamma, dbeta, accumulate);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int rgan_bn_backward_apply(const float* da, long long dsp, long long dsc, const float* y, long long P,
                                       int C, long long sp, long long sc, const float* stats, const float* gamma,
                                       const float* beta, int act, float act_alpha, const double* sums,

@@ -33,8 +33,12 @@ The [adjoint; forward] operand pairs live in one [2B, ...] buffer per layer, wri
 place by the producing kernels (no concatenation copies).  Cost: 6 D-forward-equivalents
 of MFMA work, the minimum the algebra allows.
 
-SyncBN (--rgan_sync_bn True) keeps the autograd composite path of autograd.py (its
-second-order BN sums would need their own cross-rank reductions).
+SyncBN (--rgan_sync_bn True): every BatchNorm sum of the three sweeps (the first
+backward's, the double backward's stage-1 / stage-2 sums, sweep 2's) is all-reduced before
+it normalises anything and the kernels get the global pixel count, while the affine
+gradients come from the rank's own (pre-all-reduce) sums -- the bucketed gradient
+all-reduce then sums them like every other gradient (include/rgan.h rgan_bn_dd_apply's
+*_local sums, rgan_bn_affine_grads).  No ATen arithmetic under either BatchNorm mode.
 """
 import torch
 
@@ -69,8 +73,16 @@ class _Rec:
 
 def supported(D):
     """The native engine covers every D of the reference (arch 0/1, spectral, BN, any
-    activation); SyncBN stays on the composite path."""
-    return not dp.sync_bn()
+    activation), with per-shard BatchNorm or SyncBN."""
+    return True
+
+
+def _global(sums):
+    """(global sums, local sums): the SyncBN all-reduce of a rank's BatchNorm sums (a copy;
+    the local ones give the affine gradients), or the sums themselves."""
+    if not dp.sync_bn():
+        return sums, sums
+    return dp.all_reduce_sum(sums.clone()), sums
 
 
 class GPEngine:
@@ -150,10 +162,10 @@ class GPEngine:
                 C, Ho, Wo = r.a.shape[1], r.a.shape[2], r.a.shape[3]
                 r.yc = empty_nhwc(2 * B, C, Ho, Wo, self.dev)
             if spec.bn:
-                r.fs, dh_c = K.bn_backward_sums(dh, r.y, r.stats, r.gamma, r.beta, spec.act, spec.alpha)
-                P = r.y.shape[0] * r.y.shape[2] * r.y.shape[3]
-                r.dy, _, _ = K.bn_backward_apply(dh_c, r.y, r.stats, r.gamma, r.beta, spec.act, spec.alpha, r.fs, P,
-                                                 need_affine=False, out=r.yc[:B])
+                fs, dh_c = K.bn_backward_sums(dh, r.y, r.stats, r.gamma, r.beta, spec.act, spec.alpha)
+                r.fs, _ = _global(fs)
+                r.dy, _, _ = K.bn_backward_apply(dh_c, r.y, r.stats, r.gamma, r.beta, spec.act, spec.alpha, r.fs,
+                                                 self._P(r), need_affine=False, out=r.yc[:B])
             elif spec.act != "none":
                 r.fs = None
                 r.dy = K.act_backward_ex(dh, r.a, spec.act, spec.alpha, out=r.yc[:B])
@@ -180,12 +192,15 @@ class GPEngine:
             w = r.w.detach()
             if spec.bn:
                 a_adj = K.conv_fwd(ubar, w, spec.geom, wscale=r.wscale, cache=True)
-                P = r.y.shape[0] * r.y.shape[2] * r.y.shape[3]
-                s1 = K.bn_dd_sums(a_adj, r.y, r.dh, r.stats, r.gamma, r.beta, spec.act, spec.alpha, 1)
-                s2 = (K.bn_dd_sums(a_adj, r.y, r.dh, r.stats, r.gamma, r.beta, spec.act, spec.alpha, 2, s1, P)
-                      if has2 else None)
+                P = self._P(r)
+                s1, s1_loc = _global(K.bn_dd_sums(a_adj, r.y, r.dh, r.stats, r.gamma, r.beta, spec.act, spec.alpha, 1))
+                s2, s2_loc = (_global(K.bn_dd_sums(a_adj, r.y, r.dh, r.stats, r.gamma, r.beta, spec.act, spec.alpha,
+                                                   2, s1, P)) if has2 else (None, None))
+                sync = dp.sync_bn()
                 adj, ydir = K.bn_dd_apply(a_adj, r.y, r.dh, r.stats, r.gamma, r.beta, spec.act, spec.alpha, r.fs,
-                                          s1, s2, P, adj_dh=nxt, ydir=r.yc[B:], need_adj=not last,
+                                          s1, s2, P, s1_local=s1_loc if sync else None,
+                                          s2_local=s2_loc if sync else None, adj_dh=nxt, ydir=r.yc[B:],
+                                          need_adj=not last,
                                           dgamma2=_grad_buf(r.gamma) if r.gamma is not None else None,
                                           dbeta2=_grad_buf(r.beta) if r.beta is not None else None,
                                           accumulate_affine=True)
@@ -208,12 +223,16 @@ class GPEngine:
             if gbar is not None:
                 if spec.bn:
                     sums, g_c = K.bn_backward_sums(gbar, r.y, r.stats, r.gamma, r.beta, spec.act, spec.alpha)
-                    P = r.y.shape[0] * r.y.shape[2] * r.y.shape[3]
-                    ybar = K.bn_backward_apply_ex(g_c, r.y, r.stats, r.gamma, r.beta, spec.act, spec.alpha, sums, P,
-                                                  add=ydir, out=r.yc[B:],
-                                                  dgamma=_grad_buf(r.gamma) if r.gamma is not None else None,
-                                                  dbeta=_grad_buf(r.beta) if r.beta is not None else None,
+                    sums, sums_loc = _global(sums)
+                    dgb = _grad_buf(r.gamma) if r.gamma is not None else None
+                    dbb = _grad_buf(r.beta) if r.beta is not None else None
+                    sync = dp.sync_bn()
+                    ybar = K.bn_backward_apply_ex(g_c, r.y, r.stats, r.gamma, r.beta, spec.act, spec.alpha, sums,
+                                                  self._P(r), add=ydir, out=r.yc[B:],
+                                                  dgamma=None if sync else dgb, dbeta=None if sync else dbb,
                                                   accumulate_affine=True)
+                    if sync:  # the affine gradients from this rank's own sums
+                        K.bn_affine_grads(sums_loc, r.stats, r.y.shape[1], dgb, dbb, accumulate=True)
                 elif spec.act != "none":
                     ybar = K.act_backward_ex(gbar, r.a, spec.act, spec.alpha, add=ydir, out=r.yc[B:])
                 else:
@@ -223,6 +242,13 @@ class GPEngine:
             self._weight_grad(li, r, ybar)
             gbar = (K.conv_dgrad(ybar, r.w.detach(), spec.geom, tuple(r.h_in.shape), wscale=r.wscale,
                                  like=r.h_in, cache=True) if (ybar is not None and li > 0) else None)
+
+    @staticmethod
+    def _P(r):
+        """Pixels per channel the layer's BatchNorm normalises over: the rank's shard, or the
+        global batch under SyncBN."""
+        P = r.y.shape[0] * r.y.shape[2] * r.y.shape[3]
+        return P * dp.world() if dp.sync_bn() else P
 
     def _weight_grad(self, li, r, ybar):
         """dW_l += wgrad(ubar_{l-1}, dy_l) [+ wgrad(h_{l-1}, ybar_l)] as one GEMM over the pair

@@ -584,6 +584,13 @@ def bn_backward_apply(da, y, stats, gamma, beta, act, alpha, sums, P_global, nee
     return dy, dgamma, dbeta
 
 
+def bn_affine_grads(sums, stats, C, dgamma=None, dbeta=None, accumulate=False):
+    """dgamma / dbeta (given buffers) from BatchNorm backward sums [2][C] (rgan_bn_affine_grads):
+    written, or added into with ``accumulate``."""
+    L.check(L.lib().rgan_bn_affine_grads(L.ptr(sums), L.ptr(stats), int(C), L.ptr(dgamma), L.ptr(dbeta),
+                                         int(bool(accumulate)), L.stream()), "rgan_bn_affine_grads")
+
+
 def bn_segment_stats_n(part, S, nseg, C, eps, momentum, running_mean, running_var, num_batches_tracked, out):
     """bn_segment_stats of the nseg equal batch segments of [0, S) in one launch: out[nseg][2C],
     running statistics updated in segment order."""

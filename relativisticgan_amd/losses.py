@@ -220,9 +220,8 @@ def gradient_penalty(D, x, x_fake, u, penalty):
     """penalty * mean((||dD(x_hat)/dx_hat||_2 - 1)^2), x_hat = x*u + x_fake*(1-u) (GLI:648-657).
 
     Native engine (gp.py): forward, create-graph backward and double backward as explicit
-    kernel sweeps.  Under SyncBN the double backward runs through the create-graph path of
-    ConvLayerFn (conv dgrad/wgrad GEMMs differentiated on the MFMA kernels, BN algebra as
-    autograd tensor ops)."""
+    kernel sweeps, with per-shard BatchNorm or SyncBN (cross-rank BN sums all-reduced).  The
+    autograd composite below is the engine's test reference (tests/test_gp_gpu.py)."""
     from . import gp as _gp
     if _gp.supported(D):
         return _gp.gradient_penalty(D, x, x_fake, u, penalty)

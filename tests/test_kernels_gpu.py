@@ -1108,3 +1108,29 @@ def test_dgrad_post_op_emulated(K, mode):
     assert _rel(got, want) < 2e-6, _rel(got, want)
     if mode == 2:
         assert _rel(pe.part, p32.part) < 2e-6
+
+
+@pytest.mark.parametrize("B,cin,cout,H,tr", [(2, 8, 16, 16, False), (64, 128, 256, 16, False), (1, 256, 512, 8, False),
+                                             (2, 16, 8, 8, True), (16, 256, 128, 8, True), (4, 24, 40, 12, False)])
+def test_wgrad_torch_order_tiles(K, B, cin, cout, H, tr):
+    """4x4 weight gradients on the torch-order FAST tiles (8 channels x 16 taps per 128-wide n
+    tile, written straight into [O][C][4][4]: no tap staging / taps_transpose), unsplit and
+    split-K (small batches), written, accumulated (``out``) and into a given tensor
+    (``into``) -- vs torch fp64."""
+    g = K.ConvGeom(4, 2, 1, tr)
+    torch.manual_seed(B + cin)
+    x = _nhwc(torch.randn(B, cin, H, H, device=DEV))
+    Ho = 2 * H if tr else H // 2
+    dy = _nhwc(torch.randn(B, cout, Ho, Ho, device=DEV))
+    wshape = (cin, cout, 4, 4) if tr else (cout, cin, 4, 4)
+    w64 = torch.zeros(wshape, dtype=torch.float64, requires_grad=True)
+    (F.conv_transpose2d if tr else F.conv2d)(x.double().cpu(), w64, stride=2, padding=1).backward(dy.double().cpu())
+    dw, _ = K.conv_wgrad(x, dy, g, wshape)
+    assert _rel(dw, w64.grad) < 2e-6
+    base = torch.randn(wshape, device=DEV)
+    acc = base.clone()
+    K.conv_wgrad(x, dy, g, wshape, out=acc)
+    assert _rel(acc - base, w64.grad) < 2e-5
+    into = torch.full(wshape, float("nan"), device=DEV)
+    K.conv_wgrad(x, dy, g, wshape, into=into)
+    assert torch.equal(into, dw)

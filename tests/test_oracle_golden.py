@@ -10,18 +10,23 @@ import pytest
 from tests.golden.configs import PINNED, SLOW_PIN
 from tests.oracle_replay import golden_meta, load_golden, replay
 
-# SLOW_PIN configs (the 256^2 headline shard: ~3 min of oracle time on this container's 8
-# vCPUs, ~30 s on the GPU box's host) run with the GPU-box suite (-m gpu; the test itself is
-# CPU-only and also runs here with `-m gpu -k <name>`).
-PIN_CASES = [pytest.param(n, marks=[pytest.mark.gpu, pytest.mark.slow]) if n in SLOW_PIN else n for n in PINNED]
+# Bitwise pins hold on the CPU the fixtures were captured on (this build container): torch's
+# CPU kernels take ISA-dependent paths, so another host (the GPU box's EPYC) reproduces the
+# oracle only to rounding.  SLOW_PIN configs (the 256^2 headline shard, ~70 s of oracle time
+# per iteration here) pin their first iteration by default and every iteration with
+# RGAN_SLOW=1.
 
 
-@pytest.mark.parametrize("name", PIN_CASES)
+@pytest.mark.parametrize("name", PINNED)
 def test_oracle_bitwise_matches_reference(name):
+    import os
     g = load_golden(name)
     meta = golden_meta(g)
-    got, _ = replay(name, n_iter=meta["n_iter"], threads=meta["threads"])
-    want_keys = {k for k in g if k != "meta.json"}
+    n_iter = meta["n_iter"]
+    if name in SLOW_PIN and not os.environ.get("RGAN_SLOW"):
+        n_iter = 1
+    got, _ = replay(name, n_iter=n_iter, threads=meta["threads"])
+    want_keys = {k for k in g if k != "meta.json" and (k.startswith("init.") or int(k[2:k.index(".")]) < n_iter)}
     missing = want_keys - set(got)
     assert not missing, f"oracle did not produce: {sorted(missing)[:10]}"
     bad = []
