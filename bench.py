@@ -176,6 +176,30 @@ def cpu_baseline(loss_D, size, batch, h, spectral, seconds_hint, arch=0, min_ite
                       f"torch {torch.__version__} CPU fp32, {threads} threads on {cpus['model']}"}
 
 
+def emu_parity_evidence():
+    """The bf16x6 variant's qualification: the full-size BASELINE configs'
+    teacher-forced GPU-vs-reference parity run with rgan_set_gemm_emulation(1) -- the committed
+    audit's compact summary (profiles/round*_parity_summary.json, tests/test_parity_gpu.py
+    ``-bf16x6`` cases): tensors passed directly / against the mask-forced fp64 step, envelope
+    uses (0 = fp32-accurate), and the fp32 run's counts beside them."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "round*_parity_summary.json")),
+                   key=lambda f: int(os.path.basename(f).split("_")[0][5:]))
+    if not files:
+        return None
+    with open(files[-1]) as fh:
+        d = json.load(fh)
+    out = {"source": os.path.relpath(files[-1], ROOT), "configs": {}}
+    for name, e in d["configs"].items():
+        if not name.endswith("-bf16x6"):
+            continue
+        base = d["configs"].get(name[:-len("-bf16x6")], {})
+        out["configs"][name[:-len("-bf16x6")]] = {
+            "tensors": e["tensors"], "direct": e["direct"], "forced": e.get("forced", 0), "envelope": e["envelope"],
+            "failed": e.get("FAIL") or 0, "fp32_direct": base.get("direct"), "fp32_forced": base.get("forced")}
+    return out
+
+
 def restatement_check():
     """the oracle timed against the unmodified reference script on the same host
     (tests/golden/time_reference.py, run in the build container -- the reference does not
@@ -515,7 +539,8 @@ def main():
             "steps": emu_res["steps"], "hip_graph": emu_res["graph"],
             "gemm_arith": "forward / data-gradient conv GEMMs: fp32 operands split exactly into 3 bf16 "
                           "pieces, 6 bf16 MFMA products accumulated in fp32 (weight gradients: fp32 MFMA)",
-            "roofline": roofline_of(emu_res, args.workload)}
+            "roofline": roofline_of(emu_res, args.workload),
+            "parity": emu_parity_evidence()}
     if world == 1 and not args.no_hbm:
         out["hbm_kernels"] = hbm_kernels(args.workload, K)
     if world == 1 and not args.no_cpu_baseline:

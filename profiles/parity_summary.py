@@ -30,9 +30,12 @@ max|gpu - forced| / (RMS(forced) * tol) (must be <= ELEM_FACTOR = 10).
 
 def main(d, head="", rnd="4"):
     rows, tot, direct, forced = [], 0, 0, 0
+    compact = {}
     for f in sorted(glob.glob(os.path.join(d, "*.json"))):
         r = json.load(open(f))
         assert r.get("FAIL", 0) == 0, f
+        compact[r["config"]] = {k: r.get(k) for k in ("tensors", "direct", "forced", "envelope", "flip", "FAIL",
+                                                      "premise_max_abs_over_rms", "worst_elem_vs_forced")}
         fl = sum(x["elements"] for x in r.get("flips", []))
         we = r.get("worst_elem_vs_forced")
         wtxt = f"{we['max_over_rms'] / we['tol']:.2f}" if we else "-"
@@ -47,6 +50,9 @@ def main(d, head="", rnd="4"):
            f"\n\nTotal: {direct} of {tot} tensors direct ({100.0 * direct / tot:.1f} %), "
            f"{direct + forced} direct or against the mask-forced fp64 step ({100.0 * (direct + forced) / tot:.1f} %).\n")
     open(os.path.join(d, "SUMMARY.md"), "w").write(out)
+    # compact per-config counts (read by bench.py on the GPU box, where the audit dir is not sent)
+    with open(os.path.join(os.path.dirname(os.path.abspath(d)), f"round{rnd}_parity_summary.json"), "w") as fh:
+        json.dump({"audit": os.path.basename(os.path.abspath(d)), "head": head, "configs": compact}, fh, indent=1)
     print(out)
 
 
