@@ -108,8 +108,6 @@ struct GemmArgs {
   int xgroup, nph;        // XCD-grouped tile order (blocks sharing A rows on one XCD); phases
   double* bnp;            // nullable: BatchNorm moments of every 64-row output segment (vector epilogue)
   int accum;              // WGRAD: add into C (gradient accumulation) instead of overwriting it
-  int wt16;               // WGRAD FAST, 4x4 kernel: n tiles of 8 channels x 16 taps in torch order
-                          // (n = ci * 16 + tap): C rows are the weight's own rows, no tap staging
   // Post-op for the layer that PRODUCED this GEMM's output operand (rgan_conv_post: a data
   // gradient, or G's image-layer gradient GEMM), applied where the value is final (unsplit
   // epilogue or split-K reduce); px has C's layout (host-checked):
@@ -293,7 +291,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   auto sw_p = [&](int R, int i) { return ((tid >> 3) & 3) + 4 * ((tid >> 5) / (R / 32)) + (32 / (R / 32)) * i; };
   // WGRAD FAST: im2col pixel offsets of the next tiles, per tap of the block's n tile (a
   // tile holds one tap when Cin >= BN, else BN / Cin <= 4 whole taps of one kernel row)
-  __shared__ int ptab[2][(MODE == MODE_WGRAD ? 16 : 1) * BK];
+  __shared__ int ptab[2][4 * BK];
   __amdgpu_buffer_rsrc_t arsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g.a.p, (short)0, g.a_bytes, 0x00020000);
   __amdgpu_buffer_rsrc_t brsrc =
       MODE == MODE_WGRAD ? __builtin_amdgcn_make_buffer_rsrc((void*)g.im.p, (short)0, g.im_bytes, 0x00020000)
@@ -330,15 +328,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
       w_ntap = cin >= BN ? 1 : BN / cin;
       w_tq = cin >= BN ? 0 : c4 / cin;
       w_qb = (c4 - w_tq * cin) * 4;
-      if (g.wt16) {
-        // torch-order tile: n0 / 16 = first of its 8 channels, all 16 taps; quad q = (channel
-        // half h, tap t) loads channels 4h..4h+3 of tap t (table rows are taps, pixel-only)
-        const int q = sw_q(BN);
-        w_ntap = 16;
-        w_tq = q & 15;
-        w_qb = (n0 / 16 + 4 * (q >> 4)) * 4;
-        w_tab = -g.pad * (int)g.im.sh - g.pad * (int)g.im.sw;
-      }
     }
   }
   // CONV/CONVT2 FAST: per-row offsets for the current tap
@@ -367,25 +356,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   auto build_table = [&](int k0, int slot) {
     if constexpr (FAST && MODE == MODE_WGRAD) {
       const int l = tid & 63;
-      if (g.wt16) {  // 16 taps x BK pixels: lane l -> pixel l % 32, taps 8 (l / 32) ..
-        const int p = k0 + (l & 31);
-        const uint32_t b = g.fghw.div(p);
-        const uint32_t rem = p - b * g.fghw.d;
-        const uint32_t oi = g.fgw.div(rem);
-        const uint32_t oj = rem - oi * g.fgw.d;
-        const int pix = (int)b * (int)g.im.sb + (int)oi * g.stride * (int)g.im.sh + (int)oj * g.stride * (int)g.im.sw;
-        const bool pok = p < kend;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int t = 8 * (l >> 5) + u, ih = (int)oi * g.stride - g.pad + (t >> 2),
-                    iw = (int)oj * g.stride - g.pad + (t & 3);
-          ptab[slot][t * BK + (l & 31)] =
-              (pok && (unsigned)ih < (unsigned)g.im.H && (unsigned)iw < (unsigned)g.im.W)
-                  ? (pix + w_tab + (t >> 2) * (int)g.im.sh + (t & 3) * (int)g.im.sw) * 4
-                  : OOB;
-        }
-        return;
-      }
       if (l < BK) {
         const int p = k0 + l;
         const uint32_t b = g.fghw.div(p);
@@ -604,22 +574,20 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
     float* Bs = As + A_SZ;
     if constexpr (SWZ) {
       // element (row, k) at row * 32 + 4 ((k >> 2) ^ ((row >> 1) & 7)) + (k & 3)
-      // quad q's element j goes to row 4 q + j; torch-order B tiles (wt16): channel 4 h + j
-      // of tap t (q = 16 h + t) goes to row (4 h + j) * 16 + t = n - n0
-      auto put = [&](float* T, int R, const float* v, int nld, bool torch_order) {
+      auto put = [&](float* T, int R, const float* v, int nld) {
         const int q = sw_q(R);
 #pragma unroll
         for (int i = 0; i < nld; ++i) {
           const int k = sw_p(R, i);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            const int row = torch_order ? (4 * (q >> 4) + j) * 16 + (q & 15) : 4 * q + j;
+            const int row = 4 * q + j;
             T[row * KROW_LD + 4 * ((k >> 2) ^ ((row >> 1) & 7)) + (k & 3)] = v[4 * i + j];
           }
         }
       };
-      put(As, BM, ra, FA_N, false);
-      put(Bs, BN, rb, FB_N, BN == 128 && g.wt16);
+      put(As, BM, ra, FA_N);
+      put(Bs, BN, rb, FB_N);
       return;
     } else if constexpr (KROW) {
       const int q = tid & 7;
@@ -2605,9 +2573,19 @@ static void tile_dims(int cfg, int& bm, int& bn) {
   bn = cfg == CFG_L ? 128 : (cfg == CFG_M ? 64 : 32);
 }
 
+#ifndef RGAN_SPLIT_CFGM  // experiment: 128 x 64 tiles when 128 x 128 ones would split K this many ways
+#define RGAN_SPLIT_CFGM 0
+#endif
+
 static void choose_tiling(Plan& p) {
   GemmArgs& g = p.g;
   p.cfg = g.N <= 32 ? CFG_N : (g.N <= 64 ? CFG_M : CFG_L);
+#if RGAN_SPLIT_CFGM
+  if (p.cfg == CFG_L && p.mode != MODE_WGRAD) {
+    const long long t = (long long)ceil_div(g.M, 128) * ceil_div(g.N, 128) * p.phases;
+    if (t * RGAN_SPLIT_CFGM <= RGAN_SPLIT_TARGET && ceil_div(g.K, BK) >= 4 * RGAN_SPLIT_CFGM) p.cfg = CFG_M;
+  }
+#endif
   int bm, bn;
   tile_dims(p.cfg, bm, bn);
   const int tiles_m = ceil_div(g.M, bm), tiles_n = ceil_div(g.N, bn);
@@ -2688,14 +2666,10 @@ static void set_fast(Plan& p, int batch) {
     const long long im_bytes = img_span_bytes(g.im, batch);
     if (im_bytes > FAST_MAX_BYTES) return;
     if (g.a.sh != (long long)g.a.W * g.a.sw || g.a.sb != (long long)g.a.H * g.a.sh) return;
-    // a B tile is one tap's BN channels, or BN / Cin <= 4 whole taps of one kernel row, or
-    // (wt16) 8 channels x all 16 taps of a 4x4 kernel in torch order
+    // a B tile is one tap's BN channels, or BN / Cin <= 4 whole taps of one kernel row
     const int cin = g.im.C;
-    if (g.wt16) {
-      if (bn != 128 || g.KH != 4 || g.KW != 4 || cin % 8 != 0) return;
-    } else if (cin % bn != 0 && !(bn % cin == 0 && cin % 4 == 0 && bn / cin <= 4 && g.KW % (bn / cin) == 0)) {
+    if (cin % bn != 0 && !(bn % cin == 0 && cin % 4 == 0 && bn / cin <= 4 && g.KW % (bn / cin) == 0))
       return;
-    }
     g.a_bytes = (int)a_bytes;
     g.im_bytes = (int)im_bytes;
   }
@@ -2992,23 +2966,7 @@ static int plan_wgrad(const RganConv* d, const float* x, const float* dy, float*
          aligned16(g.a.p);
   p.bv = vec_img_ok(g.im);
   choose_tiling(p);
-  // 4x4 kernels whose torch-layout rows are contiguous ([O][C][4][4], o.sb == C * 16): the
-  // FAST tiles take n in torch order (8 channels x 16 taps), so C is written straight into
-  // the weight gradient (no tap-major staging + taps_transpose)
-  {
-    const OutMap& o = g.out;
-    g.wt16 = p.cfg == CFG_L && g.KH == 4 && g.KW == 4 && o.fnkw.d == 4 && (uint32_t)g.N == 16 * o.fnc.d &&
-             o.th == 4 && o.tw == 1 && o.tc == 16 && o.sb == (long long)g.N && o.fnc.d % 8 == 0;
-  }
   set_fast(p, d->batch);
-  if (g.wt16 && !p.fast) {
-    g.wt16 = 0;
-    set_fast(p, d->batch);
-  }
-  if (g.wt16) {
-    g.out = make_out(1, 1, 1, g.N, 0, 0, 1, 1, g.N, 0, 0, 1);  // [M][N], n = ci * 16 + tap contiguous
-    return 0;
-  }
   // unsplit FAST wgrads with 4x4 taps: row-contiguous staging + taps_transpose
   const OutMap& o = g.out;
   if (p.fast && g.splits == 1 && p.cfg == CFG_L && o.fnkw.d == 4 && (uint32_t)g.N == 16 * o.fnc.d &&
@@ -3413,7 +3371,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     auto al4 = [](long long v) { return (v & 3) == 0; };
     int kind = RED_ANY;
     uint32_t per = (uint32_t)g.M * g.N, d = g.N;
-    if ((p.mode != MODE_WGRAD || g.wt16) && o.tc == 1 && o.fnc.d % 4 == 0 && g.N % 4 == 0 && al4(o.th) &&
+    if (p.mode != MODE_WGRAD && o.tc == 1 && o.fnc.d % 4 == 0 && g.N % 4 == 0 && al4(o.th) &&
         al4(o.tw) && al4(o.sb) && al4(o.sh) && al4(o.sw) && ((uintptr_t)g.C & 15) == 0) {
       kind = RED_VEC;
       per /= 4;

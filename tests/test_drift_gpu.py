@@ -8,6 +8,9 @@ GPU's errD/errG trajectory may not diverge from the float64 oracle trajectory fa
 the fp32 oracle itself does (the oracle is pinned bitwise to the reference).
   * steps 0-9: per-step relative gap <= max(5e-3, 10 x the fp32 oracle's own gap);
   * all 100 steps: mean gap <= 3 x the fp32 oracle's mean gap + 1e-3.
+At the north-star config itself (RaLSGAN 64^2, B=32, h=128) the envelope is the reference's
+own: its trajectories at 1, 2, 4 and 8 threads, recorded from the unmodified script
+(test_c1_100_step_drift_within_reference_thread_envelope; bounds in its docstring).
 """
 import numpy as np
 import pytest
@@ -73,7 +76,9 @@ def test_100_step_drift_within_fp32_envelope(name):
 TRAJ_Q = ("errD", "errG", "D.y_pred", "D.y_pred_fake", "G.y_pred", "G.y_pred_fake")
 DRAWS = ("D.x", "D.z", "G.z", "G.x")
 ENV_MULT = 3.0     # GPU divergence from the 8-thread reference <= ENV_MULT x the reference's spread so far
-STEP_REL = 1e-4    # ... or the per-step tolerance (north_star: rel 1e-4) while that spread is ~0
+ENV_LAG = 2        # ... taken ENV_LAG steps later (see the test's docstring)
+STEP_REL = 1e-4    # plus the per-step tolerance (north_star: rel 1e-4), on the quantity's scale
+MEAN_MULT = 1.0    # mean gap over the 100 steps <= MEAN_MULT x the reference's mean thread spread
 
 
 def _ref_trajectories(name):
@@ -123,6 +128,21 @@ def gpu_c1_trajectory(name, n_iter):
 
 
 def test_c1_100_step_drift_within_reference_thread_envelope():
+    """100 free-running C1 iterations on the GPU (host RNG: the reference's draws) against the
+    reference's own 1 / 2 / 4 / 8-thread trajectories.  Per quantity q (losses, mean D outputs
+    of both steps) with scale s_q = mean |q| over the 8-thread trajectory:
+      * the draws (dataset indices, z) equal the reference's at every step;
+      * step 0: |gpu - ref8| <= STEP_REL * s_q (one fp32 step, before any Adam update);
+      * step k >= 1: |gpu - ref8| <= ENV_MULT * s_q * env(k + ENV_LAG) + STEP_REL * s_q, env(k)
+        = the running max over steps <= k of the reference's spread between thread counts,
+        relative to each quantity's scale and pooled over the quantities.  The lag: the CPU
+        reference is thread-invariant through its first Adam step (spread ~1e-7 at steps 0-1),
+        while any other fp32 summation order -- the GPU's -- flips the signs of near-zero
+        gradients in Adam's first (sign) step; the thread counts' trajectories reach that
+        divergence two steps later and grow alike from there;
+      * mean over the 100 steps of |gpu - ref8| <= MEAN_MULT x the mean thread spread."""
+    import json
+    import os
     from tests.golden.configs import TRAJ_ITERS
     name = "ralsgan_c1"
     ref = _ref_trajectories(name)
@@ -132,24 +152,29 @@ def test_c1_100_step_drift_within_reference_thread_envelope():
     for k in DRAWS:
         np.testing.assert_allclose(g[k], r8[k], rtol=1e-12, atol=1e-9, err_msg=k)
     errs, report = [], {}
-    # the reference's own divergence between thread counts, per step, on each quantity's scale
-    # (mean |value| over the trajectory) and pooled over the quantities (the divergence is a
-    # property of the training state, not of one scalar), as a running max (chaos only grows)
     scale = {q: float(np.mean(np.abs(r8[q]))) for q in TRAJ_Q}
-    rel_spread = np.max([(np.ptp(np.stack([ref[th][q] for th in ref]), 0)) / scale[q] for q in TRAJ_Q], axis=0)
-    env = np.maximum.accumulate(rel_spread)
+    spread = {q: np.ptp(np.stack([ref[th][q] for th in ref]), 0) for q in TRAJ_Q}
+    env = np.maximum.accumulate(np.max([spread[q] / scale[q] for q in TRAJ_Q], axis=0))
+    n = len(env)
+    lagged = env[np.minimum(np.arange(n) + ENV_LAG, n - 1)]
     for q in TRAJ_Q:
         d = np.abs(g[q] - r8[q])
-        bound = ENV_MULT * env * scale[q] + STEP_REL * np.abs(r8[q]) + 1e-7
+        bound = ENV_MULT * scale[q] * lagged + STEP_REL * scale[q]
+        bound[0] = STEP_REL * scale[q]
         bad = np.nonzero(d > bound)[0]
-        report[q] = {"max_ratio": float(np.max(d / bound)), "gpu_mean_gap": float(d.mean()),
-                     "ref_mean_spread": float(np.ptp(np.stack([ref[th][q] for th in ref]), 0).mean()),
-                     "step0_rel": float(d[0] / max(abs(r8[q][0]), 1e-30))}
+        report[q] = {"max_gap_over_bound": float(np.max(d / bound)), "gpu_mean_gap": float(d.mean()),
+                     "ref_mean_spread": float(spread[q].mean()), "step0_gap_over_scale": float(d[0] / scale[q])}
         if bad.size:
-            errs.append(f"{q}: {bad.size} steps outside {ENV_MULT} x the reference's thread envelope, first at "
-                        f"{bad[0]} (gap {d[bad[0]]:.3e} vs bound {bound[bad[0]]:.3e})")
-        # step 0: the thread counts agree to ~1e-7; the GPU within the per-step tolerance
-        if not d[0] <= STEP_REL * abs(r8[q][0]) + 1e-7:
-            errs.append(f"{q}: step 0 gap {d[0]:.3e}")
+            errs.append(f"{q}: {bad.size} steps outside the bound, first at {bad[0]} "
+                        f"(gap {d[bad[0]]:.3e} vs bound {bound[bad[0]]:.3e})")
+        if d.mean() > MEAN_MULT * spread[q].mean():
+            errs.append(f"{q}: mean gap {d.mean():.3e} > {MEAN_MULT} x the mean thread spread {spread[q].mean():.3e}")
     print("c1 drift:", {q: {k: f"{v:.3g}" for k, v in r.items()} for q, r in report.items()})
+    out_dir = os.environ.get("RGAN_PARITY_AUDIT")
+    if out_dir:
+        os.makedirs(out_dir, exist_ok=True)
+        with open(os.path.join(out_dir, "drift_ralsgan_c1.json"), "w") as f:
+            json.dump({"report": report, "gpu": {k: v.tolist() for k, v in g.items()},
+                       "ref8": {k: r8[k].tolist() for k in TRAJ_Q}, "env": env.tolist(),
+                       "ENV_MULT": ENV_MULT, "ENV_LAG": ENV_LAG, "STEP_REL": STEP_REL, "MEAN_MULT": MEAN_MULT}, f)
     assert not errs, "\n".join(errs)

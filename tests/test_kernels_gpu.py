@@ -1112,10 +1112,9 @@ def test_dgrad_post_op_emulated(K, mode):
 
 @pytest.mark.parametrize("B,cin,cout,H,tr", [(2, 8, 16, 16, False), (64, 128, 256, 16, False), (1, 256, 512, 8, False),
                                              (2, 16, 8, 8, True), (16, 256, 128, 8, True), (4, 24, 40, 12, False)])
-def test_wgrad_torch_order_tiles(K, B, cin, cout, H, tr):
-    """4x4 weight gradients on the torch-order FAST tiles (8 channels x 16 taps per 128-wide n
-    tile, written straight into [O][C][4][4]: no tap staging / taps_transpose), unsplit and
-    split-K (small batches), written, accumulated (``out``) and into a given tensor
+def test_wgrad_write_accumulate_into(K, B, cin, cout, H, tr):
+    """4x4 weight gradients (FAST tap-major tiles + taps_transpose, split-K for small batches,
+    the generic path for Cin = 24), written, accumulated (``out``) and into a given tensor
     (``into``) -- vs torch fp64."""
     g = K.ConvGeom(4, 2, 1, tr)
     torch.manual_seed(B + cin)
