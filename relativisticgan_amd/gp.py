@@ -130,7 +130,7 @@ class GPEngine:
             else:
                 xc_next = empty_nhwc(2 * B, cout, Ho, Wo, self.dev)
                 out = xc_next[B:]
-            w = r.w.detach()
+            w = r.w  # the parameter (or its view) itself: the pack cache is keyed by the weight's base
             if spec.bn:
                 y, part, S = K.conv_fwd_bn(h, w, spec.geom, bias=r.bias, wscale=r.wscale, cache=True)
                 r.stats = AG._train_stats(y, spec, bn.running_mean, bn.running_var, bn.num_batches_tracked,
@@ -171,7 +171,7 @@ class GPEngine:
                 r.dy = K.act_backward_ex(dh, r.a, spec.act, spec.alpha, out=r.yc[:B])
             else:
                 r.fs, r.dy = None, dh
-            dh = K.conv_dgrad(r.dy, r.w.detach(), spec.geom, tuple(r.h_in.shape), wscale=r.wscale, like=r.h_in,
+            dh = K.conv_dgrad(r.dy, r.w, spec.geom, tuple(r.h_in.shape), wscale=r.wscale, like=r.h_in,
                               cache=True, out=(r.xc[:B] if li == 0 else None))
         self.g = dh  # dD(x_hat)/dx_hat, in the image pair's first half (backward() overwrites it with v)
 
@@ -189,7 +189,7 @@ class GPEngine:
             if last and not spec.bn and not has2:
                 break  # dy_L = dh_L act' with dh_L = ones and act'' = 0: no adjoint flows on
             nxt = None if last else recs[li + 1].xc[:B]
-            w = r.w.detach()
+            w = r.w
             if spec.bn:
                 a_adj = K.conv_fwd(ubar, w, spec.geom, wscale=r.wscale, cache=True)
                 P = self._P(r)
@@ -240,7 +240,7 @@ class GPEngine:
             elif ydir is not None:
                 ybar = ydir  # already in the pair buffer's second half
             self._weight_grad(li, r, ybar)
-            gbar = (K.conv_dgrad(ybar, r.w.detach(), spec.geom, tuple(r.h_in.shape), wscale=r.wscale,
+            gbar = (K.conv_dgrad(ybar, r.w, spec.geom, tuple(r.h_in.shape), wscale=r.wscale,
                                  like=r.h_in, cache=True) if (ybar is not None and li > 0) else None)
 
     @staticmethod
