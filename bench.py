@@ -216,28 +216,30 @@ def restatement_check():
     return out
 
 
-def run_workload(name, steps, warmup, world, args, K, emu=False, dp_path=False):
+def run_workload(name, steps, warmup, world, args, K, emu=False, dp_path=False, host_rng=False):
     """Train `steps` timed iterations of workload `name` (after `warmup`); returns the
     measurement (max over ranks).  emu: forward / data-gradient GEMMs on bf16x6.  dp_path:
     run one process exactly as every rank of an N > 1 run does (separate D(x) / D(x_fake)
     passes, eager launches, no HIP graph) -- the like-for-like N = 1 baseline of the scaling
-    runs."""
+    runs.  host_rng: batches and z drawn on the host in the reference's order (numpy choice,
+    torch CPU generator, seed 1: SURVEY §8(d) -- the oracle's exact draws), eager launches
+    (a graph replay would repeat its capture's draws)."""
     prev_emu = K.set_gemm_emulation(emu)
     try:
-        return _run_workload(name, steps, warmup, world, args, K, dp_path)
+        return _run_workload(name, steps, warmup, world, args, K, dp_path, host_rng)
     finally:
         K.set_gemm_emulation(prev_emu)
 
 
-def _run_workload(name, steps, warmup, world, args, K, dp_path=False):
+def _run_workload(name, steps, warmup, world, args, K, dp_path=False, host_rng=False):
     from relativisticgan_amd.config import make_param
     from relativisticgan_amd.train import Trainer, synthetic_images
     loss_D, size, bpg, h = WORKLOADS[name]
     spectral = name == "C5"
     bd = False if dp_path else {"auto": None, "on": True, "off": False}[args.batch_d]
     p = make_param(loss_D=loss_D, image_size=size, batch_size=bpg * world, G_h_size=h, D_h_size=h, seed=1,
-                   print_every=10 ** 9, spectral=spectral, rgan_rng="device", arch=ARCH.get(name, 0),
-                   rgan_batch_D=bd)
+                   print_every=10 ** 9, spectral=spectral, rgan_rng="host" if host_rng else "device",
+                   arch=ARCH.get(name, 0), rgan_batch_D=bd)
     images = synthetic_images(1024, size, device="cuda")
     t = Trainer(p, images)
     flops_iter = conv_flops_per_iteration(t)
@@ -250,7 +252,9 @@ def _run_workload(name, steps, warmup, world, args, K, dp_path=False):
     # cannot launch them mid-way)
     n_params = sum(q.numel() for q in list(t.G.parameters()) + list(t.D.parameters()))
     multi = world > 1 or dp_path
-    if args.graph == "auto":
+    if host_rng:
+        mode = "eager"
+    elif args.graph == "auto":
         mode = ("piecewise" if n_params < 50e6 else "eager") if multi else "graph"
     elif args.graph == "on":
         mode = "piecewise" if multi else "graph"
@@ -468,6 +472,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dp-path", action="store_true",
                     help="skip the N=1 runs of the data-parallel launch mode (dp_path_n1)")
+    ap.add_argument("--no-host-draws", action="store_true",
+                    help="skip the N=1 eager run with the reference's host-side draws (host_draws_n1)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-hbm", action="store_true", help="skip the HBM-bound kernels' GB/s table (hbm_kernels)")
     ap.add_argument("--sync-bn", action="store_true",
@@ -494,7 +500,7 @@ def main():
     emu_res = None
     if world == 1 and not args.no_emu_extra:
         emu_res = run_workload(args.workload, args.steps, min(args.warmup, 5), world, args, K, emu=True)
-    extras, dp_paths = {}, {}
+    extras, dp_paths, host_draws = {}, {}, {}
     if world == 1:
         for name in [w for w in args.extra.split(",") if w and w != args.workload]:
             r = run_workload(name, args.steps, min(args.warmup, 5), world, args, K)
@@ -510,13 +516,22 @@ def main():
                 r = run_workload(name, args.steps, min(args.warmup, 5), world, args, K, dp_path=True)
                 dp_paths[name] = {"value": r["value"], "unit": "images/s", "ms_per_step": r["ms_per_step"],
                                   "steps": r["steps"], "batched_D_step": r["batch_D"], "launch_mode": r["mode"]}
+        if not args.no_host_draws:
+            for name in [args.workload] + [w for w in ("C1",) if w in args.extra.split(",")]:
+                r = run_workload(name, args.steps, min(args.warmup, 5), world, args, K, host_rng=True)
+                host_draws[name] = {"value": r["value"], "unit": "images/s", "ms_per_step": r["ms_per_step"],
+                                    "steps": r["steps"], "launch_mode": r["mode"],
+                                    "draws": "host: numpy.random.choice batches + torch CPU z, seed 1, "
+                                             "the reference's order (SURVEY §8(d)); H2D per draw"}
     if rank != 0:
         torch.distributed.destroy_process_group()
         return
     out = {
         "metric": METRIC, "value": res["value"], "unit": "images/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": res["ms_per_step"], "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp32", "data": "synthetic",
+        "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (1024 seeded images resident in HBM; batches / z drawn on the device -- "
+                "host_draws_n1: the reference's host draws)",
         "config": {"workload": describe(res), "loss_D": res["loss_D"], "image_size": res["size"],
                    "batch_per_gpu": res["bpg"], "global_batch": res["bpg"] * world, "G_h_size": res["h"],
                    "D_h_size": res["h"], "arch": res["arch"], "parallelism": f"dp{world}",
@@ -533,6 +548,10 @@ def main():
         # what each rank of the N > 1 runs executes (separate D passes, eager), on one GPU:
         # the like-for-like N = 1 baseline for the scaling efficiency of `value` at N > 1
         out["dp_path_n1"] = dp_paths
+    if host_draws:
+        # `value` draws on the device (Philox, csrc/sampling.hip) so that the iteration can be
+        # replayed as a HIP graph; this is the same workload with the oracle's own host draws
+        out["host_draws_n1"] = host_draws
     if emu_res is not None:
         out["fp32_emulated_bf16x6"] = {
             "value": emu_res["value"], "unit": "images/s", "ms_per_step": emu_res["ms_per_step"],

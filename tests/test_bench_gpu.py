@@ -42,6 +42,9 @@ def test_bench_one_gpu_line():
     # the N > 1 launch mode on one GPU (the scaling runs' like-for-like baseline)
     dpp = d["dp_path_n1"]["C1"]
     assert dpp["value"] > 0 and dpp["batched_D_step"] is True and dpp["launch_mode"] == "piecewise"
+    # the same workload on the reference's host draws (eager)
+    hd = d["host_draws_n1"]["C1"]
+    assert hd["value"] > 0 and hd["launch_mode"] == "eager"
 
 
 @pytest.mark.parametrize("world", [2, 4])

@@ -26,11 +26,11 @@ for s in $steps; do
       timeout -k 10 500 python -u bench.py $wl > "$out/bench$sfx.json" 2> "$out/bench$sfx.err"
       rc=$?; echo "bench$sfx rc=$rc"; stop $rc bench ;;
     prof*)
-      timeout -k 10 450 tools/profile_bench.sh "$out/prof$sfx" --steps 10 --warmup 3 --no-cpu-baseline --no-emu-extra --no-dp-path --graph off \
+      timeout -k 10 450 tools/profile_bench.sh "$out/prof$sfx" --steps 10 --warmup 3 --no-cpu-baseline --no-emu-extra --no-dp-path --no-host-draws --graph off \
         --extra= $wl
       rc=$?; echo "prof$sfx rc=$rc"; head -25 "$out/prof$sfx/summary.txt"; stop $rc prof ;;
     pmc*)
-      timeout -k 10 850 tools/pmc_traffic.sh "$out/pmc$sfx" --steps 5 --warmup 2 --no-cpu-baseline --no-emu-extra --no-dp-path --graph off \
+      timeout -k 10 850 tools/pmc_traffic.sh "$out/pmc$sfx" --steps 5 --warmup 2 --no-cpu-baseline --no-emu-extra --no-dp-path --no-host-draws --graph off \
         --extra= $wl
       rc=$?; echo "pmc$sfx rc=$rc"; stop $rc pmc ;;
     smoke)
