@@ -18,7 +18,8 @@
 // register-staged global loads (next tile's loads in flight while the current tile's
 // MFMAs run).  LDS images keep every MFMA operand read a conflict-free ds_read_b32:
 // m-major tiles use row stride BK+1, k-major tiles BM+4 / BN+4.  Split-K writes fp32
-// slabs reduced in fixed order (deterministic) by splitk_reduce.
+// slabs reduced in fixed order (deterministic) by splitk_reduce (an in-launch combine by each
+// tile's last-arriving block, GemmArgs::fixup, is kept as a measured-slower experiment).
 #include "common.h"
 
 #include <string>
@@ -54,6 +55,27 @@ constexpr int BK = 32;
 #ifndef RGAN_SPLIT_TARGET  // split-K occupancy target (blocks); variant builds sweep it (tools/build_variant.py)
 #define RGAN_SPLIT_TARGET 512
 #endif
+// In-launch split-K combine (GemmArgs::fixup; experiment, off): FAST 128x128 CONV / CONVT2 tiles
+// split at most RGAN_FIXUP_MAX ways, the last arriver reads splits x 64 KB; RGAN_FIXUP_WGRAD
+// extends it to the weight gradients.  Measured against the separate reduce launches (same box,
+// profiles/round4_splitk_fixup_ab.txt): C1 3.86 -> 4.21 ms/step, C4 4.15 -> 4.53 (the dominant
+// GEMM 0.80 -> 0.70 of peak): every split block pays the drain + agent-scope release, and the
+// combine + epilogue of a tile runs on one block of its splits instead of the whole chip
+#ifndef RGAN_FIXUP
+#define RGAN_FIXUP 0
+#endif
+#ifndef RGAN_FIXUP_MAX
+#define RGAN_FIXUP_MAX 16
+#endif
+#ifndef RGAN_FIXUP_WGRAD
+#define RGAN_FIXUP_WGRAD 0
+#endif
+// arrival counters of the in-launch combine: FIX_REGIONS rotating regions of FIX_TILES tile
+// words (zero at load; each tile's last arriver puts its word back to 0), one region per
+// launch in turn, so GEMMs in flight together on different streams (fewer than FIX_REGIONS)
+// never share a word
+constexpr int FIX_TILES = 1024, FIX_REGIONS = 16;
+__device__ unsigned int g_split_tickets[FIX_REGIONS * FIX_TILES];
 
 // n / d for 0 <= n < 2^31 via multiply-high (host-computed magic numbers)
 struct FastDiv {
@@ -108,6 +130,10 @@ struct GemmArgs {
   int xgroup, nph;        // XCD-grouped tile order (blocks sharing A rows on one XCD); phases
   double* bnp;            // nullable: BatchNorm moments of every 64-row output segment (vector epilogue)
   int accum;              // WGRAD: add into C (gradient accumulation) instead of overwriting it
+  // splits > 1 with fixup: each block writes its partial tile to a tile-major slab
+  // ([phase][tile][split][fragment order]), and the tile's last-arriving block (ticket in
+  // g_split_tickets[fix_region]) sums the splits in split order and runs the unsplit epilogue
+  int fixup, fix_region;
   // Post-op for the layer that PRODUCED this GEMM's output operand (rgan_conv_post: a data
   // gradient, or G's image-layer gradient GEMM), applied where the value is final (unsplit
   // epilogue or split-K reduce); px has C's layout (host-checked):
@@ -873,6 +899,76 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   }
   }  // EMU / fp32 main loop
 
+  // ---------------- in-launch split-K combine ----------------
+  // The release / acquire hand-off of cdna_hip_programming.md §5 (in-launch split-K
+  // reduction): every block stores its partial tile with plain 16-B stores in fragment order
+  // (each wave's float4 store = 64 lanes x 16 B contiguous), drains them, and after a block
+  // barrier one lane releases at agent scope and takes a ticket; the block that draws
+  // splits - 1 acquires, reads every split's partial tile in split order (the same fp32 sums
+  // splitk_reduce forms) into its accumulators and continues as an unsplit tile.
+  if (g.fixup) {
+    constexpr int TILE = BM * BN;
+    const int tiles_ph = ((g.M + BM - 1) / BM) * g.tiles_n;
+    const int tix = phase * tiles_ph + tm_i * g.tiles_n + tn_i;
+    float* tbase = g.slab + (size_t)tix * g.splits * TILE;
+    auto frag = [&](int i, int j, int r4) { return ((((wid * TM + i) * TN + j) * 4 + r4) * 64 + lane) * 4; };
+    {
+      float* mine = tbase + (size_t)split * TILE;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4)
+            *reinterpret_cast<float4*>(mine + frag(i, j, r4)) =
+                make_float4(acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2], acc[i][j][4 * r4 + 3]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);  // the main loop's last barrier has passed
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      unsigned int* cnt = &g_split_tickets[g.fix_region * FIX_TILES + tix];
+      const unsigned int prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = prev == (unsigned int)(g.splits - 1);
+      if (last) {
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every split has arrived
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    const int last = flag[0];
+    __syncthreads();  // every wave has read the flag before the epilogue reuses smem
+    if (!last) return;
+    for (int sp = 0; sp < g.splits; ++sp) {
+      const float* src = tbase + (size_t)sp * TILE;
+      float4 v[TM][TN][4];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4) v[i][j][r4] = *reinterpret_cast<const float4*>(src + frag(i, j, r4));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int r4 = 0; r4 < 4; ++r4) {
+            const float4 q = v[i][j][r4];
+            if (sp == 0) {
+              acc[i][j][4 * r4] = q.x; acc[i][j][4 * r4 + 1] = q.y; acc[i][j][4 * r4 + 2] = q.z; acc[i][j][4 * r4 + 3] = q.w;
+            } else {
+              acc[i][j][4 * r4] += q.x; acc[i][j][4 * r4 + 1] += q.y; acc[i][j][4 * r4 + 2] += q.z; acc[i][j][4 * r4 + 3] += q.w;
+            }
+          }
+    }
+  }
+  const bool split_out = g.splits > 1 && !g.fixup;  // partial sums for a separate splitk_reduce
+
   // ---------------- epilogue ----------------
   if constexpr (KROW && BM / WM == 64 && BN / WN == 64) {
     // Vector epilogue (FAST, 64x64 per wave): each wave stages its finished sub-tile in LDS
@@ -880,7 +976,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
     // back as float4 rows -- 16 b128 stores per lane instead of 64 scalar ones, 256
     // contiguous bytes per output row.  The scalar stores' bursts at the end of every tile
     // (all blocks finish together) held the MFMA pipes idle on short-K layers.
-    const bool slab_out = g.splits > 1;
+    const bool slab_out = split_out;
 #if RGAN_EXP_SCALAR_SLAB
     if (!slab_out && g.vec_out) {
 #else
@@ -1030,7 +1126,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
       return;
     }
   }
-  if (g.splits > 1) {
+  if (split_out) {
     float* slab = g.slab + (size_t)z * g.M * g.N;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -2607,8 +2703,21 @@ static void choose_tiling(Plan& p) {
   g.ksplit = per * BK;
   g.splits = ceil_div(g.K, g.ksplit);
   if (g.splits < 1) g.splits = 1;
-  p.slab_floats = g.splits > 1 ? (size_t)g.splits * g.M * g.N * p.phases : 0;
+  // sized for either slab layout: [phase][split][M][N] (splitk_reduce) or the fixup's
+  // tile-major [phase][tile][split][bm * bn] (whole tiles, so at least as large)
+  p.slab_floats = g.splits > 1 ? (size_t)g.splits * tiles * bm * bn : 0;
 }
+
+// in-launch split-K combine (GemmArgs::fixup): FAST 128x128 tiles, few splits, tickets for
+// every tile of the launch
+static bool fixup_ok(const Plan& p) {
+  const GemmArgs& g = p.g;
+  if (!RGAN_FIXUP || g.splits <= 1 || g.splits > RGAN_FIXUP_MAX || !p.fast || p.cfg != CFG_L) return false;
+  if (p.mode == MODE_WGRAD && !RGAN_FIXUP_WGRAD) return false;
+  if (p.mode != MODE_CONV && p.mode != MODE_CONVT2 && p.mode != MODE_WGRAD) return false;
+  return (long long)ceil_div(g.M, 128) * g.tiles_n * p.phases <= FIX_TILES;
+}
+static unsigned g_fix_next = 0;
 
 static OutMap make_out(int gh, int gw, int step, long long sb, long long sh, long long sw, int nkh,
                        int nkw, int nc, long long th, long long tw, long long tc) {
@@ -3047,7 +3156,7 @@ static bool plan_emu(const Plan& p) {
 template <int MODE>
 static void launch_mode(const Plan& p, dim3 grid, hipStream_t s) {
   if constexpr (MODE == MODE_CONV || MODE == MODE_CONVT2) {
-    if (p.g.pmode && p.g.splits == 1) {  // post_ok: FAST 128x128 (the post-op in the epilogue)
+    if (p.g.pmode && (p.g.splits == 1 || p.g.fixup)) {  // post_ok: FAST 128x128 (the post-op in the epilogue)
       if (plan_emu(p)) gemm_post_bf16x6<MODE><<<grid, 256, 0, s>>>(p.g);
       else gemm_post<MODE><<<grid, 256, 0, s>>>(p.g);
       return;
@@ -3216,7 +3325,7 @@ static void run_dense1(const Plan& p, const float* packed, hipStream_t s) {
 static bool bn_epilogue_ok(const Plan& p) {
   const GemmArgs& g = p.g;
   if (p.mode != MODE_CONV && p.mode != MODE_CONVT2) return false;
-  if (!p.fast || p.cfg != CFG_L || g.splits != 1 || !g.vec_out || p.tap_stage) return false;
+  if (!p.fast || p.cfg != CFG_L || (g.splits != 1 && !g.fixup) || !g.vec_out || p.tap_stage) return false;
   if (g.out.fnc.d != (uint32_t)g.N || g.M % 64 != 0 || p.bn_segs < 1) return false;
   if (p.bn_segs > 1 && (p.phases != 1 || g.M % p.bn_segs != 0 || (g.M / p.bn_segs) % 64 != 0)) return false;
   return true;
@@ -3235,7 +3344,7 @@ static bool red_vec_ok(const Plan& p, bool check_ptr) {
 static bool bn_reduce_ok(const Plan& p, bool check_ptr) {
   const GemmArgs& g = p.g;
   if (p.mode != MODE_CONV && p.mode != MODE_CONVT2) return false;
-  if (g.splits <= 1 || p.tap_stage || g.accum || !red_vec_ok(p, check_ptr) || g.N < 4 * REDBN_QB) return false;
+  if (g.splits <= 1 || g.fixup || p.tap_stage || g.accum || !red_vec_ok(p, check_ptr) || g.N < 4 * REDBN_QB) return false;
   if (g.out.fnc.d != (uint32_t)g.N || g.M % 64 != 0 || p.bn_segs < 1) return false;
   if (p.bn_segs > 1 && (p.phases != 1 || g.M % p.bn_segs != 0 || (g.M / p.bn_segs) % 64 != 0)) return false;
   return true;
@@ -3251,11 +3360,12 @@ static bool post_ok(const Plan& p, int mode, int nseg, bool check_ptr) {
   const GemmArgs& g = p.g;
   if (p.mode != MODE_CONV && p.mode != MODE_CONVT2) return false;
   if (p.tap_stage || g.accum || g.bias || g.act != RGAN_ACT_NONE) return false;
-  if (g.splits == 1 && !(p.fast && p.cfg == CFG_L && g.vec_out)) return false;  // gemm_post's epilogue
+  const bool whole = g.splits == 1 || g.fixup;  // the epilogue sees whole sums
+  if (whole && !(p.fast && p.cfg == CFG_L && g.vec_out)) return false;  // gemm_post's epilogue
   if (mode == 1) return true;
   if (mode != 2 || nseg < 1 || g.out.fnc.d != (uint32_t)g.N || g.M % 64 != 0) return false;
   if (nseg > 1 && (g.M % nseg != 0 || (g.M / nseg) % 64 != 0)) return false;
-  if (g.splits == 1) return p.fast && p.cfg == CFG_L && g.vec_out;
+  if (whole) return p.fast && p.cfg == CFG_L && g.vec_out;
   return red_vec_ok(p, check_ptr) && g.N >= 4 * REDBN_QB;
 }
 
@@ -3320,6 +3430,8 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     p.g.vec_out = p.mode != MODE_WGRAD && o.tc == 1 && o.fnc.d % 4 == 0 && p.g.N % 4 == 0 && al4(o.th) &&
                   al4(o.tw) && al4(o.sb) && al4(o.sh) && al4(o.sw) && aligned16(p.g.C);
   }
+  p.g.fixup = fixup_ok(p) ? 1 : 0;
+  p.g.fix_region = p.g.fixup ? (int)(g_fix_next++ % FIX_REGIONS) : 0;
   p.bn_fused = p.bn_part && (bn_epilogue_ok(p) || bn_reduce_ok(p, true));
   p.g.bnp = p.bn_fused ? p.bn_part : nullptr;
   p.post_fused = p.post && !p.bn_fused && post_ok(p, p.post->mode, p.post->nseg, true) &&
@@ -3346,7 +3458,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     rec.flops = g_cur_flops;
     rec.kid = kernel_id(p.mode, p.cfg, p.av, p.bv, p.fast);
     if (plan_emu(p)) rec.kid = 51 + p.mode;
-    if (p.g.pmode && p.g.splits == 1) rec.kid = (plan_emu(p) ? 55 : 53) + p.mode;
+    if (p.g.pmode && (p.g.splits == 1 || p.g.fixup)) rec.kid = (plan_emu(p) ? 55 : 53) + p.mode;
     hipEventRecord(rec.a, s);
   }
   switch (p.mode) {
@@ -3365,7 +3477,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     taps_transpose<<<dim3(ceil_div(cin, 64), p.g.M), 256, 0, s>>>(p.g.C, tap_dst, cin, tap_osb, p.g.accum);
     RGAN_CHECK_LAUNCH();
   }
-  if (p.g.splits > 1) {
+  if (p.g.splits > 1 && !p.g.fixup) {
     const GemmArgs& g = p.g;
     const OutMap& o = g.out;
     auto al4 = [](long long v) { return (v & 3) == 0; };
