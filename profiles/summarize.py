@@ -37,7 +37,7 @@ def from_csv(path):
 
 def main():
     src = sys.argv[1]
-    top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+    top = int(sys.argv[2]) if len(sys.argv) > 2 else 100
     if os.path.isdir(src):
         dbs = glob.glob(os.path.join(src, "**", "*.db"), recursive=True)
         csvs = glob.glob(os.path.join(src, "**", "*kernel_stats.csv"), recursive=True)

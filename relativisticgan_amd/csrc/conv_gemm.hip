@@ -47,10 +47,17 @@ constexpr int OOB = (int)0x80000000;
 // fast-path tensors must fit a buffer descriptor with this margin
 constexpr long long FAST_MAX_BYTES = (1LL << 31) - (1LL << 24);
 
-enum { MODE_CONV = 0, MODE_CONVT2 = 1, MODE_WGRAD = 2, MODE_NARROW_T = 3, MODE_NARROW_IN = 4, MODE_DENSE1 = 5 };
+enum { MODE_CONV = 0, MODE_CONVT2 = 1, MODE_WGRAD = 2, MODE_NARROW_T = 3, MODE_NARROW_IN = 4, MODE_DENSE1 = 5,
+       MODE_NARROW3 = 6, MODE_NARROW3W = 7 };
 constexpr int BK = 32;
 #ifndef RGAN_XGROUP
 #define RGAN_XGROUP 1
+#endif
+#ifndef RGAN_NARROW3  // arch 1's 3x3 image layers on the narrow kernels (0: the generic GEMM, for A/B)
+#define RGAN_NARROW3 1
+#endif
+#ifndef RGAN_XGROUP_W  // weight-column XCD grouping for weight-heavy layers (xgroup 2)
+#define RGAN_XGROUP_W 1
 #endif
 #ifndef RGAN_SPLIT_TARGET  // split-K occupancy target (blocks); variant builds sweep it (tools/build_variant.py)
 #define RGAN_SPLIT_TARGET 512
@@ -127,7 +134,7 @@ struct GemmArgs {
   // FAST paths (raw buffer loads, scalar per-tile offsets): descriptor sizes in bytes
   int a_bytes, im_bytes, bw_bytes;
   int vec_out;            // output n-quads contiguous and 16-B aligned (host-checked)
-  int xgroup, nph;        // XCD-grouped tile order (blocks sharing A rows on one XCD); phases
+  int xgroup, nph;        // XCD-grouped tile order (1: blocks sharing A rows on one XCD, 2: sharing weight columns); phases
   double* bnp;            // nullable: BatchNorm moments of every 64-row output segment (vector epilogue)
   int accum;              // WGRAD: add into C (gradient accumulation) instead of overwriting it
   // splits > 1 with fixup: each block writes its partial tile to a tile-major slab
@@ -235,9 +242,20 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   // Tile order.  Default: x = (m tile, n tile), z = (phase, split).  xgroup: blocks are
   // dispatched round-robin over the 8 XCDs, so the blocks that read the same A rows (the
   // n tiles and sub-pixel phases of one m tile) are put 8 dispatch slots apart -- one XCD,
-  // one L2 -- instead of on 4-8 different L2s.
+  // one L2 -- instead of on 4-8 different L2s.  xgroup 2 (layers whose weights outweigh
+  // their input: the deep D convs, G's deep data gradients / ConvTs): the blocks that read
+  // the same weight columns (the m tiles and phases of one n tile) share an XCD instead, so
+  // the weight is fetched into one L2 rather than into every L2 once per m tile.
   int tm_i, tn_i, phase, split, z;
-  if (g.xgroup) {
+  if (g.xgroup == 2) {
+    const int b = blockIdx.x, r = b >> 3, tiles_m = (g.M + BM - 1) / BM, per = tiles_m * g.nph;
+    const int q = r % per;
+    tn_i = (r / per) * 8 + (b & 7);
+    tm_i = q % tiles_m;
+    phase = q / tiles_m;
+    split = blockIdx.z;
+    z = phase * g.splits + split;
+  } else if (g.xgroup) {
     const int b = blockIdx.x, r = b >> 3, per = g.tiles_n * g.nph;
     const int q = r % per;
     tm_i = (r / per) * 8 + (b & 7);
@@ -1699,10 +1717,21 @@ struct NarrowArgs {
   int x_bytes, y_bytes;   // conv_img_in: byte extents of x and y (< 2^31, buffer descriptors)
   int splits = 1, cps = 0;  // convt2_narrow_mfma: input-channel splits (cps channels each, a multiple of 16)
   float* slab = nullptr;  // ... their raw sums [split][b][co][oh][ow] when splits > 1 (narrow_split_reduce)
+  // conv_narrow_in_mfma / conv3_narrow_out: weight element (out n, in c, tap t) at
+  // w[n * w_sn + c * w_sc + (w_flip ? taps - 1 - t : t)] (torch Conv2d layout: w_sn = C * taps,
+  // w_sc = taps; a data gradient reads the kernel transposed and flipped)
+  long long w_sn = 0, w_sc = 0;
+  int w_flip = 0, ks = 4;
+  // wgrad3_narrow: dy (the layer's output gradient) and its strides; chunks of output pixels
+  const float* dy = nullptr;
+  long long dsb = 0, dsc = 0, dsh = 0, dsw = 0;
+  int chunks = 0;
 };
 
-// Conv2d with a 4x4 kernel and CI <= 4 input channels (D's image layer, GLI:410) as ONE MFMA
-// GEMM tile pass: M = output pixels, N = Cout, K = 16*CI (16..64).  K is too short for the
+// Conv2d with a KS x KS kernel (KS = 4: D's image layer GLI:410; KS = 3: arch 1's, GLI:202 /
+// 260, and the data gradient of arch 1's 3-channel output layer) and CI <= 4 input channels as
+// ONE MFMA GEMM tile pass: M = output pixels, N = Cout, K = KS*KS*CI rounded up to 8 (zero
+// weights past the real taps).  K is too short for the
 // pipelined GEMM (one or two BK tiles around a full prologue/epilogue, and a per-element
 // im2col index decomposition in every tile), so a block builds its whole 128 x K im2col
 // tile once (per-row pixel decomposition, per-k (ci, kh, kw) from bit fields), stages the
@@ -1715,9 +1744,9 @@ struct NarrowArgs {
 // 128 ch): 100 us as one VALU thread per pixel, 76 us here; without the stores 53 us --
 // fp32 MFMA and VALU share one issue pipe on gfx950, so the im2col/epilogue VALU is paid
 // in MFMA time.
-template <int CI>
+template <int CI, int KS = 4>
 __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
-  constexpr int K = CI * 16, KH2 = K / 2, LD = K + 4;
+  constexpr int KK = KS * KS, KR = CI * KK, K = (KR + 7) / 8 * 8, KH2 = K / 2, LD = K + 4;
   __shared__ __attribute__((aligned(16))) float As[128 * LD];
   __shared__ __attribute__((aligned(16))) float Bs[128 * LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, lk = lane >> 5;
@@ -1731,8 +1760,9 @@ __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
     float wv[K / 2];
 #pragma unroll
     for (int j = 0; j < K / 2; ++j) {
-      const int e = tid + 256 * j, r = e / K, k = e - r * K, n = n0 + r;
-      wv[j] = n < a.Cout ? a.w[(size_t)n * K + k] : 0.f;
+      const int e = tid + 256 * j, r = e / K, k = e - r * K, n = n0 + r, c = k / KK, t = k - c * KK;
+      wv[j] = (n < a.Cout && k < KR) ? a.w[(long long)n * a.w_sn + (long long)c * a.w_sc + (a.w_flip ? KK - 1 - t : t)]
+                                     : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < K / 2; ++j) {
@@ -1751,8 +1781,8 @@ __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
       const float* xb = a.x + (long long)b * a.xsb;
 #pragma unroll
       for (int kk = 0; kk < KH2; ++kk) {
-        const int k = half * KH2 + kk, ci = k >> 4, ih = ih0 + ((k >> 2) & 3), iw = iw0 + (k & 3);
-        av[kk] = ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+        const int k = half * KH2 + kk, ci = k / KK, t = k - ci * KK, ih = ih0 + t / KS, iw = iw0 + t % KS;
+        av[kk] = (k < KR && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
                      ? xb[(long long)ci * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
                      : 0.f;
       }
@@ -1836,6 +1866,130 @@ __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
     }
     __syncthreads();  // As / moff are rewritten for the next tile
   }
+}
+
+// Conv2d 3x3 stride 1 with NC <= 4 output channels over an NHWC input of C channels (C % 16 ==
+// 0, C <= N3_MAXC): arch 1's image layer (GLI:222-223) and, reading the kernel transposed and
+// flipped, the data gradient of arch 1's 3-channel input layer (GLI:202, the WGAN-GP input
+// gradient).  As an implicit GEMM (N = NC) every MFMA would be >= 7/8 padding; here a thread =
+// one output pixel x a quarter of the channels (channels 16 j + 4 q: the four quarters of a
+// pixel read one 64-B run per step), 4 x NC FMAs per loaded float4 against the weights in LDS
+// ([tap][channel] -> float4 of the NC outputs, broadcast reads), then the four quarters are
+// added by a fixed xor butterfly (a + b == b + a: every lane of the group holds the same sum).
+constexpr int N3_MAXC = 256;
+template <int NC>
+__global__ __launch_bounds__(256) void conv3_narrow_out(NarrowArgs a) {
+  __shared__ float4 ws[9 * N3_MAXC];
+  const int C = a.C;
+  for (int i = threadIdx.x; i < 9 * C; i += 256) {
+    const int t = i / C, c = i - t * C, tw = a.w_flip ? 8 - t : t;
+    float v[4];
+#pragma unroll
+    for (int o = 0; o < 4; ++o) v[o] = o < NC ? a.w[(long long)o * a.w_sn + (long long)c * a.w_sc + tw] : 0.f;
+    ws[i] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  __syncthreads();
+  const int HW = a.Ho * a.Wo, P = a.B * HW;
+  const int pix = blockIdx.x * 64 + (threadIdx.x >> 2), q = threadIdx.x & 3;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int b = 0, oh = 0, ow = 0;
+  if (pix < P) {
+    b = pix / HW;
+    const int r = pix - b * HW;
+    oh = r / a.Wo;
+    ow = r - oh * a.Wo;
+    const float* xb = a.x + (long long)b * a.xsb + 4 * q;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int ih = oh + t / 3 - a.pad, iw = ow + t % 3 - a.pad;
+      if ((unsigned)ih >= (unsigned)a.H || (unsigned)iw >= (unsigned)a.W) continue;
+      const float* xp = xb + (long long)ih * a.xsh + (long long)iw * a.xsw;
+      const float4* wp = ws + t * C + 4 * q;
+      for (int j = 0; j < C; j += 16) {
+        const float4 xv = *reinterpret_cast<const float4*>(xp + j);
+        const float4 w0 = wp[j], w1 = wp[j + 1], w2 = wp[j + 2], w3 = wp[j + 3];
+        acc[0] += xv.x * w0.x + xv.y * w1.x + xv.z * w2.x + xv.w * w3.x;
+        if (NC > 1) acc[1] += xv.x * w0.y + xv.y * w1.y + xv.z * w2.y + xv.w * w3.y;
+        if (NC > 2) acc[2] += xv.x * w0.z + xv.y * w1.z + xv.z * w2.z + xv.w * w3.z;
+        if (NC > 3) acc[3] += xv.x * w0.w + xv.y * w1.w + xv.z * w2.w + xv.w * w3.w;
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 0; o < NC; ++o) {
+    acc[o] += __shfl_xor(acc[o], 1);
+    acc[o] += __shfl_xor(acc[o], 2);
+  }
+  if (pix < P && q == 0) {
+    const float wsc = a.wscale ? a.wscale[0] : 1.f;
+    float* yp = a.y + (long long)b * a.ysb + (long long)oh * a.ysh + (long long)ow * a.ysw;
+#pragma unroll
+    for (int o = 0; o < NC; ++o)
+      yp[(long long)o * a.ysc] = act_fwd(acc[o] * wsc + (a.bias ? a.bias[o] : 0.f), a.act, a.alpha);
+  }
+}
+
+// Weight gradient of a 3x3 stride-1 Conv2d with NC <= 4 channels on one side and CW (% 4 == 0)
+// on the other: dW[co][ci][kh][kw] = sum_p dy[p][co] x[p + (kh, kw) - pad][ci].  WIDE_X: x is
+// the wide side (arch 1's 3-channel output layer: dy has NC channels); else dy is (arch 1's
+// 3-channel input layer).  Thread = (tap, 4 wide channels), block = a chunk of N3W_CH output
+// pixels walked in order; the chunk's 4 x NC partial sums per thread go to a slab in the WGRAD
+// GEMM's [split][co][(kh, kw, ci)] layout, which splitk_reduce(_wide) adds in chunk order into
+// torch layout (and into .grad when accumulating).  (As a GEMM this is M = NC or K = 9 NC: a
+// 128 x 128 tile >= 97 % padding; 1.3-8 TF/s at C4.)
+constexpr int N3W_CH = 128;
+template <int NC, bool WIDE_X>
+__global__ void wgrad3_narrow(NarrowArgs a, int CW) {
+  const int q = threadIdx.x % (CW / 4), t = threadIdx.x / (CW / 4);
+  if (t >= 9) return;
+  const int kh = t / 3, kw = t % 3, HW = a.Ho * a.Wo, P = a.B * HW;
+  const int p0 = blockIdx.x * N3W_CH, p1 = min(P, p0 + N3W_CH);
+  float acc[4][4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[e][c] = 0.f;
+  int b = p0 / HW, r = p0 - b * HW, oh = r / a.Wo, ow = r - oh * a.Wo;
+  for (int p = p0; p < p1; ++p) {
+    const int ih = oh + kh - a.pad, iw = ow + kw - a.pad;
+    if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W) {
+      const float* xp = a.x + (long long)b * a.xsb + (long long)ih * a.xsh + (long long)iw * a.xsw;
+      const float* dp = a.dy + (long long)b * a.dsb + (long long)oh * a.dsh + (long long)ow * a.dsw;
+      float wide[4], nar[4];
+      if constexpr (WIDE_X) {
+        const float4 v = *reinterpret_cast<const float4*>(xp + 4 * q);
+        wide[0] = v.x; wide[1] = v.y; wide[2] = v.z; wide[3] = v.w;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) nar[c] = dp[(long long)c * a.dsc];
+      } else {
+        const float4 v = *reinterpret_cast<const float4*>(dp + 4 * q);
+        wide[0] = v.x; wide[1] = v.y; wide[2] = v.z; wide[3] = v.w;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) nar[c] = xp[(long long)c * a.xsc];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) acc[e][c] += wide[e] * nar[c];
+    }
+    if (++ow == a.Wo) {
+      ow = 0;
+      if (++oh == a.Ho) {
+        oh = 0;
+        ++b;
+      }
+    }
+  }
+  // slab [chunk][co][(t, ci)]: M = Cout rows of N = 9 Cin
+  const int cin = WIDE_X ? CW : NC, cout = WIDE_X ? NC : CW;
+  float* sl = a.slab + (size_t)blockIdx.x * cout * 9 * cin;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int co = WIDE_X ? c : 4 * q + e, ci = WIDE_X ? 4 * q + e : c;
+      sl[((size_t)co * 9 + t) * cin + ci] = acc[e][c];
+    }
 }
 
 // Conv2d k4 s2 p1 over an image with CI <= 3 channels producing Cout % 128 == 0 channels
@@ -2862,7 +3016,9 @@ static bool plan_narrow_t(Plan& p, int batch, const float* x, const long long* x
 // Conv2d with a 4x4 kernel and <= 4 input channels (any input strides)
 static bool plan_narrow_in(Plan& p, const RganConv* d, const float* x, const float* w, const float* wscale,
                            const float* bias, float* y, int act, float alpha) {
-  if (d->transposed || d->cin > 4 || d->kh != 4 || d->kw != 4) return false;
+  const bool k3 = d->kh == 3 && d->kw == 3;
+  if (k3 && !RGAN_NARROW3) return false;
+  if (d->transposed || d->cin > 4 || !((d->kh == 4 && d->kw == 4) || k3)) return false;
   p.mode = MODE_NARROW_IN;
   // the wave-tiled kernel (conv_img_in): k4 s2 p1 halving of an image with <= 3 channels,
   // 128-channel tiles, NHWC output, 32-pixel wave tiles (row segments or two 16-wide rows),
@@ -2871,7 +3027,7 @@ static bool plan_narrow_in(Plan& p, const RganConv* d, const float* x, const flo
                               (d->win - 1) * d->xs[3]);
   const long long yext = 4 * (1 + (d->batch - 1) * d->ys[0] + (d->cout - 1) * d->ys[1] + (d->hout - 1) * d->ys[2] +
                               (d->wout - 1) * d->ys[3]);
-  p.img_in = d->stride == 2 && d->pad == 1 && d->hout * 2 == d->hin &&
+  p.img_in = !k3 && d->stride == 2 && d->pad == 1 && d->hout * 2 == d->hin &&
              d->wout * 2 == d->win && d->cin <= 3 && (d->cout % 128 == 0 || (d->cin == 3 && d->cout % 32 == 0)) &&
              vec_nhwc(y, d->ys, d->cout) &&
              (d->wout == 16 || d->wout % 32 == 0) && ((long long)d->batch * d->hout * d->wout / 32) < (1LL << 31) &&
@@ -2885,6 +3041,60 @@ static bool plan_narrow_in(Plan& p, const RganConv* d, const float* x, const flo
   a.bias = bias; a.wscale = wscale; a.act = act; a.alpha = alpha;
   a.x_bytes = (int)std::min(xext, (1LL << 31) - 1);
   a.y_bytes = (int)std::min(yext, (1LL << 31) - 1);
+  a.ks = d->kh;
+  a.w_sn = (long long)d->cin * d->kh * d->kw;  // torch Conv2d layout
+  a.w_sc = d->kh * d->kw;
+  a.w_flip = 0;
+  p.pack = false;
+  return true;
+}
+
+// Conv2d 3x3 stride 1 with nc <= 4 outputs over an NHWC input of C channels (C % 16 == 0):
+// conv3_narrow_out.  Weight element (out n, in c, tap t) at w[n w_sn + c w_sc + (flip ? 8 - t : t)].
+static bool plan_narrow3_out(Plan& p, int batch, const float* x, const long long* xs, int H, int W, int C,
+                             const float* w, long long w_sn, long long w_sc, int flip, int nc, float* y,
+                             const long long* ys, int Ho, int Wo, int pad, const float* wscale, const float* bias,
+                             int act, float alpha) {
+  if (!RGAN_NARROW3 || nc > 4 || C % 16 != 0 || C > N3_MAXC || xs[1] != 1 || xs[0] % 4 || xs[2] % 4 || xs[3] % 4 || !aligned16(x))
+    return false;
+  if (Ho != H + 2 * pad - 2 || Wo != W + 2 * pad - 2) return false;
+  p.mode = MODE_NARROW3;
+  NarrowArgs& a = p.na;
+  a.x = x; a.xsb = xs[0]; a.xsc = xs[1]; a.xsh = xs[2]; a.xsw = xs[3];
+  a.B = batch; a.H = H; a.W = W; a.C = C;
+  a.w = w; a.w_sn = w_sn; a.w_sc = w_sc; a.w_flip = flip;
+  a.y = y; a.ysb = ys[0]; a.ysc = ys[1]; a.ysh = ys[2]; a.ysw = ys[3];
+  a.Ho = Ho; a.Wo = Wo; a.Cout = nc; a.stride = 1; a.pad = pad;
+  a.bias = bias; a.wscale = wscale; a.act = act; a.alpha = alpha;
+  p.pack = false;
+  return true;
+}
+
+// weight gradient of a 3x3 stride-1 Conv2d with <= 4 channels on one side (wgrad3_narrow +
+// the WGRAD split reduce); the wide side NHWC with channels % 4 == 0
+static bool plan_wgrad3_narrow(Plan& p, const RganConv* d, const float* x, const float* dy, float* dw) {
+  if (!RGAN_NARROW3 || d->transposed || d->kh != 3 || d->kw != 3 || d->stride != 1) return false;
+  const bool wide_x = d->cout <= 4;
+  const int cw = wide_x ? d->cin : d->cout;
+  if (!wide_x && d->cin > 4) return false;
+  const long long* ws = wide_x ? d->xs : d->ys;
+  const float* wp = wide_x ? x : dy;
+  if (cw % 4 || 9 * (cw / 4) > 1024 || ws[1] != 1 || ws[0] % 4 || ws[2] % 4 || ws[3] % 4 || !aligned16(wp)) return false;
+  p.mode = MODE_NARROW3W;
+  NarrowArgs& a = p.na;
+  a.x = x; a.xsb = d->xs[0]; a.xsc = d->xs[1]; a.xsh = d->xs[2]; a.xsw = d->xs[3];
+  a.dy = dy; a.dsb = d->ys[0]; a.dsc = d->ys[1]; a.dsh = d->ys[2]; a.dsw = d->ys[3];
+  a.B = d->batch; a.H = d->hin; a.W = d->win; a.C = d->cin;
+  a.Ho = d->hout; a.Wo = d->wout; a.Cout = d->cout; a.stride = 1; a.pad = d->pad;
+  const long long P = (long long)d->batch * d->hout * d->wout;
+  a.chunks = (int)ceil_div(P, (long long)N3W_CH);
+  p.slab_floats = (size_t)a.chunks * d->cout * 9 * d->cin;
+  // the reduce: the WGRAD GEMM's [split][M = cout][N = (kh, kw, ci)] slab into torch layout
+  GemmArgs& g = p.g;
+  g.M = d->cout; g.N = 9 * d->cin; g.K = (int)P; g.splits = a.chunks;
+  g.C = dw; g.bias = nullptr; g.wscale = nullptr; g.act = RGAN_ACT_NONE; g.alpha = 0.f; g.pmode = 0;
+  g.out = make_out(1, 1, 1, (long long)d->cin * 9, 0, 0, 3, 3, d->cin, 3, 1, 9);
+  p.phases = 1;
   p.pack = false;
   return true;
 }
@@ -2926,6 +3136,10 @@ static int plan_fwd(const RganConv* d, const float* x, const float* w, const flo
     return 0;
   if (plan_narrow_in(p, d, x, w, wscale, bias, y, act, alpha)) return 0;
   if (plan_dense1(p, d, 0, x, w, wscale, bias, y, nullptr, act, alpha)) return 0;
+  if (!d->transposed && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->cout <= 4 &&
+      plan_narrow3_out(p, d->batch, x, d->xs, d->hin, d->win, d->cin, w, (long long)d->cin * 9, 9, 0, d->cout, y,
+                       d->ys, d->hout, d->wout, d->pad, wscale, bias, act, alpha))
+    return 0;
   g.a = make_img(x, d->hin, d->win, d->cin, d->xs);
   g.C = y; g.bias = bias; g.act = act; g.alpha = alpha;
   if (!d->transposed) {
@@ -3002,6 +3216,28 @@ static int plan_dgrad(const RganConv* d, const float* dy, const float* w, const 
     for (int i = 0; i < 4; ++i) { c.xs[i] = d->ys[i]; c.ys[i] = d->xs[i]; }
     if (plan_narrow_in(p, &c, dy, w, wscale, nullptr, dx, RGAN_ACT_NONE, 0.f)) return 0;
   }
+  // 3x3 stride-1 Conv2d: the data gradient is the conv of dy with the kernel transposed and
+  // flipped (pad 2 - p): <= 4 dy channels -> the narrow-in kernel, <= 4 dx channels -> the
+  // narrow-out one; W[co][ci][t] read as [out = ci][in = co][8 - t]
+  if (!d->transposed && d->kh == 3 && d->kw == 3 && d->stride == 1) {
+    if (d->cout <= 4) {
+      RganConv c = *d;
+      c.cin = d->cout; c.hin = d->hout; c.win = d->wout;
+      c.cout = d->cin; c.hout = d->hin; c.wout = d->win;
+      c.pad = 2 - d->pad;
+      for (int i = 0; i < 4; ++i) { c.xs[i] = d->ys[i]; c.ys[i] = d->xs[i]; }
+      if (plan_narrow_in(p, &c, dy, w, wscale, nullptr, dx, RGAN_ACT_NONE, 0.f)) {
+        p.na.w_sn = 9;
+        p.na.w_sc = (long long)d->cin * 9;
+        p.na.w_flip = 1;
+        return 0;
+      }
+    } else if (d->cin <= 4 &&
+               plan_narrow3_out(p, d->batch, dy, d->ys, d->hout, d->wout, d->cout, w, 9, (long long)d->cin * 9, 1,
+                                d->cin, dx, d->xs, d->hin, d->win, 2 - d->pad, wscale, nullptr, RGAN_ACT_NONE, 0.f)) {
+      return 0;
+    }
+  }
   g.a = make_img(dy, d->hout, d->wout, d->cout, d->ys);
   g.C = dx; g.bias = nullptr; g.act = RGAN_ACT_NONE; g.alpha = 0.f;
   g.out = make_out(d->hin, d->win, 1, d->xs[0], d->xs[2], d->xs[3], 1, 1, d->cin, 0, 0, d->xs[1]);
@@ -3049,6 +3285,7 @@ static int plan_dgrad(const RganConv* d, const float* dy, const float* w, const 
 static int plan_wgrad(const RganConv* d, const float* x, const float* dy, float* dw, Plan& p) {
   if (!desc_ok(d)) return RGAN_EINVAL;
   if (plan_dense1(p, d, 2, x, nullptr, nullptr, nullptr, const_cast<float*>(dy), dw, RGAN_ACT_NONE, 0.f)) return 0;
+  if (plan_wgrad3_narrow(p, d, x, dy, dw)) return 0;
   GemmArgs& g = p.g;
   const int KK = d->kh * d->kw;
   p.mode = MODE_WGRAD;
@@ -3190,12 +3427,14 @@ static std::vector<ProfRec> g_recs;
 static std::vector<std::string> g_kernel_names;
 static double g_cur_flops = 0.0;
 
-constexpr int N_KERNEL_IDS = 57;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in + 2 bf16x6 + 2 post + 2 post bf16x6
+constexpr int N_KERNEL_IDS = 59;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in + 2 bf16x6 + 2 post + 2 post bf16x6 + 2 narrow 3x3
 
 static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
   const int id = mode == MODE_NARROW_T ? 45
                  : mode == MODE_NARROW_IN ? 46
                  : mode == MODE_DENSE1 ? 47 + cfg
+                 : mode == MODE_NARROW3 ? 57
+                 : mode == MODE_NARROW3W ? 58
                  : fast ? 36 + mode * 3 + cfg
                         : ((mode * 3 + cfg) * 2 + (av ? 1 : 0)) * 2 + (bv ? 1 : 0);
   if (g_kernel_names.empty()) {
@@ -3229,6 +3468,8 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
     g_kernel_names[54] = "void rgan::gemm_post<1>(rgan::GemmArgs)";
     g_kernel_names[55] = "void rgan::gemm_post_bf16x6<0>(rgan::GemmArgs)";
     g_kernel_names[56] = "void rgan::gemm_post_bf16x6<1>(rgan::GemmArgs)";
+    g_kernel_names[57] = "void rgan::conv3_narrow_out<NC>(rgan::NarrowArgs)";
+    g_kernel_names[58] = "void rgan::wgrad3_narrow<NC, WIDE_X>(rgan::NarrowArgs, int)";
   }
   return id;
 }
@@ -3289,12 +3530,59 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
   } else {
     // persistent: two resident blocks per CU loop over the M tiles
     dim3 grid(std::min(ceil_div(a.B * a.Ho * a.Wo, 128), 512), ceil_div(a.Cout, 128));
-    switch (a.C) {
-      case 1: conv_narrow_in_mfma<1><<<grid, 256, 0, s>>>(a); break;
-      case 2: conv_narrow_in_mfma<2><<<grid, 256, 0, s>>>(a); break;
-      case 3: conv_narrow_in_mfma<3><<<grid, 256, 0, s>>>(a); break;
-      default: conv_narrow_in_mfma<4><<<grid, 256, 0, s>>>(a); break;
+    if (a.ks == 3) {
+      switch (a.C) {
+        case 1: conv_narrow_in_mfma<1, 3><<<grid, 256, 0, s>>>(a); break;
+        case 2: conv_narrow_in_mfma<2, 3><<<grid, 256, 0, s>>>(a); break;
+        case 3: conv_narrow_in_mfma<3, 3><<<grid, 256, 0, s>>>(a); break;
+        default: conv_narrow_in_mfma<4, 3><<<grid, 256, 0, s>>>(a); break;
+      }
+    } else {
+      switch (a.C) {
+        case 1: conv_narrow_in_mfma<1><<<grid, 256, 0, s>>>(a); break;
+        case 2: conv_narrow_in_mfma<2><<<grid, 256, 0, s>>>(a); break;
+        case 3: conv_narrow_in_mfma<3><<<grid, 256, 0, s>>>(a); break;
+        default: conv_narrow_in_mfma<4><<<grid, 256, 0, s>>>(a); break;
+      }
     }
+  }
+  return 0;
+}
+
+static int run_narrow3(Plan& p, hipStream_t s) {
+  NarrowArgs a = p.na;
+  if (p.mode == MODE_NARROW3) {
+    const unsigned blocks = (unsigned)ceil_div((long long)a.B * a.Ho * a.Wo, 64LL);
+    switch (a.Cout) {
+      case 1: conv3_narrow_out<1><<<blocks, 256, 0, s>>>(a); break;
+      case 2: conv3_narrow_out<2><<<blocks, 256, 0, s>>>(a); break;
+      case 3: conv3_narrow_out<3><<<blocks, 256, 0, s>>>(a); break;
+      default: conv3_narrow_out<4><<<blocks, 256, 0, s>>>(a); break;
+    }
+    return 0;
+  }
+  const bool wide_x = a.Cout <= 4;
+  const int nc = wide_x ? a.Cout : a.C, cw = wide_x ? a.C : a.Cout;
+  const int threads = ceil_div(9 * (cw / 4), 64) * 64;
+#define RGAN_W3(NN)                                                                                 \
+  if (wide_x) wgrad3_narrow<NN, true><<<a.chunks, threads, 0, s>>>(a, cw);                         \
+  else wgrad3_narrow<NN, false><<<a.chunks, threads, 0, s>>>(a, cw);
+  switch (nc) {
+    case 1: RGAN_W3(1) break;
+    case 2: RGAN_W3(2) break;
+    case 3: RGAN_W3(3) break;
+    default: RGAN_W3(4) break;
+  }
+#undef RGAN_W3
+  RGAN_CHECK_LAUNCH();
+  GemmArgs g = p.g;
+  g.slab = a.slab;
+  const uint32_t per = (uint32_t)g.M * g.N;
+  const FastDiv fd((uint32_t)g.N);
+  if (g.splits >= 4 * REDW_LANES && per <= 65536) {
+    splitk_reduce_wide<MODE_WGRAD><<<dim3((unsigned)ceil_div((long long)per, REDW_OUT), 1), 256, 0, s>>>(g, fd, per);
+  } else {
+    splitk_reduce<MODE_WGRAD, RED_ANY><<<dim3(std::min<uint32_t>((per + 255) / 256, 8192), 1), 256, 0, s>>>(g, fd, per);
   }
   return 0;
 }
@@ -3371,7 +3659,8 @@ static bool post_ok(const Plan& p, int mode, int nseg, bool check_ptr) {
 
 static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   if (ws_bytes < plan_ws_bytes(p)) return RGAN_EINVAL;
-  if (p.mode == MODE_NARROW_T || p.mode == MODE_NARROW_IN || p.mode == MODE_DENSE1) {
+  if (p.mode == MODE_NARROW_T || p.mode == MODE_NARROW_IN || p.mode == MODE_DENSE1 || p.mode == MODE_NARROW3 ||
+      p.mode == MODE_NARROW3W) {
     const float* packed = p.prepacked;
     if (p.pack && !packed) {
       if (!ws) return RGAN_EINVAL;
@@ -3392,6 +3681,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
       hipEventRecord(rec.a, s);
     }
     if (p.mode == MODE_DENSE1) run_dense1(p, packed, s);
+    else if (p.mode == MODE_NARROW3 || p.mode == MODE_NARROW3W) run_narrow3(p, s);
     else run_narrow(p, packed, s);
     RGAN_CHECK_LAUNCH();
     if (prof) {
@@ -3448,6 +3738,15 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   const int tiles_m = ceil_div(p.g.M, bm);
   p.g.nph = p.phases;
   p.g.xgroup = RGAN_XGROUP && p.fast && p.mode != MODE_WGRAD && tiles_m % 8 == 0 && p.g.tiles_n * p.phases > 1;
+  // weight-column grouping where the weights dominate: under A-row grouping every XCD fetches
+  // the whole weight (D's 2048 -> 4096 conv at C3: 4.36 GB of FETCH per launch for a 537 MB
+  // weight; 1.01 GB grouped by weight columns).  Under weight-column grouping every XCD reads
+  // the input through its im2col windows instead, which costs more than the input's bytes: at
+  // a 2:1 weight / input ratio (D's 1024 -> 2048 conv) it fetched 2.02 GB against 1.33, hence
+  // the factor 4 (run r4g)
+  if (RGAN_XGROUP_W && p.fast && p.mode != MODE_WGRAD && p.g.tiles_n % 8 == 0 &&
+      (long long)p.g.bw_bytes * p.phases > 4LL * p.g.a_bytes && tiles_m * p.phases > 1)
+    p.g.xgroup = 2;
   dim3 grid = p.g.xgroup ? dim3(tiles_m * p.g.tiles_n * p.phases, 1, p.g.splits)
                          : dim3(tiles_m * p.g.tiles_n, 1, p.phases * p.g.splits);
   ProfRec rec{};

@@ -1133,3 +1133,48 @@ def test_wgrad_write_accumulate_into(K, B, cin, cout, H, tr):
     into = torch.full(wshape, float("nan"), device=DEV)
     K.conv_wgrad(x, dy, g, wshape, into=into)
     assert torch.equal(into, dw)
+
+
+# arch 1's 3x3 stride-1 image layers (GLI:202 / 222-223, 260 / 300-301): narrow-in MFMA tile
+# (conv_narrow_in_mfma<CI, 3>), narrow-out per-pixel kernel (conv3_narrow_out) and the narrow
+# weight gradient (wgrad3_narrow + the WGRAD split reduce).  (B, H): pixel counts below one
+# chunk, a few chunks (generic reduce) and the C4 shape (wide reduce).
+@pytest.mark.parametrize("nc", [1, 3, 4])
+@pytest.mark.parametrize("B,H", [(2, 5), (3, 16), (32, 32)])
+def test_conv3x3_narrow_layers(K, nc, B, H):
+    g = K.ConvGeom(3, 1, 1, False)
+    torch.manual_seed(nc * 100 + B)
+    s = torch.tensor([0.5], device=DEV)
+    # D's input layer: nc -> 64 over the NCHW image
+    img = torch.randn(B, nc, H, H, device=DEV)
+    w_in = torch.randn(64, nc, 3, 3, device=DEV) * 0.2
+    b_in = torch.randn(64, device=DEV)
+    y = K.conv_fwd(img, w_in, g, bias=b_in, act="lrelu", alpha=0.1, wscale=s)
+    assert _rel(y, F.leaky_relu(_ref_conv(img, w_in * 0.5, g, b_in), 0.1)) < 3e-6
+    dy = _nhwc(torch.randn(B, 64, H, H, device=DEV))
+    x64 = img.double().cpu().requires_grad_(True)
+    w64 = (w_in * 0.5).double().cpu().requires_grad_(True)
+    F.conv2d(x64, w64, padding=1).backward(dy.double().cpu())
+    dx = K.conv_dgrad(dy, w_in, g, img.shape, wscale=s, like=img)
+    assert _rel(dx, x64.grad) < 3e-6
+    dw, db = K.conv_wgrad(img, dy, g, w_in.shape, with_bias=True)
+    assert _rel(dw, w64.grad) < 3e-6
+    assert _rel(db, dy.double().cpu().sum((0, 2, 3))) < 3e-6
+    acc = torch.randn_like(w_in)
+    base = acc.clone()
+    K.conv_wgrad(img, dy, g, w_in.shape, out=acc)
+    assert _rel(acc - base, w64.grad) < 2e-5
+    # G's output layer: 64 -> nc, NCHW image out with tanh
+    x = _nhwc(torch.randn(B, 64, H, H, device=DEV))
+    w_out = torch.randn(nc, 64, 3, 3, device=DEV) * 0.1
+    b_out = torch.randn(nc, device=DEV)
+    y = K.conv_fwd(x, w_out, g, bias=b_out, act="tanh", wscale=s, nchw_out=True)
+    assert _rel(y, torch.tanh(_ref_conv(x, w_out * 0.5, g, b_out))) < 3e-6
+    gy = torch.randn(B, nc, H, H, device=DEV)
+    x64 = x.double().cpu().requires_grad_(True)
+    w64 = (w_out * 0.5).double().cpu().requires_grad_(True)
+    F.conv2d(x64, w64, padding=1).backward(gy.double().cpu())
+    dx = K.conv_dgrad(gy, w_out, g, x.shape, wscale=s)
+    assert _rel(dx, x64.grad) < 3e-6
+    dw, _ = K.conv_wgrad(x, gy, g, w_out.shape)
+    assert _rel(dw, w64.grad) < 3e-6

@@ -5,7 +5,7 @@ workload and records, per call, the library's HIP-event GEMM time and algorithmi
 FLOPs (profile_begin/profile_end around the call).  Prints a table aggregated by
 (op, shapes, kernel) sorted by total time.
 
-usage: python tools/conv_breakdown.py [C2|C1|C3|C5] [iters]
+usage: python tools/conv_breakdown.py [C1|C2|C3|C4|C4p|C5] [iters]
 """
 import collections
 import os
@@ -16,7 +16,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-from bench import WORKLOADS  # noqa: E402
+from bench import ARCH, WORKLOADS  # noqa: E402
 from relativisticgan_amd import kernels as K  # noqa: E402
 from relativisticgan_amd.config import make_param  # noqa: E402
 from relativisticgan_amd.train import Trainer, synthetic_images  # noqa: E402
@@ -52,7 +52,7 @@ def main():
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     loss_D, size, bpg, h = WORKLOADS[wl]
     p = make_param(loss_D=loss_D, image_size=size, batch_size=bpg, G_h_size=h, D_h_size=h, seed=1,
-                   print_every=10 ** 9, spectral=wl == "C5", rgan_rng="device")
+                   print_every=10 ** 9, spectral=wl == "C5", rgan_rng="device", arch=ARCH.get(wl, 0))
     t = Trainer(p, synthetic_images(1024, size, device="cuda"))
     K.conv_fwd = wrap("fwd", K.conv_fwd, lambda x, w, geom, *a, **kw: (tuple(x.shape), tuple(w.shape), g(geom)))
     K.conv_fwd_bn = wrap("fwd_bn", K.conv_fwd_bn, lambda x, w, geom, *a, **kw: (tuple(x.shape), tuple(w.shape),
