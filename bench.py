@@ -251,7 +251,8 @@ def _run_workload(name, steps, warmup, world, args, K, dp_path=False, host_rng=F
     # whose gradient buckets all-reduce overlapped with the backward (a captured backward
     # cannot launch them mid-way)
     n_params = sum(q.numel() for q in list(t.G.parameters()) + list(t.D.parameters()))
-    multi = world > 1 or dp_path
+    from relativisticgan_amd import dp as _dpm
+    multi = world > 1 or dp_path or _dpm.active()
     if host_rng:
         mode = "eager"
     elif args.graph == "auto":
@@ -478,6 +479,10 @@ def main():
     ap.add_argument("--no-hbm", action="store_true", help="skip the HBM-bound kernels' GB/s table (hbm_kernels)")
     ap.add_argument("--sync-bn", action="store_true",
                     help="SyncBN over ranks (default: per-shard BN = the reference's DataParallel)")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="run the data-parallel path (process group, distributed heads, gradient buckets on "
+                         "the second communicator) even with one rank: a one-GPU rehearsal of the N > 1 "
+                         "collectives over RCCL (RGAN_BENCH_BACKEND, default nccl)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -489,13 +494,18 @@ def main():
         local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     from relativisticgan_amd import dp, kernels as K
-    if world > 1:
+    distributed = world > 1 or args.force_dp
+    if distributed:
         import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-        dp.setup(sync_bn=args.sync_bn)
+        dp.setup(sync_bn=args.sync_bn, force=args.force_dp)
     res = run_workload(args.workload, args.steps, args.warmup, world, args, K)
     emu_res = None
     if world == 1 and not args.no_emu_extra:
@@ -537,7 +547,8 @@ def main():
                    "D_h_size": res["h"], "arch": res["arch"], "parallelism": f"dp{world}",
                    "batched_D_step": res["batch_D"], "hip_graph": res["graph"], "launch_mode": res["mode"],
                    "graph_segments": res["segments"],
-                   "batchnorm": "SyncBN" if args.sync_bn else "per-shard (reference DataParallel)"},
+                   "batchnorm": "SyncBN" if args.sync_bn else "per-shard (reference DataParallel)",
+                   "forced_dp": bool(args.force_dp)},
         "step_mfma_util": res["flops_iter"] * args.steps / res["elapsed"] / (world * FP32_MFMA_PEAK),
         "conv_tflop_per_step": res["flops_iter"] / 1e12,
         "roofline": roofline_of(res, args.workload),
@@ -567,7 +578,7 @@ def main():
                                            args.cpu_seconds, arch=res["arch"])
         out["cpu_baseline"]["restatement_check"] = restatement_check()
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         torch.distributed.destroy_process_group()
 
 

@@ -1717,21 +1717,19 @@ struct NarrowArgs {
   int x_bytes, y_bytes;   // conv_img_in: byte extents of x and y (< 2^31, buffer descriptors)
   int splits = 1, cps = 0;  // convt2_narrow_mfma: input-channel splits (cps channels each, a multiple of 16)
   float* slab = nullptr;  // ... their raw sums [split][b][co][oh][ow] when splits > 1 (narrow_split_reduce)
-  // conv_narrow_in_mfma / conv3_narrow_out: weight element (out n, in c, tap t) at
+  // conv3_narrow_out: weight element (out n, in c, tap t) at
   // w[n * w_sn + c * w_sc + (w_flip ? taps - 1 - t : t)] (torch Conv2d layout: w_sn = C * taps,
   // w_sc = taps; a data gradient reads the kernel transposed and flipped)
   long long w_sn = 0, w_sc = 0;
-  int w_flip = 0, ks = 4;
-  // wgrad3_narrow: dy (the layer's output gradient) and its strides; chunks of output pixels
+  int w_flip = 0;
+  // wgrad3_narrow: dy (the layer's output gradient) and its strides; blocks of `rows` output rows
   const float* dy = nullptr;
   long long dsb = 0, dsc = 0, dsh = 0, dsw = 0;
-  int chunks = 0;
+  int chunks = 0, rows = 0;
 };
 
-// Conv2d with a KS x KS kernel (KS = 4: D's image layer GLI:410; KS = 3: arch 1's, GLI:202 /
-// 260, and the data gradient of arch 1's 3-channel output layer) and CI <= 4 input channels as
-// ONE MFMA GEMM tile pass: M = output pixels, N = Cout, K = KS*KS*CI rounded up to 8 (zero
-// weights past the real taps).  K is too short for the
+// Conv2d with a 4x4 kernel and CI <= 4 input channels (D's image layer, GLI:410) as ONE MFMA
+// GEMM tile pass: M = output pixels, N = Cout, K = 16*CI (16..64).  K is too short for the
 // pipelined GEMM (one or two BK tiles around a full prologue/epilogue, and a per-element
 // im2col index decomposition in every tile), so a block builds its whole 128 x K im2col
 // tile once (per-row pixel decomposition, per-k (ci, kh, kw) from bit fields), stages the
@@ -1744,9 +1742,9 @@ struct NarrowArgs {
 // 128 ch): 100 us as one VALU thread per pixel, 76 us here; without the stores 53 us --
 // fp32 MFMA and VALU share one issue pipe on gfx950, so the im2col/epilogue VALU is paid
 // in MFMA time.
-template <int CI, int KS = 4>
+template <int CI>
 __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
-  constexpr int KK = KS * KS, KR = CI * KK, K = (KR + 7) / 8 * 8, KH2 = K / 2, LD = K + 4;
+  constexpr int K = CI * 16, KH2 = K / 2, LD = K + 4;
   __shared__ __attribute__((aligned(16))) float As[128 * LD];
   __shared__ __attribute__((aligned(16))) float Bs[128 * LD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, l32 = lane & 31, lk = lane >> 5;
@@ -1760,9 +1758,8 @@ __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
     float wv[K / 2];
 #pragma unroll
     for (int j = 0; j < K / 2; ++j) {
-      const int e = tid + 256 * j, r = e / K, k = e - r * K, n = n0 + r, c = k / KK, t = k - c * KK;
-      wv[j] = (n < a.Cout && k < KR) ? a.w[(long long)n * a.w_sn + (long long)c * a.w_sc + (a.w_flip ? KK - 1 - t : t)]
-                                     : 0.f;
+      const int e = tid + 256 * j, r = e / K, k = e - r * K, n = n0 + r;
+      wv[j] = n < a.Cout ? a.w[(size_t)n * K + k] : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < K / 2; ++j) {
@@ -1781,8 +1778,8 @@ __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
       const float* xb = a.x + (long long)b * a.xsb;
 #pragma unroll
       for (int kk = 0; kk < KH2; ++kk) {
-        const int k = half * KH2 + kk, ci = k / KK, t = k - ci * KK, ih = ih0 + t / KS, iw = iw0 + t % KS;
-        av[kk] = (k < KR && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+        const int k = half * KH2 + kk, ci = k >> 4, ih = ih0 + ((k >> 2) & 3), iw = iw0 + (k & 3);
+        av[kk] = ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
                      ? xb[(long long)ci * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
                      : 0.f;
       }
@@ -1929,67 +1926,73 @@ __global__ __launch_bounds__(256) void conv3_narrow_out(NarrowArgs a) {
   }
 }
 
-// Weight gradient of a 3x3 stride-1 Conv2d with NC <= 4 channels on one side and CW (% 4 == 0)
-// on the other: dW[co][ci][kh][kw] = sum_p dy[p][co] x[p + (kh, kw) - pad][ci].  WIDE_X: x is
-// the wide side (arch 1's 3-channel output layer: dy has NC channels); else dy is (arch 1's
-// 3-channel input layer).  Thread = (tap, 4 wide channels), block = a chunk of N3W_CH output
-// pixels walked in order; the chunk's 4 x NC partial sums per thread go to a slab in the WGRAD
-// GEMM's [split][co][(kh, kw, ci)] layout, which splitk_reduce(_wide) adds in chunk order into
-// torch layout (and into .grad when accumulating).  (As a GEMM this is M = NC or K = 9 NC: a
-// 128 x 128 tile >= 97 % padding; 1.3-8 TF/s at C4.)
-constexpr int N3W_CH = 128;
-template <int NC, bool WIDE_X>
-__global__ void wgrad3_narrow(NarrowArgs a, int CW) {
-  const int q = threadIdx.x % (CW / 4), t = threadIdx.x / (CW / 4);
+// Weight gradient of a 3x3 stride-1 pad-1 Conv2d with NC <= 4 output channels over a CW-channel
+// input (CW % 4 == 0; arch 1's 3-channel output layer, GLI:222): dW[co][ci][kh][kw] = sum_p
+// dy[p][co] x[p + (kh, kw) - 1][ci].  A block owns R whole output rows of one image (R * Wo <=
+// N3W_PIX): it first stages their dy rows and the R + 2 x rows around them (zero halo) in LDS
+// with every thread's loads in flight together, then thread (tap, 4 input channels) accumulates
+// its 4 x NC outputs over the block's pixels in order from LDS.  The per-block partials go to a
+// slab in the WGRAD GEMM's [split][co][(kh, kw, ci)] layout, which splitk_reduce(_wide) adds in
+// block order into torch layout (and into .grad when accumulating).  As a GEMM this is M = NC:
+// a 128 x 128 tile >= 97 % padding (88 us per C4 call; 42 us here, incl. the reduce).  The
+// mirror case (<= 4 input channels, arch 1's input layer) stays on the GEMM: the same staging
+// measured 40 us per call against its 29 us (K = 9 NC is only short, M is full).
+constexpr int N3W_PIX = 128;
+template <int NC>
+__global__ void wgrad3_narrow(NarrowArgs a, int CW, int R) {
+  extern __shared__ __attribute__((aligned(16))) float sm3[];
+  const int Wo = a.Wo, XW = Wo + 2;
+  float* xs = sm3;                          // [(R + 2) * XW][CW]
+  float* ds = sm3 + (R + 2) * XW * CW;      // [R * Wo][NC]
+  const int rows_per_img = (a.Ho + R - 1) / R, b = blockIdx.x / rows_per_img;
+  const int oh0 = (blockIdx.x - b * rows_per_img) * R, nr = min(R, a.Ho - oh0);
+  const int tid = threadIdx.x, nt = blockDim.x;
+  // stage: x rows oh0 - 1 .. oh0 + nr (zero outside the image), dy rows oh0 .. oh0 + nr - 1
+  const int xn = (R + 2) * XW * CW;
+  for (int i = tid; i < xn; i += nt) {
+    const int c = i % CW, pix = i / CW, rr = pix / XW, cc = pix - rr * XW;
+    const int ih = oh0 - 1 + rr, iw = cc - 1;
+    xs[i] = (rr < nr + 2 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                ? a.x[(long long)b * a.xsb + (long long)c * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
+                : 0.f;
+  }
+  const int dn = nr * Wo * NC;
+  for (int i = tid; i < dn; i += nt) {
+    const int c = i % NC, pix = i / NC, rr = pix / Wo, cc = pix - rr * Wo;
+    ds[i] = a.dy[(long long)b * a.dsb + (long long)c * a.dsc + (long long)(oh0 + rr) * a.dsh + (long long)cc * a.dsw];
+  }
+  __syncthreads();
+  const int q = tid % (CW / 4), t = tid / (CW / 4);
   if (t >= 9) return;
-  const int kh = t / 3, kw = t % 3, HW = a.Ho * a.Wo, P = a.B * HW;
-  const int p0 = blockIdx.x * N3W_CH, p1 = min(P, p0 + N3W_CH);
-  float acc[4][4];
+  const int kh = t / 3, kw = t % 3;
+  float acc[4][NC];
 #pragma unroll
   for (int e = 0; e < 4; ++e)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) acc[e][c] = 0.f;
-  int b = p0 / HW, r = p0 - b * HW, oh = r / a.Wo, ow = r - oh * a.Wo;
-  for (int p = p0; p < p1; ++p) {
-    const int ih = oh + kh - a.pad, iw = ow + kw - a.pad;
-    if ((unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W) {
-      const float* xp = a.x + (long long)b * a.xsb + (long long)ih * a.xsh + (long long)iw * a.xsw;
-      const float* dp = a.dy + (long long)b * a.dsb + (long long)oh * a.dsh + (long long)ow * a.dsw;
-      float wide[4], nar[4];
-      if constexpr (WIDE_X) {
-        const float4 v = *reinterpret_cast<const float4*>(xp + 4 * q);
-        wide[0] = v.x; wide[1] = v.y; wide[2] = v.z; wide[3] = v.w;
-#pragma unroll
-        for (int c = 0; c < NC; ++c) nar[c] = dp[(long long)c * a.dsc];
-      } else {
-        const float4 v = *reinterpret_cast<const float4*>(dp + 4 * q);
-        wide[0] = v.x; wide[1] = v.y; wide[2] = v.z; wide[3] = v.w;
-#pragma unroll
-        for (int c = 0; c < NC; ++c) nar[c] = xp[(long long)c * a.xsc];
-      }
+    for (int c = 0; c < NC; ++c) acc[e][c] = 0.f;
+  for (int rr = 0; rr < nr; ++rr) {
+    const float* xr = xs + ((rr + kh) * XW + kw) * CW + 4 * q;
+    const float* dr = ds + rr * Wo * NC;
+    for (int cc = 0; cc < Wo; ++cc) {
+      const float4 xv = *reinterpret_cast<const float4*>(xr + cc * CW);
+      const float x4[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int c = 0; c < NC; ++c) acc[e][c] += wide[e] * nar[c];
-    }
-    if (++ow == a.Wo) {
-      ow = 0;
-      if (++oh == a.Ho) {
-        oh = 0;
-        ++b;
-      }
+        for (int c = 0; c < NC; ++c) acc[e][c] += x4[e] * dr[cc * NC + c];
     }
   }
-  // slab [chunk][co][(t, ci)]: M = Cout rows of N = 9 Cin
-  const int cin = WIDE_X ? CW : NC, cout = WIDE_X ? NC : CW;
-  float* sl = a.slab + (size_t)blockIdx.x * cout * 9 * cin;
+  // slab [block][co][(t, ci)]: M = NC rows of N = 9 CW
+  float* sl = a.slab + (size_t)blockIdx.x * NC * 9 * CW;
 #pragma unroll
   for (int e = 0; e < 4; ++e)
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int co = WIDE_X ? c : 4 * q + e, ci = WIDE_X ? 4 * q + e : c;
-      sl[((size_t)co * 9 + t) * cin + ci] = acc[e][c];
-    }
+    for (int c = 0; c < NC; ++c) sl[((size_t)c * 9 + t) * CW + 4 * q + e] = acc[e][c];
+}
+
+// bytes of wgrad3_narrow's LDS staging for R output rows
+static inline size_t wgrad3_lds_bytes(int R, int Wo, int CW, int NC) {
+  return (size_t)((R + 2) * (Wo + 2) * CW + R * Wo * NC) * 4;
 }
 
 // Conv2d k4 s2 p1 over an image with CI <= 3 channels producing Cout % 128 == 0 channels
@@ -3016,9 +3019,7 @@ static bool plan_narrow_t(Plan& p, int batch, const float* x, const long long* x
 // Conv2d with a 4x4 kernel and <= 4 input channels (any input strides)
 static bool plan_narrow_in(Plan& p, const RganConv* d, const float* x, const float* w, const float* wscale,
                            const float* bias, float* y, int act, float alpha) {
-  const bool k3 = d->kh == 3 && d->kw == 3;
-  if (k3 && !RGAN_NARROW3) return false;
-  if (d->transposed || d->cin > 4 || !((d->kh == 4 && d->kw == 4) || k3)) return false;
+  if (d->transposed || d->cin > 4 || d->kh != 4 || d->kw != 4) return false;
   p.mode = MODE_NARROW_IN;
   // the wave-tiled kernel (conv_img_in): k4 s2 p1 halving of an image with <= 3 channels,
   // 128-channel tiles, NHWC output, 32-pixel wave tiles (row segments or two 16-wide rows),
@@ -3027,7 +3028,7 @@ static bool plan_narrow_in(Plan& p, const RganConv* d, const float* x, const flo
                               (d->win - 1) * d->xs[3]);
   const long long yext = 4 * (1 + (d->batch - 1) * d->ys[0] + (d->cout - 1) * d->ys[1] + (d->hout - 1) * d->ys[2] +
                               (d->wout - 1) * d->ys[3]);
-  p.img_in = !k3 && d->stride == 2 && d->pad == 1 && d->hout * 2 == d->hin &&
+  p.img_in = d->stride == 2 && d->pad == 1 && d->hout * 2 == d->hin &&
              d->wout * 2 == d->win && d->cin <= 3 && (d->cout % 128 == 0 || (d->cin == 3 && d->cout % 32 == 0)) &&
              vec_nhwc(y, d->ys, d->cout) &&
              (d->wout == 16 || d->wout % 32 == 0) && ((long long)d->batch * d->hout * d->wout / 32) < (1LL << 31) &&
@@ -3041,10 +3042,6 @@ static bool plan_narrow_in(Plan& p, const RganConv* d, const float* x, const flo
   a.bias = bias; a.wscale = wscale; a.act = act; a.alpha = alpha;
   a.x_bytes = (int)std::min(xext, (1LL << 31) - 1);
   a.y_bytes = (int)std::min(yext, (1LL << 31) - 1);
-  a.ks = d->kh;
-  a.w_sn = (long long)d->cin * d->kh * d->kw;  // torch Conv2d layout
-  a.w_sc = d->kh * d->kw;
-  a.w_flip = 0;
   p.pack = false;
   return true;
 }
@@ -3070,16 +3067,16 @@ static bool plan_narrow3_out(Plan& p, int batch, const float* x, const long long
   return true;
 }
 
-// weight gradient of a 3x3 stride-1 Conv2d with <= 4 channels on one side (wgrad3_narrow +
-// the WGRAD split reduce); the wide side NHWC with channels % 4 == 0
+// weight gradient of a 3x3 stride-1 pad-1 Conv2d with <= 4 output channels (wgrad3_narrow + the
+// WGRAD split reduce)
 static bool plan_wgrad3_narrow(Plan& p, const RganConv* d, const float* x, const float* dy, float* dw) {
-  if (!RGAN_NARROW3 || d->transposed || d->kh != 3 || d->kw != 3 || d->stride != 1) return false;
-  const bool wide_x = d->cout <= 4;
-  const int cw = wide_x ? d->cin : d->cout;
-  if (!wide_x && d->cin > 4) return false;
-  const long long* ws = wide_x ? d->xs : d->ys;
-  const float* wp = wide_x ? x : dy;
-  if (cw % 4 || 9 * (cw / 4) > 1024 || ws[1] != 1 || ws[0] % 4 || ws[2] % 4 || ws[3] % 4 || !aligned16(wp)) return false;
+  if (!RGAN_NARROW3 || d->transposed || d->kh != 3 || d->kw != 3 || d->stride != 1 || d->pad != 1 || d->cout > 4)
+    return false;
+  const int cw = d->cin;
+  if (cw % 4 || 9 * (cw / 4) > 1024) return false;
+  // R whole output rows per block, staged in LDS
+  const int R = std::max(1, std::min(d->hout, N3W_PIX / std::max(1, d->wout)));
+  if (wgrad3_lds_bytes(R, d->wout, cw, d->cout) > 64 * 1024) return false;
   p.mode = MODE_NARROW3W;
   NarrowArgs& a = p.na;
   a.x = x; a.xsb = d->xs[0]; a.xsc = d->xs[1]; a.xsh = d->xs[2]; a.xsw = d->xs[3];
@@ -3087,7 +3084,8 @@ static bool plan_wgrad3_narrow(Plan& p, const RganConv* d, const float* x, const
   a.B = d->batch; a.H = d->hin; a.W = d->win; a.C = d->cin;
   a.Ho = d->hout; a.Wo = d->wout; a.Cout = d->cout; a.stride = 1; a.pad = d->pad;
   const long long P = (long long)d->batch * d->hout * d->wout;
-  a.chunks = (int)ceil_div(P, (long long)N3W_CH);
+  a.rows = R;
+  a.chunks = d->batch * ceil_div(d->hout, R);
   p.slab_floats = (size_t)a.chunks * d->cout * 9 * d->cin;
   // the reduce: the WGRAD GEMM's [split][M = cout][N = (kh, kw, ci)] slab into torch layout
   GemmArgs& g = p.g;
@@ -3216,28 +3214,15 @@ static int plan_dgrad(const RganConv* d, const float* dy, const float* w, const 
     for (int i = 0; i < 4; ++i) { c.xs[i] = d->ys[i]; c.ys[i] = d->xs[i]; }
     if (plan_narrow_in(p, &c, dy, w, wscale, nullptr, dx, RGAN_ACT_NONE, 0.f)) return 0;
   }
-  // 3x3 stride-1 Conv2d: the data gradient is the conv of dy with the kernel transposed and
-  // flipped (pad 2 - p): <= 4 dy channels -> the narrow-in kernel, <= 4 dx channels -> the
-  // narrow-out one; W[co][ci][t] read as [out = ci][in = co][8 - t]
-  if (!d->transposed && d->kh == 3 && d->kw == 3 && d->stride == 1) {
-    if (d->cout <= 4) {
-      RganConv c = *d;
-      c.cin = d->cout; c.hin = d->hout; c.win = d->wout;
-      c.cout = d->cin; c.hout = d->hin; c.wout = d->win;
-      c.pad = 2 - d->pad;
-      for (int i = 0; i < 4; ++i) { c.xs[i] = d->ys[i]; c.ys[i] = d->xs[i]; }
-      if (plan_narrow_in(p, &c, dy, w, wscale, nullptr, dx, RGAN_ACT_NONE, 0.f)) {
-        p.na.w_sn = 9;
-        p.na.w_sc = (long long)d->cin * 9;
-        p.na.w_flip = 1;
-        return 0;
-      }
-    } else if (d->cin <= 4 &&
-               plan_narrow3_out(p, d->batch, dy, d->ys, d->hout, d->wout, d->cout, w, 9, (long long)d->cin * 9, 1,
-                                d->cin, dx, d->xs, d->hin, d->win, 2 - d->pad, wscale, nullptr, RGAN_ACT_NONE, 0.f)) {
-      return 0;
-    }
-  }
+  // 3x3 stride-1 Conv2d with <= 4 inputs (arch 1's input layer): its data gradient is the conv
+  // of dy with the kernel transposed and flipped (pad 2 - p), <= 4 outputs: the narrow-out
+  // kernel, W[co][ci][t] read as [out = ci][in = co][8 - t].  (The mirror case -- <= 4 dy
+  // channels into the narrow-in MFMA tile with a 3x3 kernel -- measured no faster than the
+  // generic GEMM at C4: 21 vs 19 us per call.)
+  if (!d->transposed && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->cin <= 4 &&
+      plan_narrow3_out(p, d->batch, dy, d->ys, d->hout, d->wout, d->cout, w, 9, (long long)d->cin * 9, 1, d->cin, dx,
+                       d->xs, d->hin, d->win, 2 - d->pad, wscale, nullptr, RGAN_ACT_NONE, 0.f))
+    return 0;
   g.a = make_img(dy, d->hout, d->wout, d->cout, d->ys);
   g.C = dx; g.bias = nullptr; g.act = RGAN_ACT_NONE; g.alpha = 0.f;
   g.out = make_out(d->hin, d->win, 1, d->xs[0], d->xs[2], d->xs[3], 1, 1, d->cin, 0, 0, d->xs[1]);
@@ -3469,7 +3454,7 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
     g_kernel_names[55] = "void rgan::gemm_post_bf16x6<0>(rgan::GemmArgs)";
     g_kernel_names[56] = "void rgan::gemm_post_bf16x6<1>(rgan::GemmArgs)";
     g_kernel_names[57] = "void rgan::conv3_narrow_out<NC>(rgan::NarrowArgs)";
-    g_kernel_names[58] = "void rgan::wgrad3_narrow<NC, WIDE_X>(rgan::NarrowArgs, int)";
+    g_kernel_names[58] = "void rgan::wgrad3_narrow<NC>(rgan::NarrowArgs, int, int)";
   }
   return id;
 }
@@ -3530,20 +3515,11 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
   } else {
     // persistent: two resident blocks per CU loop over the M tiles
     dim3 grid(std::min(ceil_div(a.B * a.Ho * a.Wo, 128), 512), ceil_div(a.Cout, 128));
-    if (a.ks == 3) {
-      switch (a.C) {
-        case 1: conv_narrow_in_mfma<1, 3><<<grid, 256, 0, s>>>(a); break;
-        case 2: conv_narrow_in_mfma<2, 3><<<grid, 256, 0, s>>>(a); break;
-        case 3: conv_narrow_in_mfma<3, 3><<<grid, 256, 0, s>>>(a); break;
-        default: conv_narrow_in_mfma<4, 3><<<grid, 256, 0, s>>>(a); break;
-      }
-    } else {
-      switch (a.C) {
-        case 1: conv_narrow_in_mfma<1><<<grid, 256, 0, s>>>(a); break;
-        case 2: conv_narrow_in_mfma<2><<<grid, 256, 0, s>>>(a); break;
-        case 3: conv_narrow_in_mfma<3><<<grid, 256, 0, s>>>(a); break;
-        default: conv_narrow_in_mfma<4><<<grid, 256, 0, s>>>(a); break;
-      }
+    switch (a.C) {
+      case 1: conv_narrow_in_mfma<1><<<grid, 256, 0, s>>>(a); break;
+      case 2: conv_narrow_in_mfma<2><<<grid, 256, 0, s>>>(a); break;
+      case 3: conv_narrow_in_mfma<3><<<grid, 256, 0, s>>>(a); break;
+      default: conv_narrow_in_mfma<4><<<grid, 256, 0, s>>>(a); break;
     }
   }
   return 0;
@@ -3561,19 +3537,14 @@ static int run_narrow3(Plan& p, hipStream_t s) {
     }
     return 0;
   }
-  const bool wide_x = a.Cout <= 4;
-  const int nc = wide_x ? a.Cout : a.C, cw = wide_x ? a.C : a.Cout;
-  const int threads = ceil_div(9 * (cw / 4), 64) * 64;
-#define RGAN_W3(NN)                                                                                 \
-  if (wide_x) wgrad3_narrow<NN, true><<<a.chunks, threads, 0, s>>>(a, cw);                         \
-  else wgrad3_narrow<NN, false><<<a.chunks, threads, 0, s>>>(a, cw);
-  switch (nc) {
-    case 1: RGAN_W3(1) break;
-    case 2: RGAN_W3(2) break;
-    case 3: RGAN_W3(3) break;
-    default: RGAN_W3(4) break;
+  const int threads = ceil_div(9 * (a.C / 4), 64) * 64, R = a.rows;
+  const size_t lds = wgrad3_lds_bytes(R, a.Wo, a.C, a.Cout);
+  switch (a.Cout) {
+    case 1: wgrad3_narrow<1><<<a.chunks, threads, lds, s>>>(a, a.C, R); break;
+    case 2: wgrad3_narrow<2><<<a.chunks, threads, lds, s>>>(a, a.C, R); break;
+    case 3: wgrad3_narrow<3><<<a.chunks, threads, lds, s>>>(a, a.C, R); break;
+    default: wgrad3_narrow<4><<<a.chunks, threads, lds, s>>>(a, a.C, R); break;
   }
-#undef RGAN_W3
   RGAN_CHECK_LAUNCH();
   GemmArgs g = p.g;
   g.slab = a.slab;

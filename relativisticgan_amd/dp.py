@@ -30,6 +30,7 @@ class _State:
     world = 1
     rank = 0
     sync_bn = False
+    on = False         # data-parallel machinery active: world > 1, or forced on one rank (setup)
     slots = {}         # id(parameter) -> (GradReducer, bucket, offset): gradient-bucket storage
     capture = None     # the PiecewiseGraph being captured (collectives become cut points)
 
@@ -37,24 +38,29 @@ class _State:
 _S = _State()
 
 
-def setup(group=None, sync_bn=False):
-    """Activate data-parallel mode for the current process (after init_process_group)."""
+def setup(group=None, sync_bn=False, force=False):
+    """Activate data-parallel mode for the current process (after init_process_group).
+    ``force``: run the data-parallel machinery (distributed heads, SyncBN exchanges, gradient
+    buckets on the second communicator) even with one rank -- a one-GPU rehearsal of the
+    collective code paths over RCCL (tests, ``bench.py --force-dp``); the results are the
+    single-process step's."""
     if not dist.is_available() or not dist.is_initialized():
-        _S.group, _S.grad_group, _S.world, _S.rank = None, None, 1, 0
+        _S.group, _S.grad_group, _S.world, _S.rank, _S.on = None, None, 1, 0, False
     else:
         _S.group = group
         _S.world = dist.get_world_size(group)
         _S.rank = dist.get_rank(group)
+        _S.on = _S.world > 1 or bool(force)
         # The overlapped gradient buckets get their own communicator (own RCCL stream):
         # on the shared one, every latency-critical SyncBN all-reduce of the remaining
         # backward would queue behind a 32 MB bucket in flight.
         ranks = dist.get_process_group_ranks(group) if group is not None else list(range(_S.world))
-        _S.grad_group = dist.new_group(ranks=ranks) if _S.world > 1 else group
+        _S.grad_group = dist.new_group(ranks=ranks) if _S.on else group
     _S.sync_bn = sync_bn
 
 
 def reset():
-    _S.group, _S.grad_group, _S.world, _S.rank, _S.sync_bn = None, None, 1, 0, False
+    _S.group, _S.grad_group, _S.world, _S.rank, _S.sync_bn, _S.on = None, None, 1, 0, False, False
 
 
 def world():
@@ -66,7 +72,7 @@ def rank():
 
 
 def active():
-    return _S.world > 1
+    return _S.on
 
 
 def group():
@@ -74,7 +80,7 @@ def group():
 
 
 def sync_bn():
-    return _S.world > 1 and _S.sync_bn
+    return _S.on and _S.sync_bn
 
 
 def grad_view(w):
@@ -82,7 +88,7 @@ def grad_view(w):
     gradient into when w has none yet this step (autograd then adopts the returned tensor
     as ``w.grad`` without copying: a fresh view has no other reference), or None (one
     process, w not bucketed, or a gradient already accumulating)."""
-    if _S.world == 1 or w.grad is not None:
+    if not _S.on or w.grad is not None:
         return None
     slot = _S.slots.get(id(w))
     if slot is None or slot[0].params_by_id.get(id(w)) is not w:
@@ -100,7 +106,7 @@ def all_reduce_sum(t):
     """In-place SUM over ranks (no-op for world 1).  While a PiecewiseGraph is being
     captured the collective becomes a cut point: the graph segment so far ends, and at every
     replay the all-reduce runs eagerly on ``t`` (a static address) before the next segment."""
-    if _S.world > 1:
+    if _S.on:
         if _S.capture is not None:
             grp = _S.group
             _S.capture.cut(lambda: dist.all_reduce(t, op=dist.ReduceOp.SUM, group=grp))
@@ -184,7 +190,7 @@ class PiecewiseGraph:
 
 def all_gather_cat(t):
     """[world * numel] concatenation of every rank's ``t`` in rank order."""
-    if _S.world == 1:
+    if not _S.on:
         return t
     flat = t.contiguous().view(-1)
     if dist.get_backend(_S.group) == "nccl":  # RCCL: one fused collective
@@ -276,7 +282,7 @@ class GradReducer:
     def arm(self):
         # under PiecewiseGraph capture the buckets are reduced at the cut finish() makes:
         # hooks firing inside the captured backward cannot launch collectives
-        if _S.world > 1 and _S.capture is None:
+        if _S.on and _S.capture is None:
             self._reset()
             self.armed = True
 

@@ -79,3 +79,20 @@ def test_bench_headline_two_rank_rehearsal():
     d = _line(r.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 64 and d["config"]["launch_mode"] == "eager"
     assert d["value"] > 0
+
+
+@pytest.mark.parametrize("workload,mode", [("C1", "piecewise"), ("C3", "eager")])
+def test_bench_forced_dp_over_rccl_one_rank(workload, mode):
+    """The driver's N > 1 command shape with ONE rank over RCCL and the data-parallel path
+    forced on (``--force-dp``): process group on nccl, distributed heads, gradient buckets on
+    the second communicator, piecewise graphs (C1) / eager overlapped buckets (C3) -- the
+    collectives the scaling runs use, on the real backend."""
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", "29652", "bench.py", "--gpus", "1",
+                        "--force-dp", "--workload", workload, "--extra=", "--steps", "2", "--warmup", "1",
+                        "--no-emu-extra", "--no-cpu-baseline", "--no-dp-path", "--no-host-draws", "--no-hbm"],
+                       cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 1 and d["config"]["forced_dp"] is True and d["config"]["launch_mode"] == mode
+    assert d["value"] > 0

@@ -355,3 +355,48 @@ def test_gradient_bucket_views_gloo_world2():
         pr.join(120)
     res = [q.get() for _ in range(world)]
     assert all(msg == "ok" for _, msg in res), res
+
+
+def _forced_worker(rank, world, port, q):
+    try:
+        dp = _init(rank, world, port)
+        assert not dp.active()  # one rank: plain single-process mode by default
+        dp.setup(force=True)
+        assert dp.active() and dp.world() == 1 and dp._S.grad_group is not None
+        t = torch.arange(6.0)
+        assert torch.equal(dp.all_reduce_sum(t.clone()), t)
+        assert torch.equal(dp.all_gather_cat(t), t)
+        params = _make_params()
+        red = dp.GradReducer(params, bucket_bytes=60)
+        ref = _make_params()
+        l1, l2 = _losses(ref, 0)
+        want = torch.autograd.grad(l1 + l2, ref)
+        l1, l2 = _losses(params, 0)
+        l1.backward()
+        red.arm()
+        l2.backward()
+        red.finish()
+        for prm, w_ in zip(params, want):
+            assert torch.allclose(prm.grad, w_, atol=1e-6)
+        q.put((rank, "ok"))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+    finally:
+        from relativisticgan_amd import dp as _dp
+        _dp.reset()
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_forced_dp_one_rank_gloo():
+    """dp.setup(force=True) with one rank (the one-GPU rehearsal of the RCCL path,
+    bench.py --force-dp): the machinery switches on -- second communicator, collectives,
+    bucketed reducer -- and every exchange is the identity."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    pr = ctx.Process(target=_forced_worker, args=(0, 1, _free_port(), q))
+    pr.start()
+    pr.join(120)
+    res = q.get()
+    assert res[1] == "ok", res

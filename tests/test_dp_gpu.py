@@ -73,14 +73,15 @@ def _run(name, world, rank, n_iter=None, device="cuda:0", batch_D=None, batch_G=
     return out
 
 
-def _worker(rank, world, port, name, path, sync_bn=True, n_iter=None, backend="gloo", batch_D=None, batch_G=None):
+def _worker(rank, world, port, name, path, sync_bn=True, n_iter=None, backend="gloo", batch_D=None, batch_G=None,
+            force=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dev = rank if backend == "nccl" else 0  # RCCL: one GPU per rank; gloo: both ranks on cuda:0
     torch.cuda.set_device(dev)
     dist.init_process_group(backend, rank=rank, world_size=world)
     from relativisticgan_amd import dp
-    dp.setup(sync_bn=sync_bn)
+    dp.setup(sync_bn=sync_bn, force=force)
     try:
         res = _run(name, world, rank, n_iter, device=f"cuda:{dev}", batch_D=batch_D, batch_G=batch_G)
         # gather the per-rank D outputs so rank 0 holds the global vectors
@@ -101,11 +102,12 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-def _spawn(name, sync_bn=True, n_iter=None, backend="gloo", batch_D=None, world=2, batch_G=None):
+def _spawn(name, sync_bn=True, n_iter=None, backend="gloo", batch_D=None, world=2, batch_G=None, force=False):
     path = os.path.join(tempfile.mkdtemp(), "dp.pt")
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, name, path, sync_bn, n_iter, backend, batch_D, batch_G))
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, name, path, sync_bn, n_iter, backend, batch_D, batch_G, force))
              for r in range(world)]
     for pr in procs:
         pr.start()
@@ -140,6 +142,19 @@ def test_dp2_rccl_matches_single_process(name):
     deferred G step overlapping the next D forward).  Skipped on a 1-GPU box."""
     single = _run(name, 1, 0)
     dpres = _spawn(name, backend="nccl")
+    _compare(name, dpres, single)
+
+
+@pytest.mark.parametrize("name,sync_bn", [("ralsgan", True), ("ralsgan", False), ("wgangp", True),
+                                          ("rahinge_spectral", False)])
+def test_dp1_rccl_forced_matches_single_process(name, sync_bn):
+    """One rank over RCCL with the data-parallel machinery forced on (dp.setup(force=True)):
+    the RCCL-only code paths -- all_gather_into_tensor of the SyncBN moments, the distributed
+    heads' all-reduces, the bucketed async all-reduce on the second communicator, the
+    deferred G step -- run on the real backend (a one-GPU box cannot hold two RCCL ranks) and
+    must reproduce the single-process step."""
+    single = _run(name, 1, 0)
+    dpres = _spawn(name, sync_bn=sync_bn, backend="nccl", world=1, force=True)
     _compare(name, dpres, single)
 
 

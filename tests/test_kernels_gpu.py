@@ -1135,10 +1135,11 @@ def test_wgrad_write_accumulate_into(K, B, cin, cout, H, tr):
     assert torch.equal(into, dw)
 
 
-# arch 1's 3x3 stride-1 image layers (GLI:202 / 222-223, 260 / 300-301): narrow-in MFMA tile
-# (conv_narrow_in_mfma<CI, 3>), narrow-out per-pixel kernel (conv3_narrow_out) and the narrow
-# weight gradient (wgrad3_narrow + the WGRAD split reduce).  (B, H): pixel counts below one
-# chunk, a few chunks (generic reduce) and the C4 shape (wide reduce).
+# arch 1's 3x3 stride-1 image layers (GLI:202 / 222-223, 260 / 300-301): the narrow-out
+# per-pixel kernel (conv3_narrow_out: the output layer's forward, the input layer's data
+# gradient), the narrow weight gradient (wgrad3_narrow + the WGRAD split reduce), and the
+# generic GEMM for the rest.  (B, H): pixel counts below one chunk, a few chunks (generic
+# reduce) and the C4 shape (wide reduce).
 @pytest.mark.parametrize("nc", [1, 3, 4])
 @pytest.mark.parametrize("B,H", [(2, 5), (3, 16), (32, 32)])
 def test_conv3x3_narrow_layers(K, nc, B, H):
