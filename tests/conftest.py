@@ -9,3 +9,39 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+# Heartbeat for long GPU tests: the full-size parity cases (the 256^2 shard's oracle replay and
+# float64 step on the host) run for minutes without a line of output under the default
+# capture, and a runner that watches for silence would take that for a hang.  While a
+# gpu-marked test runs, a daemon thread prints one line every HEARTBEAT_S seconds past the
+# capture (capsys.disabled()).
+import threading  # noqa: E402
+
+import pytest  # noqa: E402
+
+HEARTBEAT_S = 45
+
+
+@pytest.fixture(autouse=True)
+def _gpu_heartbeat(request):
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    capsys = request.getfixturevalue("capsys")
+    stop = threading.Event()
+
+    def beat():
+        n = 0
+        while not stop.wait(HEARTBEAT_S):
+            n += 1
+            with capsys.disabled():
+                print(f"\n[heartbeat] {request.node.nodeid} running {n * HEARTBEAT_S} s", flush=True)
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    try:
+        yield
+    finally:
+        stop.set()
+        th.join(5)
