@@ -2264,6 +2264,11 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
 #endif
 constexpr int NM_TR = 16, NM_TC = 32, NM_HR = NM_TR + 2, NM_HC = NM_TC + 2, NM_CH = 16, NM_LD = NM_CH + 4;
 constexpr int NM_XQ = NM_HR * NM_HC * (NM_CH / 4);  // float4 slots of one staged chunk
+// LDS row stride of the staged halo: a multiple of 64 dwords, so that the two image rows a
+// ds_read_b128 lane group spans (lanes 0-3 and 12-15 of one row, 20-27 of the next: the
+// MI355X_MICROARCH.md LDS table) land on disjoint banks -- at the packed 680-dword stride
+// (34 pixels x 20) they overlapped two ways (SQ_LDS_BANK_CONFLICT 11.9M cycles per C3 launch)
+constexpr int NM_RS = (NM_HC * NM_LD + 63) / 64 * 64;
 constexpr int NM_XPT = (NM_XQ + 255) / 256;         // ... per thread
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -2281,7 +2286,7 @@ __device__ __forceinline__ f32x4 mfma4_bcast(float a, float b, f32x4 c, int g) {
 
 template <int NC>
 __global__ __launch_bounds__(256, 2) void convt2_narrow_mfma(NarrowArgs a, int ntiles) {
-  __shared__ __attribute__((aligned(16))) float xs[NM_HR * NM_HC * NM_LD];
+  __shared__ __attribute__((aligned(16))) float xs[NM_HR * NM_RS];
   __shared__ __attribute__((aligned(16))) float wl[NM_CH * 256];  // [c][r][lane] (pack_narrow order)
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int tiles_c = (a.W + NM_TC - 1) / NM_TC, tiles_r = (a.H + NM_TR - 1) / NM_TR;
@@ -2294,15 +2299,34 @@ __global__ __launch_bounds__(256, 2) void convt2_narrow_mfma(NarrowArgs a, int n
   // blocks ran a 3-blocks-per-CU round plus a 1-block tail, every chunk's loads exposed).
   float4 stage[NM_XPT];
   float4 wv[4];
-  auto load_chunk = [&](const float* xb, int r0, int c0p, int ch0) {
+  // this thread's halo slots of the tile being prefetched: element offset of (pixel, channel
+  // quad tid % 4) within the image, or -1 outside it -- computed once per tile, so a chunk's
+  // prefetch is one add per load (the per-chunk index arithmetic was 1.6 VALU per MFMA, and
+  // fp32 MFMA and VALU share the issue port)
+  int xo[NM_XPT], sxo[NM_XPT];  // ... and its slots' LDS offsets (fixed per thread)
+  const int q4 = 4 * (tid & 3);
+#pragma unroll
+  for (int t = 0; t < NM_XPT; ++t) {
+    const int pix = (tid + 256 * t) >> 2, hr = pix / NM_HC;
+    sxo[t] = hr * NM_RS + (pix - hr * NM_HC) * NM_LD + q4;
+  }
+  auto set_tile = [&](int r0, int c0p) {
 #pragma unroll
     for (int t = 0; t < NM_XPT; ++t) {
-      const int e = tid + 256 * t, pix = e >> 2, q = e & 3;
+      const int e = tid + 256 * t, pix = e >> 2;
       const int hr = pix / NM_HC, hc = pix - hr * NM_HC;
-      const int ih = r0 - 1 + hr, iw = c0p - 1 + hc, c = ch0 + 4 * q;
+      const int ih = r0 - 1 + hr, iw = c0p - 1 + hc;
+      xo[t] = (e < NM_XQ && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                  ? ih * (int)a.xsh + iw * (int)a.xsw + q4
+                  : -1;
+    }
+  };
+  auto load_chunk = [&](const float* xb, int ch0) {
+    const bool cok = ch0 + q4 < a.C;
+#pragma unroll
+    for (int t = 0; t < NM_XPT; ++t) {
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e < NM_XQ && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W && c < a.C)
-        v = *reinterpret_cast<const float4*>(xb + (long long)ih * a.xsh + (long long)iw * a.xsw + c);
+      if (cok && xo[t] >= 0) v = *reinterpret_cast<const float4*>(xb + xo[t] + ch0);
       stage[t] = v;
     }
     // weights: this chunk's [c][r][lane] slice of the pack, contiguous (c >= C -> 0)
@@ -2330,11 +2354,14 @@ __global__ __launch_bounds__(256, 2) void convt2_narrow_mfma(NarrowArgs a, int n
   };
   int it = blockIdx.x;
   if (it >= items) return;
+  const float* xb_next;
   {
     int t, cb, ce, b, r0, c0p;
     item_of(it, t, cb, ce);
     tile_of(t, b, r0, c0p);
-    load_chunk(a.x + (long long)b * a.xsb, r0, c0p, cb);
+    set_tile(r0, c0p);
+    xb_next = a.x + (long long)b * a.xsb;
+    load_chunk(xb_next, cb);
   }
   for (; it < items; it += gridDim.x) {
     int t, cb, ce, b, r0, c0p;
@@ -2351,19 +2378,21 @@ __global__ __launch_bounds__(256, 2) void convt2_narrow_mfma(NarrowArgs a, int n
 #pragma unroll
       for (int q = 0; q < NM_XPT; ++q) {
         const int e = tid + 256 * q;
-        if (e < NM_XQ) *reinterpret_cast<float4*>(xs + (e >> 2) * NM_LD + 4 * (e & 3)) = stage[q];
+        if (e < NM_XQ) *reinterpret_cast<float4*>(xs + sxo[q]) = stage[q];
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) *reinterpret_cast<float4*>(wl + 4 * (tid + 256 * q)) = wv[q];
       __syncthreads();
       // the next chunk (or the next tile's first chunk) into registers during the MFMAs
       if (ch0 + NM_CH < ce) {
-        load_chunk(a.x + (long long)b * a.xsb, r0, c0p, ch0 + NM_CH);
+        load_chunk(xb_next, ch0 + NM_CH);
       } else if (it + (int)gridDim.x < items) {
         int t2, cb2, ce2, b2, r2, c2;
         item_of(it + (int)gridDim.x, t2, cb2, ce2);
         tile_of(t2, b2, r2, c2);
-        load_chunk(a.x + (long long)b2 * a.xsb, r2, c2, cb2);
+        set_tile(r2, c2);
+        xb_next = a.x + (long long)b2 * a.xsb;
+        load_chunk(xb_next, cb2);
       }
       for (int c4 = 0; c4 < nch / 4; ++c4) {
         float4 xv[2][3][3];
@@ -2373,7 +2402,7 @@ __global__ __launch_bounds__(256, 2) void convt2_narrow_mfma(NarrowArgs a, int n
           for (int u = 0; u < 3; ++u)
 #pragma unroll
             for (int v = 0; v < 3; ++v)
-              xv[g][u][v] = *reinterpret_cast<const float4*>(xs + ((pr + u) * NM_HC + 16 * g + pc + v) * NM_LD + 4 * c4);
+              xv[g][u][v] = *reinterpret_cast<const float4*>(xs + (pr + u) * NM_RS + (16 * g + pc + v) * NM_LD + 4 * c4);
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc) {
           // B operands: 4 registers of 4 taps each (one ds_read_b32 apiece: 64 distinct

@@ -1,6 +1,6 @@
 """Narrow ConvTranspose2d micro-benchmark (diagnostic; GPU): G's image layer (128 -> 3,
 32x32 -> 64x64, tanh) and D's image-layer data gradient (the same ConvT shape, no act) at
-C1 / C2 batch sizes, each launch sequence (narrow kernel + split reduce) timed alone with
+C1 / C2 batch sizes (NARROW_SHAPE=C3: the 256^2 shard's), each launch sequence (narrow kernel + split reduce) timed alone with
 HIP events.  Run against variant builds (RGAN_LIB=..., RGAN_NARROW_MAX_SPLITS=...).
 
 usage: python tools/narrow_micro.py [reps]
@@ -15,6 +15,8 @@ sys.path.insert(0, ROOT)
 from relativisticgan_amd import kernels as K  # noqa: E402
 
 SHAPES = [(32, 128, 32, 32), (64, 128, 32, 32), (64, 128, 64, 64), (32, 64, 32, 32)]
+if os.environ.get("NARROW_SHAPE") == "C3":  # G's 256^2 image layer at the C3 shard (32 x 128 x 128^2)
+    SHAPES = [(32, 128, 128, 128)]
 
 
 def one(fn, reps):
