@@ -1364,10 +1364,54 @@ __global__ __launch_bounds__(1024) void chsum_merge(const double* __restrict__ p
   out[c] = accum ? out[c] + (float)t : (float)t;
 }
 
+// One-launch channel sum for few pixel rows (the bias gradients of arch 1's deep 8x8 / 4x4 layers
+// and their GP sweeps: P <= CS_MAX_ROWS): block = 16 channels (4 lanes x float4) x 64 row lanes,
+// each lane sums rows r, r + 64, ... in double (4 loads in flight), the 64 lanes are added by a
+// fixed LDS tree, and the result is written (or added) directly -- no partials, no merge launch.
+constexpr int CS_LANES = 64;
+constexpr long long CS_MAX_ROWS = 2048;
+__global__ __launch_bounds__(256) void chsum_small(const float* __restrict__ t, long long P, int C,
+                                                   float* __restrict__ out, int accum) {
+  __shared__ double sh[CS_LANES][16];
+  const int q = threadIdx.x & 3, r = threadIdx.x >> 2, c0 = blockIdx.x * 16 + 4 * q;
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  long long p = r;
+  for (; p + 3 * CS_LANES < P; p += 4 * CS_LANES) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(t + (p + u * CS_LANES) * C + c0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s[0] += (double)v[u].x; s[1] += (double)v[u].y; s[2] += (double)v[u].z; s[3] += (double)v[u].w;
+    }
+  }
+  for (; p < P; p += CS_LANES) {
+    const float4 v = *reinterpret_cast<const float4*>(t + p * C + c0);
+    s[0] += (double)v.x; s[1] += (double)v.y; s[2] += (double)v.z; s[3] += (double)v.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) sh[r][4 * q + i] = s[i];
+  __syncthreads();
+  for (int h = CS_LANES / 2; h > 0; h >>= 1) {
+    if (r < h)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sh[r][4 * q + i] += sh[r + h][4 * q + i];
+    __syncthreads();
+  }
+  if (r == 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[c0 + i] = accum ? out[c0 + i] + (float)sh[0][4 * q + i] : (float)sh[0][4 * q + i];
+}
+
 extern "C" int rgan_channel_sum(const float* t, long long P, int C, long long sp, long long sc, float* out,
                                 int accumulate, void* partial, void* stream) {
   RGAN_REQUIRE(t && out && partial && P > 0 && C > 0);
   hipStream_t s = (hipStream_t)stream;
+  if (P <= CS_MAX_ROWS && C % 16 == 0 && sc == 1 && sp == C && ((uintptr_t)t & 15) == 0) {
+    chsum_small<<<C / 16, 256, 0, s>>>(t, P, C, out, accumulate);
+    RGAN_CHECK_LAUNCH();
+    return 0;
+  }
   BnGeo g = bn_geo(P, C, sp, sc);
   if (g.vec && ((uintptr_t)t & 15)) g = bn_geo(P, C, 1, 2);
   double* part = (double*)partial;

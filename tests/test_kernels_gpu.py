@@ -1179,3 +1179,20 @@ def test_conv3x3_narrow_layers(K, nc, B, H):
     assert _rel(dx, x64.grad) < 3e-6
     dw, _ = K.conv_wgrad(x, gy, g, w_out.shape)
     assert _rel(dw, w64.grad) < 3e-6
+
+
+@pytest.mark.parametrize("B,C,H", [(1, 16, 1), (3, 64, 5), (64, 512, 4), (32, 256, 8), (2, 64, 33), (64, 64, 8),
+                                   (8, 20, 4), (64, 128, 16)])
+def test_channel_sum(K, B, C, H):
+    """Bias-gradient channel sums: the one-launch kernel (<= 2048 rows, C % 16 == 0) and the
+    two-level one (more rows / other C), written and accumulated, vs torch fp64."""
+    torch.manual_seed(B * C + H)
+    t = _nhwc(torch.randn(B, C, H, H, device=DEV))
+    ref = t.double().cpu().sum((0, 2, 3))
+    out = torch.full((C,), float("nan"), device=DEV)
+    K.channel_sum(t, out)
+    assert _rel(out, ref) < 1e-6
+    base = torch.randn(C, device=DEV)
+    acc = base.clone()
+    K.channel_sum(t, acc, accumulate=True)
+    assert _rel(acc.double().cpu() - base.double().cpu(), ref) < 1e-5
