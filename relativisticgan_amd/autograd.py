@@ -37,12 +37,33 @@ class owning_grads:
     ``torch.autograd.grad`` call, which must not touch ``.grad`` -- autograd's own
     accumulation is used."""
     active = False
+    # Weight gradients written into .grad (the _own_grad path) may run on a second stream,
+    # overlapping the data-gradient chain below them; the context's exit joins it back, so
+    # .grad is complete for whatever follows the backward (Adam, a test reading it).
+    side_stream = False
+    _streams = {}
 
     def __enter__(self):
         self.prev, owning_grads.active = owning_grads.active, True
 
     def __exit__(self, *exc):
         owning_grads.active = self.prev
+        s = owning_grads._used
+        if s is not None:
+            owning_grads._used = None
+            torch.cuda.current_stream(s.device).wait_stream(s)
+
+    _used = None
+
+    @staticmethod
+    def wgrad_stream(device):
+        """The weight-gradient stream for ``device``, forked from the current stream."""
+        s = owning_grads._streams.get(device)
+        if s is None:
+            s = owning_grads._streams[device] = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        owning_grads._used = s
+        return s
 
 ACT_TRACE = None
 ACT_TAGS = []      # per ACT_TRACE entry: the net that produced it ("G" / "D", set by nets._Net)
@@ -422,6 +443,22 @@ class ConvLayerFn(torch.autograd.Function):
                     u, v, inv_sigma = sn
                     dwe, _ = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape))
                     g = K.spectral_backward(w, dwe, u, v, inv_sigma, spec.geom.transposed, out=acc)
+                elif owning_grads.side_stream:
+                    # on the weight-gradient stream: x, dy and .grad stay allocated until it
+                    # has read / written them (record_stream); the context's exit joins it
+                    main = torch.cuda.current_stream(w.device)
+                    ws = owning_grads.wgrad_stream(w.device)
+                    with torch.cuda.stream(ws):
+                        x.record_stream(ws)
+                        dy.record_stream(ws)
+                        if acc is not None:
+                            acc.record_stream(ws)
+                        if ctx.g1:
+                            g = K.g1_wgrad(x, dy, tuple(w.shape), out=acc)
+                        else:
+                            g, _ = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), out=acc)
+                    if acc is None:
+                        g.record_stream(main)
                 elif ctx.g1:
                     g = K.g1_wgrad(x, dy, tuple(w.shape), out=acc)
                 else:
