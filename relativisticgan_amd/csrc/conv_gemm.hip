@@ -2855,6 +2855,10 @@ static void tile_dims(int cfg, int& bm, int& bn) {
   bn = cfg == CFG_L ? 128 : (cfg == CFG_M ? 64 : 32);
 }
 
+#ifndef RGAN_SPLIT_MINK  // fewest k steps (of BK) per split
+#define RGAN_SPLIT_MINK 4
+#endif
+
 #ifndef RGAN_SPLIT_CFGM  // experiment: 128 x 64 tiles when 128 x 128 ones would split K this many ways
 #define RGAN_SPLIT_CFGM 0
 #endif
@@ -2880,7 +2884,7 @@ static void choose_tiling(Plan& p) {
   constexpr long long target = RGAN_SPLIT_TARGET;
   if (tiles < target) {
     splits = (int)((target + tiles - 1) / tiles);
-    splits = std::min(splits, std::max(1, nk / 4));
+    splits = std::min(splits, std::max(1, nk / RGAN_SPLIT_MINK));
     splits = std::min(splits, 256);
     // bound the slab to 256 MiB
     while (splits > 1 && (size_t)splits * g.M * g.N * p.phases > (size_t)64 << 20) --splits;
