@@ -1421,7 +1421,21 @@ __global__ __launch_bounds__(256) void splitk_reduce_bn(GemmArgs g, int mode_t2,
       const float* p0 = base + (size_t)m0 * g.N + n;
       const float* p1 = base + (size_t)m1 * g.N + n;
       float4 v0 = *reinterpret_cast<const float4*>(p0), v1 = *reinterpret_cast<const float4*>(p1);
-      for (int sp = 1; sp < g.splits; ++sp) {  // split order, as red_sum
+      int sp = 1;
+      for (; sp + 4 <= g.splits; sp += 4) {  // split order, as red_sum: 8 loads in flight, then the adds
+        float4 a0[4], a1[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          a0[u] = *reinterpret_cast<const float4*>(p0 + (size_t)(sp + u) * MN);
+          a1[u] = *reinterpret_cast<const float4*>(p1 + (size_t)(sp + u) * MN);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v0.x += a0[u].x; v0.y += a0[u].y; v0.z += a0[u].z; v0.w += a0[u].w;
+          v1.x += a1[u].x; v1.y += a1[u].y; v1.z += a1[u].z; v1.w += a1[u].w;
+        }
+      }
+      for (; sp < g.splits; ++sp) {
         const float4 a0 = *reinterpret_cast<const float4*>(p0 + (size_t)sp * MN);
         const float4 a1 = *reinterpret_cast<const float4*>(p1 + (size_t)sp * MN);
         v0.x += a0.x; v0.y += a0.y; v0.z += a0.z; v0.w += a0.w;
