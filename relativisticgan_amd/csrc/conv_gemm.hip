@@ -2877,15 +2877,30 @@ static void tile_dims(int cfg, int& bm, int& bn) {
 #define RGAN_SPLIT_CFGM 0
 #endif
 
+// opt-in fp32-on-bf16x6 GEMMs (rgan_set_gemm_emulation)
+static std::atomic<int> g_emu{0};
+static bool emu_bf16x6() { return g_emu.load(std::memory_order_relaxed) == 1; }
+
+#ifndef RGAN_SMALL_GEMM_FLOPS  // below this, 128 x 64 tiles instead of a >= 4-way split of 128 x 128 ones
+#define RGAN_SMALL_GEMM_FLOPS 4e9
+#endif
+
 static void choose_tiling(Plan& p) {
   GemmArgs& g = p.g;
   p.cfg = g.N <= 32 ? CFG_N : (g.N <= 64 ? CFG_M : CFG_L);
-#if RGAN_SPLIT_CFGM
   if (p.cfg == CFG_L && p.mode != MODE_WGRAD) {
     const long long t = (long long)ceil_div(g.M, 128) * ceil_div(g.N, 128) * p.phases;
-    if (t * RGAN_SPLIT_CFGM <= RGAN_SPLIT_TARGET && ceil_div(g.K, BK) >= 4 * RGAN_SPLIT_CFGM) p.cfg = CFG_M;
-  }
+    const int nk = ceil_div(g.K, BK);
+    // small GEMMs (arch 1 at 32x32: 0.1-1.5 GFLOP) that would split K 4+ ways: twice the
+    // tiles, a quarter of the splits and their reduce (C4 4.03 -> 3.92 ms/step, run r4t);
+    // at C1's 8.6-GFLOP GEMMs the same swap loses (round-4 run r4c)
+    const double flops = 2.0 * g.M * g.N * g.K * p.phases;
+    // (not under the bf16x6 emulation, whose kernels are 128 x 128)
+    if (flops < RGAN_SMALL_GEMM_FLOPS && t * 4 <= RGAN_SPLIT_TARGET && nk >= 16 && !emu_bf16x6()) p.cfg = CFG_M;
+#if RGAN_SPLIT_CFGM
+    if (t * RGAN_SPLIT_CFGM <= RGAN_SPLIT_TARGET && nk >= 4 * RGAN_SPLIT_CFGM) p.cfg = CFG_M;
 #endif
+  }
   int bm, bn;
   tile_dims(p.cfg, bm, bn);
   const int tiles_m = ceil_div(g.M, bm), tiles_n = ceil_div(g.N, bn);
@@ -3416,8 +3431,6 @@ static void launch_cfg(const Plan& p, dim3 grid, hipStream_t s) {
 
 // FAST 128x128 CONV / CONVT2 GEMMs (fwd + dgrad of Conv and ConvT) on the bf16x6 emulation: opt-in
 // by rgan_set_gemm_emulation (read at every launch: a captured graph keeps its kernels)
-static std::atomic<int> g_emu{0};
-static bool emu_bf16x6() { return g_emu.load(std::memory_order_relaxed) == 1; }
 static bool plan_emu(const Plan& p) {
   return p.fast && p.cfg == CFG_L && (p.mode == MODE_CONV || p.mode == MODE_CONVT2) && emu_bf16x6();
 }
