@@ -2884,11 +2884,17 @@ static bool emu_bf16x6() { return g_emu.load(std::memory_order_relaxed) == 1; }
 #ifndef RGAN_SMALL_GEMM_FLOPS  // below this, 128 x 64 tiles instead of a >= 4-way split of 128 x 128 ones
 #define RGAN_SMALL_GEMM_FLOPS 4e9
 #endif
+#ifndef RGAN_SMALL_SPLITS  // ... when 128 x 128 tiles would split K at least this many ways
+#define RGAN_SMALL_SPLITS 4
+#endif
+#ifndef RGAN_SMALL_WGRAD  // ... weight gradients too (C4 3.93 -> 3.85 ms/step, run r4v)
+#define RGAN_SMALL_WGRAD 1
+#endif
 
 static void choose_tiling(Plan& p) {
   GemmArgs& g = p.g;
   p.cfg = g.N <= 32 ? CFG_N : (g.N <= 64 ? CFG_M : CFG_L);
-  if (p.cfg == CFG_L && p.mode != MODE_WGRAD) {
+  if (p.cfg == CFG_L && (p.mode != MODE_WGRAD || RGAN_SMALL_WGRAD)) {
     const long long t = (long long)ceil_div(g.M, 128) * ceil_div(g.N, 128) * p.phases;
     const int nk = ceil_div(g.K, BK);
     // small GEMMs (arch 1 at 32x32: 0.1-1.5 GFLOP) that would split K 4+ ways: twice the
@@ -2896,7 +2902,9 @@ static void choose_tiling(Plan& p) {
     // at C1's 8.6-GFLOP GEMMs the same swap loses (round-4 run r4c)
     const double flops = 2.0 * g.M * g.N * g.K * p.phases;
     // (not under the bf16x6 emulation, whose kernels are 128 x 128)
-    if (flops < RGAN_SMALL_GEMM_FLOPS && t * 4 <= RGAN_SPLIT_TARGET && nk >= 16 && !emu_bf16x6()) p.cfg = CFG_M;
+    if (flops < RGAN_SMALL_GEMM_FLOPS && t * RGAN_SMALL_SPLITS <= RGAN_SPLIT_TARGET && nk >= 4 * RGAN_SMALL_SPLITS &&
+        !emu_bf16x6())
+      p.cfg = CFG_M;
 #if RGAN_SPLIT_CFGM
     if (t * RGAN_SPLIT_CFGM <= RGAN_SPLIT_TARGET && nk >= 4 * RGAN_SPLIT_CFGM) p.cfg = CFG_M;
 #endif
