@@ -85,6 +85,38 @@ def test_conv_fwd_dgrad_wgrad_small(K, case, layout):
     assert _rel(dw, w64.grad) < 2e-6
 
 
+@pytest.mark.parametrize("case", [(32, 128, 128, 16, 4, 2, 1, False), (32, 256, 128, 8, 4, 2, 1, True),
+                                  (32, 128, 256, 8, 3, 1, 1, False)])
+def test_small_gemm_tiles(K, case):
+    """Arch 1's small GEMMs (< 4 GFLOP that would split K 4+ ways on 128x128 tiles) run on
+    128x64 tiles with fewer splits (conv_gemm.hip choose_tiling): forward, data and weight
+    gradients vs torch fp64, and the 128x64 kernels are the ones that ran."""
+    B, cin, cout, H, k, s, p, tr = case
+    g = K.ConvGeom(k, s, p, tr)
+    torch.manual_seed(3)
+    x = _nhwc(torch.randn(B, cin, H, H, device=DEV))
+    w = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k), device=DEV) * 0.05
+    x64 = x.double().cpu().requires_grad_(True)
+    w64 = w.double().cpu().requires_grad_(True)
+    out64 = (F.conv_transpose2d if tr else F.conv2d)(x64, w64, stride=s, padding=p)
+    dy = _nhwc(torch.randn(out64.shape, device=DEV))
+    out64.backward(dy.double().cpu())
+
+    def gemm_names(fn):
+        K.profile_begin(64)
+        out = fn()
+        return out, [kk["name"] for kk in K.profile_end()["kernels"] if "gemm_kernel" in kk["name"]]
+
+    y, fwd = gemm_names(lambda: K.conv_fwd(x, w, g))
+    dx = K.conv_dgrad(dy, w, g, x.shape, like=x)  # tiling depends on its own K (not asserted)
+    (dw, _), wgr = gemm_names(lambda: K.conv_wgrad(x, dy, g, tuple(w.shape)))
+    for names in (fwd, wgr):
+        assert len(names) == 1 and "128, 64, 2, 2" in names[0], names
+    assert _rel(y, out64.detach()) < 2e-6
+    assert _rel(dx, x64.grad) < 2e-6
+    assert _rel(dw, w64.grad) < 2e-6
+
+
 @pytest.mark.parametrize("case", [(2, 16, 8, 4), (3, 8, 3, 8), (2, 32, 64, 8), (2, 5, 7, 6), (2, 64, 32, 16)])
 @pytest.mark.parametrize("cached", [False, True])
 def test_nn_conv_upsample_fold(K, case, cached):
