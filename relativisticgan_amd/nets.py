@@ -153,6 +153,9 @@ def weights_init(m):
 
 
 # ---------------------------------------------------------------- fused layer plan
+VIEW_OUT_CHANNELS_LAST = True  # C4 3.850 -> 3.800 ms/step (tools/ab_dense_cl.py, run r4ac)
+
+
 class _Layer:
     """One fused step: conv module (+ bn module) + activation."""
 
@@ -198,6 +201,10 @@ class _Layer:
                                 link_in, link_out)
         if self.out_view is not None:
             res = res.reshape(res.shape[0], *self.out_view)
+            if VIEW_OUT_CHANNELS_LAST and res.dim() == 4 and res.shape[2] * res.shape[3] > 1:
+                # arch 1's dense output viewed as G's NCHW 4x4 map: one channels-last copy so
+                # the next ConvT and its weight gradient read it with vector loads
+                res = res.contiguous(memory_format=torch.channels_last)
         return res
 
 
