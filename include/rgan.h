@@ -25,6 +25,10 @@ extern "C" {
 
 #define RGAN_EINVAL 1001
 
+/* ABI revision.  2: rgan_adam_packed takes step = device float[2] (step[1] is the
+ * call's uint32 arrival ticket, zero before the first call); revision 1 took float[1]. */
+#define RGAN_ABI_VERSION 2
+
 /* Activation codes fused into epilogues (GLI:345,370,388,417,437,450; SELU GLI:338). */
 enum {
   RGAN_ACT_NONE = 0, RGAN_ACT_RELU = 1, RGAN_ACT_LRELU = 2, RGAN_ACT_TANH = 3,
@@ -451,7 +455,9 @@ int rgan_profile_kernel(int idx, char* name, int name_len, double* ms, double* f
  * arithmetic option; the reference computes fp32 on the CPU). */
 int rgan_set_gemm_emulation(int on);
 
-/* Library self-description: number of exported compute entry points, version string. */
+/* Library self-description: number of exported compute entry points, version string
+ * (ends in "abi<RGAN_ABI_VERSION>"; rgan_abi_version() returns the number). */
+int rgan_abi_version(void);
 const char* rgan_version(void);
 
 /* Device sampling (--rgan_rng device; replaces the draws of GLI:176,608,630,648-649,674):

@@ -416,9 +416,12 @@ class Trainer:
     right after it, mirroring the golden capture points.
     """
 
-    def __init__(self, param, images, hooks=None, seed_all=True, dtype=torch.float32):
+    def __init__(self, param, images, hooks=None, seed_all=True, dtype=torch.float32, device=None):
         """``dtype`` != float32 (test envelope only): modules and buffers are cast after the
-        fp32 initialisation, so the same initial values are used at higher precision."""
+        fp32 initialisation, so the same initial values are used at higher precision.
+        ``device`` (test envelope only, with a ``feed``: the float64 judge steps of the GPU
+        parity tests) moves modules and buffers after that cast; the fp32 replay that is
+        pinned to the reference always stays on the CPU."""
         self.p = p = param
         self.hooks = hooks
         if seed_all:
@@ -449,6 +452,11 @@ class Trainer:
             self.D.to(dtype)
             for name in ("x", "x_fake", "y", "y2", "z", "u", "z_test", "grad_outputs"):
                 setattr(self, name, getattr(self, name).to(dtype))
+        if device is not None:
+            self.G.to(device)
+            self.D.to(device)
+            for name in ("x", "x_fake", "y", "y2", "z", "u", "z_test", "grad_outputs"):
+                setattr(self, name, getattr(self, name).to(device))
         self.optD = torch.optim.Adam(self.D.parameters(), lr=p.lr_D, betas=(p.beta1, p.beta2),
                                      weight_decay=p.weight_decay)
         self.optG = torch.optim.Adam(self.G.parameters(), lr=p.lr_G, betas=(p.beta1, p.beta2),

@@ -129,6 +129,7 @@ _SIGS = {
     "rgan_profile_end": (c_int, [c_vp, c_vp, c_vp]),
     "rgan_profile_kernel": (c_int, [c_int, ctypes.c_char_p, c_int, c_vp, c_vp, c_vp]),
     "rgan_version": (ctypes.c_char_p, []),
+    "rgan_abi_version": (c_int, []),
 }
 
 EXPORTED = tuple(_SIGS)

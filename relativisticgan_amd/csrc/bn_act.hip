@@ -65,11 +65,13 @@ static int max_chunks(long long P, int C) {
 }
 
 extern "C" size_t rgan_bn_dd_partial_bytes(long long P, int C) {
+  if (P <= 0 || C <= 0) return 0;  // no such layer
   return (size_t)max_chunks(P, C) * 3 * C * sizeof(double) + 256;
 }
 
 extern "C" size_t rgan_bn_partial_bytes(long long P, int C) {
   // [chunks][2][C] partial sums + [2][C] merged sums + [3][C] moments, doubles
+  if (P <= 0 || C <= 0) return 0;  // no such layer
   return ((size_t)max_chunks(P, C) * 2 + 5) * C * sizeof(double) + 256;
 }
 
@@ -440,14 +442,8 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
 
 // apply-pass grid: pixel blocks per channel group, each thread at least `min_iter` pixel
 // rows (round-1 sweep with tools/bn_micro.py: 4096 blocks, 4 rows)
-#ifndef RGAN_BN_APPLY_BLOCKS  // (variant builds sweep these: tools/build_variant.py)
-#define RGAN_BN_APPLY_BLOCKS 4096
-#endif
-#ifndef RGAN_BN_APPLY_MIN_ITER
-#define RGAN_BN_APPLY_MIN_ITER 4
-#endif
 static dim3 apply_grid(const BnGeo& g, long long P) {
-  constexpr long long blocks = RGAN_BN_APPLY_BLOCKS, min_iter = RGAN_BN_APPLY_MIN_ITER;
+  constexpr long long blocks = 4096, min_iter = 4;
   const long long rb = std::max<long long>(
       1, std::min<long long>((P + g.rp * min_iter - 1) / (g.rp * min_iter), std::max<long long>(1, blocks / g.cgroups)));
   return dim3(g.cgroups, (unsigned)rb);
@@ -456,6 +452,7 @@ static dim3 apply_grid(const BnGeo& g, long long P) {
 extern "C" int rgan_bn_apply_segments(const float* y, long long P, int C, int nseg, const float* stats,
                                       const float* gamma, const float* beta, int act, float act_alpha, float* a,
                                       void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   // dense NHWC y and a, P % nseg == 0; stats [nseg][2C]
   RGAN_REQUIRE(y && stats && a && P > 0 && C > 0 && (nseg == 1 || nseg == 2) && P % nseg == 0);
   hipStream_t s = (hipStream_t)stream;
@@ -474,6 +471,7 @@ extern "C" int rgan_bn_apply_segments(const float* y, long long P, int C, int ns
 extern "C" int rgan_bn_apply(const float* y, long long P, int C, long long sp, long long sc,
                              const float* stats, const float* gamma, const float* beta, int act,
                              float act_alpha, float* a, long long asp, long long asc, void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   RGAN_REQUIRE(y && stats && a && P > 0 && C > 0);
   hipStream_t s = (hipStream_t)stream;
   BnGeo g = bn_geo(P, C, sp, sc);
@@ -794,6 +792,7 @@ extern "C" int rgan_bn_backward_sums(const float* da, long long dsp, long long d
                                      int C, long long sp, long long sc, const float* stats, const float* gamma,
                                      const float* beta, int act, float act_alpha, double* sums, void* partial,
                                      void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   RGAN_REQUIRE(da && y && stats && sums && partial && P > 0 && C > 0);
   hipStream_t s = (hipStream_t)stream;
   BnGeo g = bn_geo(P, C, sp, sc);
@@ -820,6 +819,7 @@ extern "C" int rgan_bn_backward_apply_ex(const float* da, long long dsp, long lo
                                          const double* sums, long long P_global, const float* add, float* dy,
                                          long long ysp, long long ysc, float* dgamma, float* dbeta,
                                          int accumulate_affine, void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   RGAN_REQUIRE(da && y && stats && sums && dy && P > 0 && C > 0 && P_global >= P);
   hipStream_t s = (hipStream_t)stream;
   BnGeo g = bn_geo(P, C, sp, sc);
@@ -865,6 +865,7 @@ extern "C" int rgan_bn_backward_apply(const float* da, long long dsp, long long 
                                       const float* beta, int act, float act_alpha, const double* sums,
                                       long long P_global, float* dy, long long ysp, long long ysc, float* dgamma,
                                       float* dbeta, void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   return rgan_bn_backward_apply_ex(da, dsp, dsc, y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, sums,
                                    P_global, nullptr, dy, ysp, ysc, dgamma, dbeta, 0, stream);
 }
@@ -873,6 +874,7 @@ extern "C" int rgan_bn_backward_segments(const float* da, const float* y, long l
                                          const float* stats, const float* gamma, const float* beta, int act,
                                          float act_alpha, float* dy, float* dgamma, float* dbeta, void* partial,
                                          void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   // dense NHWC da, y, dy; P % nseg == 0; stats [nseg][2C]; partial: nseg * rgan_bn_partial_bytes(P / nseg, C)
   RGAN_REQUIRE(da && y && stats && dy && partial && P > 0 && C > 0 && (nseg == 1 || nseg == 2) && P % nseg == 0);
   hipStream_t s = (hipStream_t)stream;
@@ -980,6 +982,7 @@ extern "C" int rgan_bn_backward(const float* da, long long dsp, long long dsc, c
                                 int C, long long sp, long long sc, const float* stats, const float* gamma,
                                 const float* beta, int act, float act_alpha, float* dy, long long ysp,
                                 long long ysc, float* dgamma, float* dbeta, void* partial, void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   RGAN_REQUIRE(partial && P > 0 && C > 0);
   if (P <= BNS_MAX_ROWS && C % BNS_CH == 0 && dense_nhwc(sp, sc, C, y) && dense_nhwc(dsp, dsc, C, da) &&
       dense_nhwc(ysp, ysc, C, dy) && stats && dy) {  // small layers: one launch
@@ -1182,6 +1185,7 @@ extern "C" int rgan_bn_dd_sums(const float* a, const float* y, const float* dh, 
                                long long sc, const float* stats, const float* gamma, const float* beta, int act,
                                float act_alpha, int stage, const double* stage1, long long P_global, double* sums,
                                void* partial, void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   RGAN_REQUIRE(a && y && dh && stats && sums && partial && P > 0 && C > 0 && (stage == 1 || stage == 2));
   RGAN_REQUIRE(stage == 1 || (stage1 && P_global >= P));
   hipStream_t s = (hipStream_t)stream;
@@ -1215,6 +1219,7 @@ extern "C" int rgan_bn_dd_apply(const float* a, const float* y, const float* dh,
                                 const double* stage2, const double* stage1_local, const double* stage2_local,
                                 long long P_global, float* adj_dh, float* ydir, float* dgamma2, float* dbeta2,
                                 int accumulate_affine, void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   RGAN_REQUIRE(a && y && dh && stats && first_sums && stage1 && ydir && P > 0 && C > 0 && P_global >= P);
   RGAN_REQUIRE(!act_has_grad2(act) || stage2);
   hipStream_t s = (hipStream_t)stream;
@@ -1252,6 +1257,7 @@ __global__ void act_dd_kernel(const float* __restrict__ a, const float* __restri
 
 extern "C" int rgan_act_dd(const float* a, const float* act_out, const float* dh, long long n, int act,
                            float act_alpha, float* adj_dh, float* ydir, void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   RGAN_REQUIRE(a && act_out && n >= 0 && (adj_dh || ydir) && (!ydir || dh));
   if (n == 0) return 0;
   const int blocks = (int)std::max<long long>(1, std::min<long long>((n + 255) / 256, 8192));
@@ -1285,6 +1291,7 @@ __global__ void act_bwd_kernel(const float* __restrict__ da, const float* __rest
 
 extern "C" int rgan_act_backward(const float* da, const float* a, long long n, int act, float act_alpha,
                                  float* dx, void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   RGAN_REQUIRE(da && a && dx && n >= 0);
   if (n == 0) return 0;
   return rgan_act_backward_ex(da, a, nullptr, n, act, act_alpha, dx, stream);
@@ -1292,6 +1299,7 @@ extern "C" int rgan_act_backward(const float* da, const float* a, long long n, i
 
 extern "C" int rgan_act_backward_ex(const float* da, const float* a, const float* add, long long n, int act,
                                     float act_alpha, float* dx, void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   RGAN_REQUIRE(da && a && dx && n >= 0);
   if (n == 0) return 0;
   const int vec = ((((uintptr_t)da | (uintptr_t)a | (uintptr_t)dx | (uintptr_t)add) & 15) == 0) ? 1 : 0;

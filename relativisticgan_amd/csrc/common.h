@@ -10,6 +10,9 @@
     if (_e != hipSuccess) return (int)_e;           \
   } while (0)
 
+// host-side check of an RGAN_ACT_* code passed through the C-ABI
+static inline bool act_ok(int act) { return act >= RGAN_ACT_NONE && act <= RGAN_ACT_SELU; }
+
 #define RGAN_REQUIRE(cond)                          \
   do {                                              \
     if (!(cond)) return RGAN_EINVAL;                \

@@ -18,24 +18,13 @@
 // register-staged global loads (next tile's loads in flight while the current tile's
 // MFMAs run).  LDS images keep every MFMA operand read a conflict-free ds_read_b32:
 // m-major tiles use row stride BK+1, k-major tiles BM+4 / BN+4.  Split-K writes fp32
-// slabs reduced in fixed order (deterministic) by splitk_reduce (an in-launch combine by each
-// tile's last-arriving block, GemmArgs::fixup, is kept as a measured-slower experiment).
+// slabs reduced in fixed order (deterministic) by splitk_reduce.
 #include "common.h"
 
 #include <string>
 #include <type_traits>
 #include <atomic>
 #include <vector>
-
-#ifndef RGAN_GEMM_SB
-#define RGAN_GEMM_SB 0
-#endif
-#ifndef RGAN_SB_NARROW
-#define RGAN_SB_NARROW 1
-#endif
-#ifndef RGAN_SB_M  // single-buffered 128x64 tile (27.6 KB per block)
-#define RGAN_SB_M 1
-#endif
 
 namespace rgan {
 
@@ -50,39 +39,8 @@ constexpr long long FAST_MAX_BYTES = (1LL << 31) - (1LL << 24);
 enum { MODE_CONV = 0, MODE_CONVT2 = 1, MODE_WGRAD = 2, MODE_NARROW_T = 3, MODE_NARROW_IN = 4, MODE_DENSE1 = 5,
        MODE_NARROW3 = 6, MODE_NARROW3W = 7 };
 constexpr int BK = 32;
-#ifndef RGAN_XGROUP
-#define RGAN_XGROUP 1
-#endif
-#ifndef RGAN_NARROW3  // arch 1's 3x3 image layers on the narrow kernels (0: the generic GEMM, for A/B)
-#define RGAN_NARROW3 1
-#endif
-#ifndef RGAN_XGROUP_W  // weight-column XCD grouping for weight-heavy layers (xgroup 2)
-#define RGAN_XGROUP_W 1
-#endif
-#ifndef RGAN_SPLIT_TARGET  // split-K occupancy target (blocks); variant builds sweep it (tools/build_variant.py)
-#define RGAN_SPLIT_TARGET 512
-#endif
-// In-launch split-K combine (GemmArgs::fixup; experiment, off): FAST 128x128 CONV / CONVT2 tiles
-// split at most RGAN_FIXUP_MAX ways, the last arriver reads splits x 64 KB; RGAN_FIXUP_WGRAD
-// extends it to the weight gradients.  Measured against the separate reduce launches (same box,
-// profiles/round4_splitk_fixup_ab.txt): C1 3.86 -> 4.21 ms/step, C4 4.15 -> 4.53 (the dominant
-// GEMM 0.80 -> 0.70 of peak): every split block pays the drain + agent-scope release, and the
-// combine + epilogue of a tile runs on one block of its splits instead of the whole chip
-#ifndef RGAN_FIXUP
-#define RGAN_FIXUP 0
-#endif
-#ifndef RGAN_FIXUP_MAX
-#define RGAN_FIXUP_MAX 16
-#endif
-#ifndef RGAN_FIXUP_WGRAD
-#define RGAN_FIXUP_WGRAD 0
-#endif
-// arrival counters of the in-launch combine: FIX_REGIONS rotating regions of FIX_TILES tile
-// words (zero at load; each tile's last arriver puts its word back to 0), one region per
-// launch in turn, so GEMMs in flight together on different streams (fewer than FIX_REGIONS)
-// never share a word
-constexpr int FIX_TILES = 1024, FIX_REGIONS = 16;
-__device__ unsigned int g_split_tickets[FIX_REGIONS * FIX_TILES];
+// split-K occupancy target (blocks): two resident 256-thread blocks per CU on 256 CUs
+constexpr long long SPLIT_TARGET = 512;
 
 // n / d for 0 <= n < 2^31 via multiply-high (host-computed magic numbers)
 struct FastDiv {
@@ -137,10 +95,6 @@ struct GemmArgs {
   int xgroup, nph;        // XCD-grouped tile order (1: blocks sharing A rows on one XCD, 2: sharing weight columns); phases
   double* bnp;            // nullable: BatchNorm moments of every 64-row output segment (vector epilogue)
   int accum;              // WGRAD: add into C (gradient accumulation) instead of overwriting it
-  // splits > 1 with fixup: each block writes its partial tile to a tile-major slab
-  // ([phase][tile][split][fragment order]), and the tile's last-arriving block (ticket in
-  // g_split_tickets[fix_region]) sums the splits in split order and runs the unsplit epilogue
-  int fixup, fix_region;
   // Post-op for the layer that PRODUCED this GEMM's output operand (rgan_conv_post: a data
   // gradient, or G's image-layer gradient GEMM), applied where the value is final (unsplit
   // epilogue or split-K reduce); px has C's layout (host-checked):
@@ -222,13 +176,12 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   constexpr int B_LD = KROW ? KROW_LD : BN + 4;
   constexpr int B_SZ = KROW ? BN * KROW_LD : BK * B_LD;
   constexpr int STAGE = A_SZ + B_SZ;
-  // RGAN_GEMM_SB (experiment): single-buffered LDS stage (two barriers per k tile) and the
-  // vector epilogue in two 32-row passes -- ~37 KB per block, four resident blocks per CU
-  // The 256x32 narrow-N tile (CFG_N) is single-buffered by default: its two stages (83 KB)
-  // left one resident block per CU; one stage (41.5 KB) gives three.  The 128x64 tile
-  // (CFG_M) likewise (two -> five blocks; C3h32 -1.6 %, C1 / C4 unchanged)
-  constexpr bool GEMM_SB = !EMU && (RGAN_GEMM_SB || (RGAN_SB_NARROW && BM == 256 && BN == 32) ||
-                                    (RGAN_SB_M && BM == 128 && BN == 64));
+  // The 256x32 narrow-N tile (CFG_N) is single-buffered (two barriers per k tile): its two
+  // stages (83 KB) left one resident block per CU; one stage (41.5 KB) gives three.  The
+  // 128x64 tile (CFG_M) likewise (two -> five blocks; C3h32 -1.6 %, C1 / C4 unchanged).  The
+  // 128x128 tile keeps two stages (single-buffered it lost 9 %: its vector epilogue needs the
+  // LDS, and two blocks per CU already hide the one barrier)
+  constexpr bool GEMM_SB = !EMU && ((BM == 256 && BN == 32) || (BM == 128 && BN == 64));
   constexpr int EPI_SZ = KROW ? 4 * (GEMM_SB ? 32 : 64) * 72 : 0;  // vector epilogue staging (4 waves x rows x 72)
   // EMU: one (single-buffered) stage of six bf16 planes (A hi/mid/lo, B hi/mid/lo), rows of
   // 32 bf16 = 16 dwords at a 20-dword stride (16 lanes' ds_read_b128 on 16 distinct quads)
@@ -826,9 +779,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
         for (int t = 0; t < TM; ++t) a4[t] = *reinterpret_cast<const float4*>(Ar + 32 * t * KROW_LD + qo);
 #pragma unroll
         for (int t = 0; t < TN; ++t) b4[t] = *reinterpret_cast<const float4*>(Br + 32 * t * KROW_LD + qo);
-#if RGAN_EXP_SETPRIO
-        __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
         for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
@@ -836,56 +786,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
 #pragma unroll
             for (int j = 0; j < TN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[i][s4], b4[j][s4], acc[i][j], 0, 0, 0);
-#if RGAN_EXP_SETPRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
       }
     } else {
-#if RGAN_GEMM_FRAGALL
-    // all of the tile's MFMA operands to registers first: the LDS reads are in flight
-    // together and the MFMA chain waits on them progressively
-    float af[BK / 2][TM], bf[BK / 2][TN];
-#pragma unroll
-    for (int kk = 0; kk < BK / 2; ++kk) {
-      const int k = 2 * kk + lk;
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-        af[kk][t] = AK ? As[k * A_LD + wm + 32 * t + l32] : As[(wm + 32 * t + l32) * A_LD + k];
-#pragma unroll
-      for (int t = 0; t < TN; ++t) bf[kk][t] = Bs[k * B_LD + wn + 32 * t + l32];
-    }
-#pragma unroll
-    for (int kk = 0; kk < BK / 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[kk][i], bf[kk][j], acc[i][j], 0, 0, 0);
-#elif RGAN_GEMM_PREF
-    // operands of step kk+PREF are read while step kk's MFMAs run
-    constexpr int PF = RGAN_GEMM_PREF;
-    float af[PF + 1][TM], bf[PF + 1][TN];
-    auto rd = [&](int kk, int s) {
-      const int k = 2 * kk + lk;
-#pragma unroll
-      for (int t = 0; t < TM; ++t)
-        af[s][t] = AK ? As[k * A_LD + wm + 32 * t + l32] : As[(wm + 32 * t + l32) * A_LD + k];
-#pragma unroll
-      for (int t = 0; t < TN; ++t) bf[s][t] = Bs[k * B_LD + wn + 32 * t + l32];
-    };
-#pragma unroll
-    for (int kk = 0; kk < PF; ++kk) rd(kk, kk);
-#pragma unroll
-    for (int kk = 0; kk < BK / 2; ++kk) {
-      if (kk + PF < BK / 2) rd(kk + PF, (kk + PF) % (PF + 1));
-      const int s = kk % (PF + 1);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s][i], bf[s][j], acc[i][j], 0, 0, 0);
-    }
-#else
     // per-lane base pointers: every operand read below is base + compile-time offset,
     // which folds into the DS instruction's immediate (no per-read address VALU)
     const float* Al = AK ? As + lk * A_LD + wm + l32 : As + (wm + l32) * A_LD + lk;
@@ -903,7 +805,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bf[j], acc[i][j], 0, 0, 0);
     }
-#endif
     }
     if constexpr (GEMM_SB) {
       if (kt + 1 < nk) {
@@ -917,75 +818,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   }
   }  // EMU / fp32 main loop
 
-  // ---------------- in-launch split-K combine ----------------
-  // The release / acquire hand-off of cdna_hip_programming.md §5 (in-launch split-K
-  // reduction): every block stores its partial tile with plain 16-B stores in fragment order
-  // (each wave's float4 store = 64 lanes x 16 B contiguous), drains them, and after a block
-  // barrier one lane releases at agent scope and takes a ticket; the block that draws
-  // splits - 1 acquires, reads every split's partial tile in split order (the same fp32 sums
-  // splitk_reduce forms) into its accumulators and continues as an unsplit tile.
-  if (g.fixup) {
-    constexpr int TILE = BM * BN;
-    const int tiles_ph = ((g.M + BM - 1) / BM) * g.tiles_n;
-    const int tix = phase * tiles_ph + tm_i * g.tiles_n + tn_i;
-    float* tbase = g.slab + (size_t)tix * g.splits * TILE;
-    auto frag = [&](int i, int j, int r4) { return ((((wid * TM + i) * TN + j) * 4 + r4) * 64 + lane) * 4; };
-    {
-      float* mine = tbase + (size_t)split * TILE;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int r4 = 0; r4 < 4; ++r4)
-            *reinterpret_cast<float4*>(mine + frag(i, j, r4)) =
-                make_float4(acc[i][j][4 * r4], acc[i][j][4 * r4 + 1], acc[i][j][4 * r4 + 2], acc[i][j][4 * r4 + 3]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int* flag = reinterpret_cast<int*>(smem);  // the main loop's last barrier has passed
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      unsigned int* cnt = &g_split_tickets[g.fix_region * FIX_TILES + tix];
-      const unsigned int prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = prev == (unsigned int)(g.splits - 1);
-      if (last) {
-        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every split has arrived
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      flag[0] = last;
-    }
-    __syncthreads();
-    const int last = flag[0];
-    __syncthreads();  // every wave has read the flag before the epilogue reuses smem
-    if (!last) return;
-    for (int sp = 0; sp < g.splits; ++sp) {
-      const float* src = tbase + (size_t)sp * TILE;
-      float4 v[TM][TN][4];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int r4 = 0; r4 < 4; ++r4) v[i][j][r4] = *reinterpret_cast<const float4*>(src + frag(i, j, r4));
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int r4 = 0; r4 < 4; ++r4) {
-            const float4 q = v[i][j][r4];
-            if (sp == 0) {
-              acc[i][j][4 * r4] = q.x; acc[i][j][4 * r4 + 1] = q.y; acc[i][j][4 * r4 + 2] = q.z; acc[i][j][4 * r4 + 3] = q.w;
-            } else {
-              acc[i][j][4 * r4] += q.x; acc[i][j][4 * r4 + 1] += q.y; acc[i][j][4 * r4 + 2] += q.z; acc[i][j][4 * r4 + 3] += q.w;
-            }
-          }
-    }
-  }
-  const bool split_out = g.splits > 1 && !g.fixup;  // partial sums for a separate splitk_reduce
+  const bool split_out = g.splits > 1;  // partial sums for a separate splitk_reduce
 
   // ---------------- epilogue ----------------
   if constexpr (KROW && BM / WM == 64 && BN / WN == 64) {
@@ -995,12 +828,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
     // contiguous bytes per output row.  The scalar stores' bursts at the end of every tile
     // (all blocks finish together) held the MFMA pipes idle on short-K layers.
     const bool slab_out = split_out;
-#if RGAN_EXP_SCALAR_SLAB
-    if (!slab_out && g.vec_out) {
-#else
     if ((slab_out && g.N % 4 == 0) || (!slab_out && g.vec_out)) {
-#endif
-      // RGAN_GEMM_SB: the 64 rows in two passes of 32 (LDS for four resident blocks per CU)
       constexpr int EP_LD = 72, EPR = GEMM_SB ? 32 : 64, NP = 64 / EPR;
       __shared__ long long emoff[BM];
       float* T = smem + wid * (EPR * EP_LD);
@@ -1103,10 +931,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
             if (m < g.M) {
               const float4 v = *reinterpret_cast<const float4*>(T + rl * EP_LD + 4 * q);
               float* dst = slab_out ? slab + (size_t)m * g.N + n : g.C + emoff[wm + EPR * pp + rl] + noff;
-#if RGAN_EXP_NOSTORE
-              if (v.x == 1234.5f)
-#endif
-*reinterpret_cast<float4*>(dst) = v;
+              *reinterpret_cast<float4*>(dst) = v;
             }
           }
         }
@@ -1184,14 +1009,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
           const int rl = wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
           if (m0 + rl < g.M && col < g.N) {
             float v = acc[i][j][r] * wsc + bv;
-#if RGAN_EXP_NOSTORE  // timing-only experiment: drop the output stores
-            if (v == 1234.5f)
-#endif
-            {
-              float* dst = g.C + moff[rl] + noff[cl];
-              v = actf(v);
-              *dst = (MODE == MODE_WGRAD && g.accum) ? *dst + v : v;
-            }
+            float* dst = g.C + moff[rl] + noff[cl];
+            v = actf(v);
+            *dst = (MODE == MODE_WGRAD && g.accum) ? *dst + v : v;
           }
         }
       };
@@ -1205,7 +1025,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, bool AV, bool BV, bool FAST>
-__global__ __launch_bounds__(256, RGAN_GEMM_SB ? 4 : 2) void gemm_kernel(GemmArgs g) {
+__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs g) {
   gemm_body<MODE, BM, BN, WM, WN, AV, BV, FAST, false>(g);
 }
 
@@ -2054,13 +1874,10 @@ __device__ __forceinline__ void dma_lds16(int m0, int voff, i32x4 rsrc) {
 // two blocks per CU a v_mul writing the data's first VGPR right behind the store replaced the
 // first dword of lanes 12-15 of every 16 (C2 / C3 image layers: 0.1-1 % of D's first-layer
 // outputs wrong on every wave's second and later tiles; tools/img_in_check.py).
-#ifndef RGAN_STORE_NOPS
-#define RGAN_STORE_NOPS "4"
-#endif
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void store16_guarded(float4 f, int voff, i32x4 rsrc, int soff) {
   const f32x4v v = {f.x, f.y, f.z, f.w};
-  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop " RGAN_STORE_NOPS
+  asm volatile("buffer_store_dwordx4 %0, %1, %2, %3 offen\n\ts_nop 4"
                :
                : "v"(v), "v"(voff), "s"(rsrc), "s"(soff)
                : "memory");
@@ -2273,9 +2090,7 @@ __global__ __launch_bounds__(256, 2) void conv_img_in(NarrowArgs a, int tiles) {
 // staged through LDS 16 channels at a time (pixel stride 20 dwords: ds_read_b128 of 4
 // channels), weights [co][c][tap] staged beside it; per 4 channels a wave reads 18 + 16
 // ds_read_b128 and issues 128 MFMAs.
-#ifndef RGAN_NARROW_MAX_SPLITS
-#define RGAN_NARROW_MAX_SPLITS 8  // input-channel splits of convt2_narrow_mfma on small grids
-#endif
+constexpr int NARROW_MAX_SPLITS = 8;  // input-channel splits of convt2_narrow_mfma on small grids
 constexpr int NM_TR = 16, NM_TC = 32, NM_HR = NM_TR + 2, NM_HC = NM_TC + 2, NM_CH = 16, NM_LD = NM_CH + 4;
 constexpr int NM_XQ = NM_HR * NM_HC * (NM_CH / 4);  // float4 slots of one staged chunk
 // LDS row stride of the staged halo: a multiple of 64 dwords, so that the two image rows a
@@ -2869,32 +2684,22 @@ static void tile_dims(int cfg, int& bm, int& bn) {
   bn = cfg == CFG_L ? 128 : (cfg == CFG_M ? 64 : 32);
 }
 
-#ifndef RGAN_SPLIT_MINK  // fewest k steps (of BK) per split
-#define RGAN_SPLIT_MINK 4
-#endif
-
-#ifndef RGAN_SPLIT_CFGM  // experiment: 128 x 64 tiles when 128 x 128 ones would split K this many ways
-#define RGAN_SPLIT_CFGM 0
-#endif
+// fewest k steps (of BK) per split (round-4 A/B against 2 / 8 / 16: profiles/round4_split_planner_ab.txt)
+constexpr int SPLIT_MINK = 4;
 
 // opt-in fp32-on-bf16x6 GEMMs (rgan_set_gemm_emulation)
 static std::atomic<int> g_emu{0};
 static bool emu_bf16x6() { return g_emu.load(std::memory_order_relaxed) == 1; }
 
-#ifndef RGAN_SMALL_GEMM_FLOPS  // below this, 128 x 64 tiles instead of a >= 4-way split of 128 x 128 ones
-#define RGAN_SMALL_GEMM_FLOPS 4e9
-#endif
-#ifndef RGAN_SMALL_SPLITS  // ... when 128 x 128 tiles would split K at least this many ways
-#define RGAN_SMALL_SPLITS 4
-#endif
-#ifndef RGAN_SMALL_WGRAD  // ... weight gradients too (C4 3.93 -> 3.85 ms/step, run r4v)
-#define RGAN_SMALL_WGRAD 1
-#endif
+// below SMALL_GEMM_FLOPS, 128 x 64 tiles instead of a >= SMALL_SPLITS-way split of 128 x 128
+// ones, weight gradients included (C4 3.93 -> 3.85 ms/step, run r4v)
+constexpr double SMALL_GEMM_FLOPS = 4e9;
+constexpr int SMALL_SPLITS = 4;
 
 static void choose_tiling(Plan& p) {
   GemmArgs& g = p.g;
   p.cfg = g.N <= 32 ? CFG_N : (g.N <= 64 ? CFG_M : CFG_L);
-  if (p.cfg == CFG_L && (p.mode != MODE_WGRAD || RGAN_SMALL_WGRAD)) {
+  if (p.cfg == CFG_L) {
     const long long t = (long long)ceil_div(g.M, 128) * ceil_div(g.N, 128) * p.phases;
     const int nk = ceil_div(g.K, BK);
     // small GEMMs (arch 1 at 32x32: 0.1-1.5 GFLOP) that would split K 4+ ways: twice the
@@ -2902,12 +2707,8 @@ static void choose_tiling(Plan& p) {
     // at C1's 8.6-GFLOP GEMMs the same swap loses (round-4 run r4c)
     const double flops = 2.0 * g.M * g.N * g.K * p.phases;
     // (not under the bf16x6 emulation, whose kernels are 128 x 128)
-    if (flops < RGAN_SMALL_GEMM_FLOPS && t * RGAN_SMALL_SPLITS <= RGAN_SPLIT_TARGET && nk >= 4 * RGAN_SMALL_SPLITS &&
-        !emu_bf16x6())
+    if (flops < SMALL_GEMM_FLOPS && t * SMALL_SPLITS <= SPLIT_TARGET && nk >= 4 * SMALL_SPLITS && !emu_bf16x6())
       p.cfg = CFG_M;
-#if RGAN_SPLIT_CFGM
-    if (t * RGAN_SPLIT_CFGM <= RGAN_SPLIT_TARGET && nk >= 4 * RGAN_SPLIT_CFGM) p.cfg = CFG_M;
-#endif
   }
   int bm, bn;
   tile_dims(p.cfg, bm, bn);
@@ -2918,10 +2719,10 @@ static void choose_tiling(Plan& p) {
   int splits = 1;
   // two resident 256-thread blocks per CU on 256 CUs (round-1 sweep of this target: 256 / 384 / 768 /
   // 1024 all lost to 512, profiles/round1_splitk_target_sweep.txt)
-  constexpr long long target = RGAN_SPLIT_TARGET;
+  constexpr long long target = SPLIT_TARGET;
   if (tiles < target) {
     splits = (int)((target + tiles - 1) / tiles);
-    splits = std::min(splits, std::max(1, nk / RGAN_SPLIT_MINK));
+    splits = std::min(splits, std::max(1, nk / SPLIT_MINK));
     splits = std::min(splits, 256);
     // bound the slab to 256 MiB
     while (splits > 1 && (size_t)splits * g.M * g.N * p.phases > (size_t)64 << 20) --splits;
@@ -2930,21 +2731,9 @@ static void choose_tiling(Plan& p) {
   g.ksplit = per * BK;
   g.splits = ceil_div(g.K, g.ksplit);
   if (g.splits < 1) g.splits = 1;
-  // sized for either slab layout: [phase][split][M][N] (splitk_reduce) or the fixup's
-  // tile-major [phase][tile][split][bm * bn] (whole tiles, so at least as large)
+  // [phase][split][M][N] (splitk_reduce), sized in whole tiles
   p.slab_floats = g.splits > 1 ? (size_t)g.splits * tiles * bm * bn : 0;
 }
-
-// in-launch split-K combine (GemmArgs::fixup): FAST 128x128 tiles, few splits, tickets for
-// every tile of the launch
-static bool fixup_ok(const Plan& p) {
-  const GemmArgs& g = p.g;
-  if (!RGAN_FIXUP || g.splits <= 1 || g.splits > RGAN_FIXUP_MAX || !p.fast || p.cfg != CFG_L) return false;
-  if (p.mode == MODE_WGRAD && !RGAN_FIXUP_WGRAD) return false;
-  if (p.mode != MODE_CONV && p.mode != MODE_CONVT2 && p.mode != MODE_WGRAD) return false;
-  return (long long)ceil_div(g.M, 128) * g.tiles_n * p.phases <= FIX_TILES;
-}
-static unsigned g_fix_next = 0;
 
 static OutMap make_out(int gh, int gw, int step, long long sb, long long sh, long long sw, int nkh,
                        int nkw, int nc, long long th, long long tw, long long tc) {
@@ -3010,9 +2799,6 @@ static void set_fast(Plan& p, int batch) {
     g.im_bytes = (int)im_bytes;
   }
   p.fast = true;
-#if RGAN_EXP_NOLOAD  // timing-only experiment: zero-record descriptors drop every operand load
-  g.a_bytes = g.im_bytes = g.bw_bytes = 0;
-#endif
 }
 
 static void set_pack(Plan& p, const float* W, const float* scale, int K, int N, int pci, int pkw,
@@ -3032,19 +2818,41 @@ static void set_pack(Plan& p, const float* W, const float* scale, int K, int N, 
 static bool desc_ok(const RganConv* d) {
   if (!d) return false;
   if (d->batch <= 0 || d->cin <= 0 || d->cout <= 0 || d->kh <= 0 || d->kw <= 0 || d->stride <= 0 ||
-      d->pad < 0)
+      d->pad < 0 || d->hin <= 0 || d->win <= 0 || d->hout <= 0 || d->wout <= 0 ||
+      (d->transposed != 0 && d->transposed != 1))
     return false;
+  // sizes bounded before any arithmetic on them (every product below stays in 64 bits)
+  constexpr int DMAX = 1 << 24, KMAX = 256;
+  if (d->batch > DMAX || d->cin > DMAX || d->cout > DMAX || d->hin > DMAX || d->win > DMAX || d->hout > DMAX ||
+      d->wout > DMAX || d->kh > KMAX || d->kw > KMAX || d->stride > KMAX || d->pad > KMAX)
+    return false;
+  const long long hin = d->hin, win = d->win, kh = d->kh, kw = d->kw, st = d->stride, pad = d->pad;
   if (!d->transposed) {
-    if (d->hout != (d->hin + 2 * d->pad - d->kh) / d->stride + 1) return false;
-    if (d->wout != (d->win + 2 * d->pad - d->kw) / d->stride + 1) return false;
+    if (hin + 2 * pad < kh || win + 2 * pad < kw) return false;
+    if (d->hout != (hin + 2 * pad - kh) / st + 1) return false;
+    if (d->wout != (win + 2 * pad - kw) / st + 1) return false;
   } else {
-    if (d->hout != (d->hin - 1) * d->stride - 2 * d->pad + d->kh) return false;
-    if (d->wout != (d->win - 1) * d->stride - 2 * d->pad + d->kw) return false;
+    if (d->hout != (hin - 1) * st - 2 * pad + kh) return false;
+    if (d->wout != (win - 1) * st - 2 * pad + kw) return false;
   }
   // 32-bit index space for the GEMM dims
   if ((long long)d->batch * d->hout * d->wout >= (1LL << 31)) return false;
   if ((long long)d->batch * d->hin * d->win >= (1LL << 31)) return false;
-  return true;
+  // kernel / channel sizes whose products (K = taps x channels, N = taps x outputs of the 1x1
+  // expansion, packed-weight sizes) stay in int; non-negative strides whose extents stay far
+  // inside 64-bit offsets (the host-side fuzz of tests/test_host_asan.py)
+  const long long taps = kh * kw;
+  if (taps * d->cin >= (1LL << 31) || taps * d->cout >= (1LL << 31) || (long long)d->cin * d->cout * taps >= (1LL << 40))
+    return false;
+  constexpr long long SMAX = 1LL << 40;
+  double xext = 0.0, yext = 0.0;
+  const int xd[4] = {d->batch, d->cin, d->hin, d->win}, yd[4] = {d->batch, d->cout, d->hout, d->wout};
+  for (int i = 0; i < 4; ++i) {
+    if (d->xs[i] < 0 || d->xs[i] > SMAX || d->ys[i] < 0 || d->ys[i] > SMAX) return false;
+    xext += (double)(xd[i] - 1) * (double)d->xs[i];
+    yext += (double)(yd[i] - 1) * (double)d->ys[i];
+  }
+  return xext < (double)SMAX && yext < (double)SMAX;
 }
 
 static bool is_k4s2p1(const RganConv* d) {
@@ -3076,7 +2884,7 @@ static bool plan_narrow_t(Plan& p, int batch, const float* x, const long long* x
   const int chunks = ceil_div(C, NM_CH);
   int splits = 1;
   if (ntiles < 256)
-    splits = (int)std::min<long long>(std::min(chunks, RGAN_NARROW_MAX_SPLITS),
+    splits = (int)std::min<long long>(std::min(chunks, NARROW_MAX_SPLITS),
                                       ceil_div(512, (int)std::max<long long>(ntiles, 1)));
   a.cps = ceil_div(chunks, std::max(splits, 1)) * NM_CH;
   a.splits = ceil_div(C, a.cps);
@@ -3122,7 +2930,7 @@ static bool plan_narrow3_out(Plan& p, int batch, const float* x, const long long
                              const float* w, long long w_sn, long long w_sc, int flip, int nc, float* y,
                              const long long* ys, int Ho, int Wo, int pad, const float* wscale, const float* bias,
                              int act, float alpha) {
-  if (!RGAN_NARROW3 || nc > 4 || C % 16 != 0 || C > N3_MAXC || xs[1] != 1 || xs[0] % 4 || xs[2] % 4 || xs[3] % 4 || !aligned16(x))
+  if (nc > 4 || C % 16 != 0 || C > N3_MAXC || xs[1] != 1 || xs[0] % 4 || xs[2] % 4 || xs[3] % 4 || !aligned16(x))
     return false;
   if (Ho != H + 2 * pad - 2 || Wo != W + 2 * pad - 2) return false;
   p.mode = MODE_NARROW3;
@@ -3140,7 +2948,7 @@ static bool plan_narrow3_out(Plan& p, int batch, const float* x, const long long
 // weight gradient of a 3x3 stride-1 pad-1 Conv2d with <= 4 output channels (wgrad3_narrow + the
 // WGRAD split reduce)
 static bool plan_wgrad3_narrow(Plan& p, const RganConv* d, const float* x, const float* dy, float* dw) {
-  if (!RGAN_NARROW3 || d->transposed || d->kh != 3 || d->kw != 3 || d->stride != 1 || d->pad != 1 || d->cout > 4)
+  if (d->transposed || d->kh != 3 || d->kw != 3 || d->stride != 1 || d->pad != 1 || d->cout > 4)
     return false;
   const int cw = d->cin;
   if (cw % 4 || 9 * (cw / 4) > 1024) return false;
@@ -3446,7 +3254,7 @@ static bool plan_emu(const Plan& p) {
 template <int MODE>
 static void launch_mode(const Plan& p, dim3 grid, hipStream_t s) {
   if constexpr (MODE == MODE_CONV || MODE == MODE_CONVT2) {
-    if (p.g.pmode && (p.g.splits == 1 || p.g.fixup)) {  // post_ok: FAST 128x128 (the post-op in the epilogue)
+    if (p.g.pmode && p.g.splits == 1) {  // post_ok: FAST 128x128 (the post-op in the epilogue)
       if (plan_emu(p)) gemm_post_bf16x6<MODE><<<grid, 256, 0, s>>>(p.g);
       else gemm_post<MODE><<<grid, 256, 0, s>>>(p.g);
       return;
@@ -3652,7 +3460,7 @@ static void run_dense1(const Plan& p, const float* packed, hipStream_t s) {
 static bool bn_epilogue_ok(const Plan& p) {
   const GemmArgs& g = p.g;
   if (p.mode != MODE_CONV && p.mode != MODE_CONVT2) return false;
-  if (!p.fast || p.cfg != CFG_L || (g.splits != 1 && !g.fixup) || !g.vec_out || p.tap_stage) return false;
+  if (!p.fast || p.cfg != CFG_L || g.splits != 1 || !g.vec_out || p.tap_stage) return false;
   if (g.out.fnc.d != (uint32_t)g.N || g.M % 64 != 0 || p.bn_segs < 1) return false;
   if (p.bn_segs > 1 && (p.phases != 1 || g.M % p.bn_segs != 0 || (g.M / p.bn_segs) % 64 != 0)) return false;
   return true;
@@ -3671,7 +3479,7 @@ static bool red_vec_ok(const Plan& p, bool check_ptr) {
 static bool bn_reduce_ok(const Plan& p, bool check_ptr) {
   const GemmArgs& g = p.g;
   if (p.mode != MODE_CONV && p.mode != MODE_CONVT2) return false;
-  if (g.splits <= 1 || g.fixup || p.tap_stage || g.accum || !red_vec_ok(p, check_ptr) || g.N < 4 * REDBN_QB) return false;
+  if (g.splits <= 1 || p.tap_stage || g.accum || !red_vec_ok(p, check_ptr) || g.N < 4 * REDBN_QB) return false;
   if (g.out.fnc.d != (uint32_t)g.N || g.M % 64 != 0 || p.bn_segs < 1) return false;
   if (p.bn_segs > 1 && (p.phases != 1 || g.M % p.bn_segs != 0 || (g.M / p.bn_segs) % 64 != 0)) return false;
   return true;
@@ -3687,7 +3495,7 @@ static bool post_ok(const Plan& p, int mode, int nseg, bool check_ptr) {
   const GemmArgs& g = p.g;
   if (p.mode != MODE_CONV && p.mode != MODE_CONVT2) return false;
   if (p.tap_stage || g.accum || g.bias || g.act != RGAN_ACT_NONE) return false;
-  const bool whole = g.splits == 1 || g.fixup;  // the epilogue sees whole sums
+  const bool whole = g.splits == 1;  // the epilogue sees whole sums
   if (whole && !(p.fast && p.cfg == CFG_L && g.vec_out)) return false;  // gemm_post's epilogue
   if (mode == 1) return true;
   if (mode != 2 || nseg < 1 || g.out.fnc.d != (uint32_t)g.N || g.M % 64 != 0) return false;
@@ -3759,8 +3567,6 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     p.g.vec_out = p.mode != MODE_WGRAD && o.tc == 1 && o.fnc.d % 4 == 0 && p.g.N % 4 == 0 && al4(o.th) &&
                   al4(o.tw) && al4(o.sb) && al4(o.sh) && al4(o.sw) && aligned16(p.g.C);
   }
-  p.g.fixup = fixup_ok(p) ? 1 : 0;
-  p.g.fix_region = p.g.fixup ? (int)(g_fix_next++ % FIX_REGIONS) : 0;
   p.bn_fused = p.bn_part && (bn_epilogue_ok(p) || bn_reduce_ok(p, true));
   p.g.bnp = p.bn_fused ? p.bn_part : nullptr;
   p.post_fused = p.post && !p.bn_fused && post_ok(p, p.post->mode, p.post->nseg, true) &&
@@ -3776,14 +3582,14 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   tile_dims(p.cfg, bm, bn);
   const int tiles_m = ceil_div(p.g.M, bm);
   p.g.nph = p.phases;
-  p.g.xgroup = RGAN_XGROUP && p.fast && p.mode != MODE_WGRAD && tiles_m % 8 == 0 && p.g.tiles_n * p.phases > 1;
+  p.g.xgroup = p.fast && p.mode != MODE_WGRAD && tiles_m % 8 == 0 && p.g.tiles_n * p.phases > 1;
   // weight-column grouping where the weights dominate: under A-row grouping every XCD fetches
   // the whole weight (D's 2048 -> 4096 conv at C3: 4.36 GB of FETCH per launch for a 537 MB
   // weight; 1.01 GB grouped by weight columns).  Under weight-column grouping every XCD reads
   // the input through its im2col windows instead, which costs more than the input's bytes: at
   // a 2:1 weight / input ratio (D's 1024 -> 2048 conv) it fetched 2.02 GB against 1.33, hence
   // the factor 4 (run r4g)
-  if (RGAN_XGROUP_W && p.fast && p.mode != MODE_WGRAD && p.g.tiles_n % 8 == 0 &&
+  if (p.fast && p.mode != MODE_WGRAD && p.g.tiles_n % 8 == 0 &&
       (long long)p.g.bw_bytes * p.phases > 4LL * p.g.a_bytes && tiles_m * p.phases > 1)
     p.g.xgroup = 2;
   dim3 grid = p.g.xgroup ? dim3(tiles_m * p.g.tiles_n * p.phases, 1, p.g.splits)
@@ -3796,7 +3602,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     rec.flops = g_cur_flops;
     rec.kid = kernel_id(p.mode, p.cfg, p.av, p.bv, p.fast);
     if (plan_emu(p)) rec.kid = 51 + p.mode;
-    if (p.g.pmode && (p.g.splits == 1 || p.g.fixup)) rec.kid = (plan_emu(p) ? 55 : 53) + p.mode;
+    if (p.g.pmode && p.g.splits == 1) rec.kid = (plan_emu(p) ? 55 : 53) + p.mode;
     hipEventRecord(rec.a, s);
   }
   switch (p.mode) {
@@ -3815,7 +3621,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
     taps_transpose<<<dim3(ceil_div(cin, 64), p.g.M), 256, 0, s>>>(p.g.C, tap_dst, cin, tap_osb, p.g.accum);
     RGAN_CHECK_LAUNCH();
   }
-  if (p.g.splits > 1 && !p.g.fixup) {
+  if (p.g.splits > 1) {
     const GemmArgs& g = p.g;
     const OutMap& o = g.out;
     auto al4 = [](long long v) { return (v & 3) == 0; };
@@ -3960,6 +3766,7 @@ extern "C" int rgan_adam_packed(int ntensors, float* const* params, const float*
                                 const double* hyper, float* step, int npacks, const RganAdamPack* packs,
                                 void* stream) {
   RGAN_REQUIRE(ntensors >= 0 && npacks >= 0 && hyper && step && (npacks == 0 || packs));
+  RGAN_REQUIRE(ntensors == 0 || (params && grads && exp_avg && exp_avg_sq && numel));
   hipStream_t s = (hipStream_t)stream;
   alignas(16) static const float dummy[4] = {0, 0, 0, 0};
   for (int j = 0; j < ntensors; ++j)
@@ -4069,6 +3876,7 @@ extern "C" int rgan_adam_packed(int ntensors, float* const* params, const float*
 }
 
 static double conv_flops(const RganConv* d) {
+  if (!d) return 0.0;  // (the planner refuses it next)
   const double pix = d->transposed ? (double)d->hin * d->win : (double)d->hout * d->wout;
   return 2.0 * d->batch * (double)d->cin * d->cout * d->kh * d->kw * pix;
 }
@@ -4076,6 +3884,7 @@ static double conv_flops(const RganConv* d) {
 extern "C" int rgan_conv_fwd(const RganConv* d, const float* x, const float* w, const float* wpacked,
                              const float* wscale, const float* bias, float* y, int act, float act_alpha, void* ws,
                              size_t ws_bytes, void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   if (!x || (!w && !wpacked) || !y) return RGAN_EINVAL;
   g_cur_flops = conv_flops(d);
   Plan p;
@@ -4150,7 +3959,7 @@ extern "C" int rgan_conv_post(const RganConv* d, int which, const float* in, con
                               const float* wscale, float* out, void* ws, size_t ws_bytes, const RganPost* post,
                               int* fused, void* stream) {
   if (!in || (!w && !wpacked) || !out || !fused || !post || (which != 0 && which != 1)) return RGAN_EINVAL;
-  if (!post->x || (post->mode != 1 && post->mode != 2)) return RGAN_EINVAL;
+  if (!post->x || (post->mode != 1 && post->mode != 2) || !act_ok(post->act)) return RGAN_EINVAL;
   if (post->mode == 2 && (!post->stats || !post->part || post->nseg < 1)) return RGAN_EINVAL;
   *fused = 0;
   g_cur_flops = conv_flops(d);

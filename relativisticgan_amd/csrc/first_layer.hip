@@ -184,6 +184,7 @@ extern "C" int rgan_g1_fwd_bn(const float* z, int B, int Cin, const float* w, in
                               const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                               long long* num_batches_tracked, int act, float act_alpha, float* y, float* a,
                               float* stats, void* stream) {
+  RGAN_REQUIRE(act_ok(act));
   RGAN_REQUIRE(z && w && y && a && stats && (B == 32 || B == 64) && (Cin == 64 || Cin == 128) &&
                Cout >= G1_CB && Cout % G1_CB == 0 && ((uintptr_t)z & 15) == 0);
   const hipStream_t s = (hipStream_t)stream;

@@ -823,6 +823,7 @@ struct AdamBatch {
 
 __global__ void adam_step_inc(float* step) { step[0] += 1.f; }
 extern "C" int rgan_adam_step_inc(float* step, void* stream) {  // (rgan_adam_packed, conv_gemm.hip)
+  RGAN_REQUIRE(step);
   adam_step_inc<<<1, 1, 0, (hipStream_t)stream>>>(step);
   RGAN_CHECK_LAUNCH();
   return 0;
@@ -878,6 +879,10 @@ extern "C" int rgan_adam(int ntensors, float* const* params, const float* const*
                          float* const* exp_avg_sq, const long long* numel, const double* hyper, float* step,
                          void* stream) {
   RGAN_REQUIRE(ntensors >= 0 && hyper && step);
+  RGAN_REQUIRE(ntensors == 0 || (params && grads && exp_avg && exp_avg_sq && numel));
+  // every tensor checked before the first launch: a refused call changes nothing
+  for (int j = 0; j < ntensors; ++j)
+    RGAN_REQUIRE(params[j] && grads[j] && exp_avg[j] && exp_avg_sq[j] && numel[j] >= 0 && numel[j] < (1LL << 31));
   hipStream_t s = (hipStream_t)stream;
   adam_step_inc<<<1, 1, 0, s>>>(step);
   RGAN_CHECK_LAUNCH();
@@ -888,7 +893,6 @@ extern "C" int rgan_adam(int ntensors, float* const* params, const float* const*
     long long blocks = 0;
     for (int i = 0; i < cnt; ++i) {
       const int j = base + i;
-      RGAN_REQUIRE(params[j] && grads[j] && exp_avg[j] && exp_avg_sq[j] && numel[j] >= 0);
       b.t[i] = AdamTensor{params[j], grads[j], exp_avg[j], exp_avg_sq[j], numel[j]};
       b.first[i] = (int)blocks;
       blocks += (numel[j] + ADAM_BLOCK_ELEMS - 1) / ADAM_BLOCK_ELEMS;
@@ -930,6 +934,7 @@ extern "C" int rgan_gather_images(const float* images, const long long* idx, int
   return 0;
 }
 
-extern "C" const char* rgan_version(void) { return "rgan-mi355x 0.1 gfx950 fp32-mfma"; }
+extern "C" const char* rgan_version(void) { return "rgan-mi355x 0.2 gfx950 fp32-mfma abi2"; }
+extern "C" int rgan_abi_version(void) { return RGAN_ABI_VERSION; }
 
 }  // namespace rgan

@@ -320,8 +320,10 @@ class GradReducer:
         self.inflight.append((work, bi, qs))
 
     def finish(self):
-        """Complete every bucket's all-reduce; afterwards .grad holds the global SUM."""
-        if _S.world == 1:
+        """Complete every bucket's all-reduce; afterwards .grad holds the global SUM.  Gated
+        on the same predicate as ``arm()`` / ``grad_view()`` (``_S.on``): with the data-parallel
+        path forced on one rank the buckets launched by the hooks are waited on here too."""
+        if not _S.on:
             return
         if _S.capture is not None:
             self._finish_captured()
@@ -384,7 +386,7 @@ class GradReducer:
 
 def allreduce_grads(params, bucket_bytes=64 << 20):
     """SUM-all-reduce the .grad of ``params`` in flat buckets (one RCCL call per bucket)."""
-    if _S.world == 1:
+    if not _S.on:
         return
     grads = [p.grad for p in params if p.grad is not None]
     bucket, size = [], 0

@@ -79,9 +79,10 @@ class Trainer:
         self.optG = Adam(self.G.parameters(), lr=p.lr_G, betas=(p.beta1, p.beta2), weight_decay=p.weight_decay)
         self.decayD = torch.optim.lr_scheduler.ExponentialLR(self.optD, gamma=1 - p.decay)
         self.decayG = torch.optim.lr_scheduler.ExponentialLR(self.optG, gamma=1 - p.decay)
-        # gradient SUM all-reduce overlapped with the last backward of each step (world > 1)
-        self.redD = dp.GradReducer(self.D.parameters()) if self.world > 1 else None
-        self.redG = dp.GradReducer(self.G.parameters()) if self.world > 1 else None
+        # gradient SUM all-reduce overlapped with the last backward of each step (world > 1,
+        # or the data-parallel path forced on one rank: dp.setup(force=True))
+        self.redD = dp.GradReducer(self.D.parameters()) if dp.active() else None
+        self.redG = dp.GradReducer(self.G.parameters()) if dp.active() else None
         self._pending_G, self._pending_decay_G = None, False
         # under DP, G's optimizer step waits for the next use of G (flush) so its gradient
         # all-reduce overlaps the next D forward; a PiecewiseGraph capture steps it in place
@@ -98,7 +99,7 @@ class Trainer:
         # (auto): single process only -- under DP the separate D(x) forward is what hides
         # G's deferred gradient all-reduce (flush), and the batched pass needs G(z) first
         bd = getattr(p, "rgan_batch_D", None)
-        bd = (self.world == 1) if bd is None else bool(bd)
+        bd = (not dp.active()) if bd is None else bool(bd)
         self.batch_D = bd and self.pac == 1 and self.D.segmentable
         # the G step's D(G(z)) and D(x) (heads 5-8) as one batched pass (--rgan_batch_G,
         # default on, under data parallelism too: nothing overlaps with its D(x) forward)

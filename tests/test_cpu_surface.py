@@ -36,6 +36,11 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
     assert set(declared) == set(_lib.EXPORTED), set(declared) ^ set(_lib.EXPORTED)
     assert b"gfx950" in lib.rgan_version()
+    # rgan_adam_packed's float[2] step (count + arrival ticket) is ABI revision 2 (include/rgan.h)
+    hdr = open(os.path.join(ROOT, "include", "rgan.h")).read()
+    want = int(re.search(r"#define RGAN_ABI_VERSION (\d+)", hdr).group(1))
+    assert lib.rgan_abi_version() == want == 2
+    assert lib.rgan_version().endswith(b"abi%d" % want)
 
 
 def test_library_rejects_bad_descriptors():

@@ -378,6 +378,22 @@ def _forced_worker(rank, world, port, q):
         red.finish()
         for prm, w_ in zip(params, want):
             assert torch.allclose(prm.grad, w_, atol=1e-6)
+        # finish() ran the forced rank's wait / rebind path: nothing left in flight, the
+        # per-step hand-out set cleared, and every .grad is its slice of the reduced bucket
+        assert red.inflight == [] and red.handed == set() and not red.armed
+        for prm in params:
+            bi, off = red.where[id(prm)], red.offset[id(prm)]
+            assert prm.grad.data_ptr() == red.region(bi, off, prm).data_ptr()
+        # a second step re-arms and hands out slices again
+        for prm in params:
+            prm.grad = None
+        l1, l2 = _losses(params, 0)
+        l1.backward()
+        red.arm()
+        l2.backward()
+        red.finish()
+        for prm, w_ in zip(params, want):
+            assert torch.allclose(prm.grad, w_, atol=1e-6)
         q.put((rank, "ok"))
     except Exception:
         import traceback

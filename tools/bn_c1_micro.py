@@ -1,8 +1,8 @@
 """BatchNorm apply / backward-apply micro-benchmark on the C1 (64², B=32 per step, h=128)
 activation shapes, each launch timed alone (diagnostic; GPU): HIP events around single
 launches separated by a device sync, so the number is one launch's latency as a training step
-sees it, not back-to-back throughput.  Run against variant builds (RGAN_LIB=...) to sweep the
-apply grid (RGAN_BN_APPLY_BLOCKS / RGAN_BN_APPLY_MIN_ITER).
+sees it, not back-to-back throughput.  Run against variant builds (RGAN_LIB=..., a patch of the
+apply grid constants in bn_act.hip built by tools/build_variant.py).
 
 usage: python tools/bn_c1_micro.py [reps]
 """

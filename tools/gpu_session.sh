@@ -21,8 +21,8 @@ for s in $steps; do
   case $s in
     tests)
       RGAN_PARITY_AUDIT=$out/parity timeout -k 10 1100 python -u -m pytest tests -m gpu -v --timeout 300 \
-        --timeout-method thread -p no:cacheprovider > "$out/pytest.log" 2>&1
-      rc=$?; echo "tests rc=$rc"; tail -3 "$out/pytest.log"; stop $rc tests ;;
+        --timeout-method thread -p no:cacheprovider --durations=40 > "$out/pytest.log" 2>&1
+      rc=$?; echo "tests rc=$rc"; grep -A45 "slowest" "$out/pytest.log" | tail -46; tail -2 "$out/pytest.log"; stop $rc tests ;;
     bench*)
       timeout -k 10 500 python -u bench.py $wl > "$out/bench$sfx.json" 2> "$out/bench$sfx.err"
       rc=$?; echo "bench$sfx rc=$rc"; stop $rc bench ;;

@@ -1,7 +1,7 @@
 """Narrow ConvTranspose2d micro-benchmark (diagnostic; GPU): G's image layer (128 -> 3,
 32x32 -> 64x64, tanh) and D's image-layer data gradient (the same ConvT shape, no act) at
 C1 / C2 batch sizes (NARROW_SHAPE=C3: the 256^2 shard's), each launch sequence (narrow kernel + split reduce) timed alone with
-HIP events.  Run against variant builds (RGAN_LIB=..., RGAN_NARROW_MAX_SPLITS=...).
+HIP events.  Run against variant builds (RGAN_LIB=..., tools/build_variant.py).
 
 usage: python tools/narrow_micro.py [reps]
 """
