@@ -662,6 +662,38 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // vector epilogue's per-tile output row offsets (FAST 64x64-per-wave tiles)
+  constexpr bool VEC_EPI = KROW && BM / WM == 64 && BN / WN == 64;
+  __shared__ long long emoff[VEC_EPI ? BM : 1];
+  // Producer post-op (gemm_post: unsplit tiles, vector epilogue): the rows of px the epilogue
+  // multiplies by are loaded into registers at the start of the LAST k tile, so their HBM
+  // latency hides under that tile's MFMAs instead of stalling the epilogue.  The row-offset
+  // table they index is written here, at the start, and published by the main loop's barriers.
+  float4 pax[VEC_EPI && POST ? 16 : 1];
+  const bool post_pf = POST && VEC_EPI && g.pmode && g.splits == 1 && g.vec_out;
+  if constexpr (POST && VEC_EPI) {
+    if (post_pf) {
+      for (int i = tid; i < BM; i += 256) {
+        const int m = m0 + i;
+        emoff[i] = m < g.M ? row_offset(g.out, m, MODE == MODE_CONVT2 ? phase : 0) : 0;
+      }
+    }
+  }
+  auto post_prefetch = [&]() {
+    if constexpr (POST && VEC_EPI) {
+      const int n = n0 + wn + 4 * (lane & 15);
+      if (post_pf && n < g.N) {
+        const long long noff = col_offset(g.out, n);
+#pragma unroll
+        for (int s4 = 0; s4 < 16; ++s4) {
+          const int rl = 4 * s4 + (lane >> 4), m = m0 + wm + rl;
+          pax[s4] = m < g.M ? *reinterpret_cast<const float4*>(g.px + emoff[wm + rl] + noff)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+    }
+  };
+
   if constexpr (FAST && MODE == MODE_WGRAD) {
     if (wid == 0) build_table(kbeg, 0);
     if (wid == 1 && nk > 1) build_table(kbeg + BK, 1);
@@ -713,6 +745,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
       // the compiler a phi of (new, old) registers whose copies wait for the loads right
       // here.  Past the last tile every offset is in-bounds or OOB (buffer loads return 0).
       load_fast(kbeg + (kt + 1) * BK, 0);
+      if (kt + 1 == nk) post_prefetch();
       __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMAs (not sunk for VGPRs)
 #pragma unroll
       for (int t = 0; t < 2; ++t) {  // two k16 steps per BK = 32 tile; lane half lk takes k 8 lk .. 8 lk + 7
@@ -759,6 +792,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
     if (kt + 1 < nk) {
       if constexpr (FAST) load_fast(kbeg + (kt + 1) * BK, (kt + 1) & 1);
       else load_tiles(kbeg + (kt + 1) * BK);
+    } else {
+      post_prefetch();
     }
     if constexpr (FAST && MODE == MODE_WGRAD) {
       if (kt + 2 < nk && wid == (kt & 3)) build_table(kbeg + (kt + 2) * BK, kt & 1);
@@ -821,7 +856,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   const bool split_out = g.splits > 1;  // partial sums for a separate splitk_reduce
 
   // ---------------- epilogue ----------------
-  if constexpr (KROW && BM / WM == 64 && BN / WN == 64) {
+  if constexpr (VEC_EPI) {
     // Vector epilogue (FAST, 64x64 per wave): each wave stages its finished sub-tile in LDS
     // (row stride 72: the two lane halves' rows 4 apart land 32 banks apart) and writes it
     // back as float4 rows -- 16 b128 stores per lane instead of 64 scalar ones, 256
@@ -830,10 +865,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
     const bool slab_out = split_out;
     if ((slab_out && g.N % 4 == 0) || (!slab_out && g.vec_out)) {
       constexpr int EP_LD = 72, EPR = GEMM_SB ? 32 : 64, NP = 64 / EPR;
-      __shared__ long long emoff[BM];
       float* T = smem + wid * (EPR * EP_LD);
       const float wsc = (!slab_out && g.wscale) ? g.wscale[0] : 1.f;
-      if (!slab_out) {
+      if (!slab_out && !post_pf) {
         for (int i = tid; i < BM; i += 256) {
           const int m = m0 + i;
           emoff[i] = m < g.M ? row_offset(g.out, m, MODE == MODE_CONVT2 ? phase : 0) : 0;
@@ -895,15 +929,10 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
           }
         }
         if (n < g.N && pmode) {
-          // producer post-op: the wave's 16 rows of px first (independent loads in flight
-          // together -- one latency, not one per row), then the rows
-          float4 ax[EPR / 4];
-#pragma unroll
-          for (int s4 = 0; s4 < EPR / 4; ++s4) {
-            const int rl = 4 * s4 + (lane >> 4), m = m0 + wm + EPR * pp + rl;
-            ax[s4] = m < g.M ? *reinterpret_cast<const float4*>(g.px + emoff[wm + EPR * pp + rl] + noff)
-                             : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
+          // producer post-op: the wave's 16 rows of px, loaded during the last k tile
+          // (post_prefetch; GEMM_SB is off for these 128x128 tiles: one pass, pp = 0)
+          static_assert(!POST || EPR == 64, "post-op prefetch covers one 64-row pass");
+          const float4* ax = pax;
 #pragma unroll
           for (int s4 = 0; s4 < EPR / 4; ++s4) {
             const int rl = 4 * s4 + (lane >> 4), m = m0 + wm + EPR * pp + rl;

@@ -30,7 +30,6 @@ def main():
             defs.append(a)
     out_dir = os.path.join(ROOT, "tools", "variants")
     os.makedirs(out_dir, exist_ok=True)
-    B.build()
     scratch = tempfile.mkdtemp(prefix="rgan_variant_")
     try:
         shutil.copytree(os.path.join(ROOT, "relativisticgan_amd", "csrc"),
@@ -44,6 +43,10 @@ def main():
                     touched.add(os.path.basename(line.split()[1]))
         if not touched:
             touched.add(os.environ.get("VARIANT_SRC", "conv_gemm.hip"))
+        # the untouched translation units come from the in-tree build (built here only if
+        # missing: the in-tree library may be on its way to a GPU box and is left alone)
+        if any(not os.path.exists(os.path.join(B.BUILD, s.replace(".hip", ".o"))) for s in B.SOURCES if s not in touched):
+            B.build()
         csrc = os.path.join(scratch, "relativisticgan_amd", "csrc")
         flags = [f if not f.startswith("-I") else "-I" + os.path.join(scratch, "include") for f in B.FLAGS]
         objs = []
