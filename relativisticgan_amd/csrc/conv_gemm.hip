@@ -208,6 +208,17 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
     phase = q / tiles_m;
     split = blockIdx.z;
     z = phase * g.splits + split;
+  } else if (g.xgroup == 3) {
+    // band order: XCD x (dispatch slot b % 8) takes the x-th eighth of the m tiles, in order,
+    // each m tile's n tiles and phases back to back -- the blocks in flight on one XCD cover
+    // consecutive output rows, which read overlapping input rows (4 x 4 windows, stride 2)
+    const int b = blockIdx.x, r = b >> 3, per = g.tiles_n * g.nph;
+    const int q = r % per;
+    tm_i = (b & 7) * ((g.M + BM - 1) / BM / 8) + r / per;
+    tn_i = q % g.tiles_n;
+    phase = q / g.tiles_n;
+    split = blockIdx.z;
+    z = phase * g.splits + split;
   } else if (g.xgroup) {
     const int b = blockIdx.x, r = b >> 3, per = g.tiles_n * g.nph;
     const int q = r % per;
@@ -3611,7 +3622,7 @@ static int run_plan(Plan& p, void* ws, size_t ws_bytes, hipStream_t s) {
   tile_dims(p.cfg, bm, bn);
   const int tiles_m = ceil_div(p.g.M, bm);
   p.g.nph = p.phases;
-  p.g.xgroup = p.fast && p.mode != MODE_WGRAD && tiles_m % 8 == 0 && p.g.tiles_n * p.phases > 1;
+  p.g.xgroup = p.fast && p.mode != MODE_WGRAD && tiles_m % 8 == 0 ? 3 : 0;
   // weight-column grouping where the weights dominate: under A-row grouping every XCD fetches
   // the whole weight (D's 2048 -> 4096 conv at C3: 4.36 GB of FETCH per launch for a 537 MB
   // weight; 1.01 GB grouped by weight columns).  Under weight-column grouping every XCD reads

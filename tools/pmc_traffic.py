@@ -22,13 +22,13 @@ import sys
 PIECE64 = ("convt2_narrow_mfma",)
 
 
-def load(pattern, counter):
+def load(pattern, counter, by_grid=False):
     acc = collections.defaultdict(lambda: [0, 0.0])
     for f in glob.glob(pattern):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            a = acc[r["Kernel_Name"]]
+            a = acc[(r["Kernel_Name"], int(r["Grid_Size"])) if by_grid else r["Kernel_Name"]]
             a[0] += 1
             a[1] += float(r["Counter_Value"]) * 1024.0
     return acc
@@ -36,17 +36,21 @@ def load(pattern, counter):
 
 def main():
     d = sys.argv[1]
-    fe = load(os.path.join(d, "fetch", "**", "*counter_collection.csv"), "FETCH_SIZE")
-    fe.update(load(os.path.join(d, "fetch", "*counter_collection.csv"), "FETCH_SIZE"))
-    wr = load(os.path.join(d, "write", "**", "*counter_collection.csv"), "WRITE_SIZE")
-    wr.update(load(os.path.join(d, "write", "*counter_collection.csv"), "WRITE_SIZE"))
+    bg = "--by-grid" in sys.argv  # per (symbol, grid size): the launches of one layer shape
+    fe = load(os.path.join(d, "fetch", "**", "*counter_collection.csv"), "FETCH_SIZE", bg)
+    fe.update(load(os.path.join(d, "fetch", "*counter_collection.csv"), "FETCH_SIZE", bg))
+    wr = load(os.path.join(d, "write", "**", "*counter_collection.csv"), "WRITE_SIZE", bg)
+    wr.update(load(os.path.join(d, "write", "*counter_collection.csv"), "WRITE_SIZE", bg))
     out = {}
     for k in fe:
         n_f, b_f = fe[k]
         n_w, b_w = wr.get(k, [0, 0.0])
         fetch = (1.0 if any(p in k for p in PIECE64) else 2.0) * b_f / max(n_f, 1)
         write = b_w / max(n_w, 1)
-        out[k] = {"launches": n_f, "fetch_bytes": fetch, "write_bytes": write, "bytes_per_launch": fetch + write}
+        key = f"{k[0]} @grid {k[1]}" if bg else k
+        if bg and "gemm" not in k[0]:
+            continue
+        out[key] = {"launches": n_f, "fetch_bytes": fetch, "write_bytes": write, "bytes_per_launch": fetch + write}
     print(json.dumps(out, indent=1, sort_keys=True))
 
 

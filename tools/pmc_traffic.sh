@@ -10,4 +10,5 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$out/fetch" -o run --output-format csv -- python3 "$root/bench.py" "$@" > "$out/fetch.log" 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$out/write" -o run --output-format csv -- python3 "$root/bench.py" "$@" > "$out/write.log" 2>&1
 python3 "$root/tools/pmc_traffic.py" "$out" > "$out/traffic.json"
+python3 "$root/tools/pmc_traffic.py" "$out" --by-grid > "$out/traffic_by_grid.json"
 echo "head $(cat "$root/BUILD_HEAD" 2>/dev/null || echo unknown); bench.py $*" > "$out/provenance.txt"
