@@ -38,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "train images/sec (D+G step) RaLSGAN DCGAN 64²/256² at 1/2/4/8 GPU; MFMA util"
-FP32_MFMA_PEAK = 157.3e12  # MI355X_MICROARCH.md: Peak FP32 (matrix) = vector peak
+from relativisticgan_amd.perf import FP32_MFMA_PEAK, conv_flops_per_iteration  # noqa: E402
 BF16_MFMA_PEAK = 2.5e15    # MI355X_MICROARCH.md: Peak BF16 MFMA, dense
 EMU_PRODUCTS = 6           # bf16 MFMA products per emulated fp32 product (bf16x6)
 
@@ -61,45 +61,6 @@ WORKLOADS = {
 ARCH = {"C4": 1}
 DEFAULT_WORKLOAD = "C3"
 EXTRA_WORKLOADS = ("C1", "C2")
-
-
-def conv_flops_per_iteration(t):
-    """Algorithmic conv FLOPs of one reference iteration, F = forward conv
-    FLOPs (2*MACs) per net, d0/g0 = the image-side first layers (no data gradient needed):
-      relativistic heads 5-8: 9 F_D + 4 F_G - 2 d0 - g0  (D step: D(x), D(fake) fwd+wgrad+
-        dgrad, G fwd; G step: G fwd, D(fake) fwd + dgrad, G wgrad + dgrad, D(x) fwd);
-      heads 1-4: the G step has no D(x): 8 F_D + 4 F_G - 2 d0 - g0;
-      gradient penalty (GLI:646-658): + D(x_hat) fwd, its create-graph dgrad chain, and the
-        double backward (adjoint conv fwd + wgrad per dgrad, then wgrad + dgrad back through
-        the forward): 6 F_D - d0 - 3 F_end."""
-    def layer_flops(net, x_shape):
-        out, h = [], torch.zeros(x_shape, device="meta")
-        for layer in net._plan:
-            c = layer.conv
-            geom = layer.spec.geom
-            if layer.in_view is not None:
-                h = torch.zeros((h.shape[0],) + tuple(layer.in_view), device="meta")
-            B, cin, H, W = h.shape
-            w = c.w if hasattr(c, "w") else c.weight
-            if layer.w_view is not None:
-                w = w.view(*layer.w_view)
-            cout = w.shape[1] if geom.transposed else w.shape[0]
-            Ho, Wo = geom.out_hw(H, W)
-            pix = H * W if geom.transposed else Ho * Wo
-            out.append(2.0 * B * cin * cout * geom.k * geom.k * pix)
-            h = torch.zeros((B, cout, Ho, Wo), device="meta")
-            if layer.out_view is not None:
-                h = torch.zeros((B,) + tuple(layer.out_view), device="meta")
-        return out
-    p = t.p
-    fg = layer_flops(t.G, (t.B, p.z_size, 1, 1))
-    fd = layer_flops(t.D, (t.B, p.n_colors * getattr(p, "pac", 1), p.image_size, p.image_size))
-    total = 9 * sum(fd) + 4 * sum(fg) - 2 * fd[0] - fg[0]
-    if p.loss_D <= 4:
-        total -= sum(fd)
-    if p.loss_D == 3 or p.grad_penalty:
-        total += 6 * sum(fd) - fd[0] - 3 * fd[-1]
-    return total
 
 
 def pmc_traffic(workload, symbol):

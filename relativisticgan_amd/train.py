@@ -24,6 +24,7 @@ from .kernels import DeviceRNG
 from .losses import gradient_penalty, loss_D, loss_D_cat, loss_D_fake, loss_D_real, loss_G, loss_G_cat, unit_seed
 from .nets import DCGAN_D, DCGAN_G, weights_init
 from .optim import Adam
+from .perf import ThroughputMeter
 
 
 def synthetic_images(n, size, n_colors=3, seed=1234, device="cuda"):
@@ -474,6 +475,9 @@ def main(argv=None):
         say(f"Resumed from iteration {current_set_images * p.gen_every}.")
     say(t.G)
     say(t.D)
+    meter = ThroughputMeter(t) if p.rgan_perf_log else None
+    if meter is not None:
+        meter.tick(iter_offset, time.time())
     for i in range(iter_offset, p.n_iter):
         t.iteration(i)
         if i % p.print_every == 0:  # GLI:563-565 (the sample batch was drawn inside the iteration)
@@ -481,7 +485,11 @@ def main(argv=None):
             if lead:
                 save_image(grid, os.path.join(base, "images", "fake_samples_iter%05d.png" % i), normalize=True)
         if (i + 1) % p.print_every == 0:
-            say(t.log_line(i, time.time() - start))
+            say(t.log_line(i, time.time() - start))  # the reference's line, unchanged (GLI:723-726)
+            if meter is not None:  # plus img/s and MFMA%, on a line of its own
+                perf = meter.tick(i + 1, time.time())
+                if perf:
+                    say(perf)
         if (i + 1) % p.gen_every == 0:
             current_set_images += 1
             if p.save:

@@ -25,6 +25,10 @@ def test_train_cli_outputs_and_resume():
     assert os.path.isfile(os.path.join(base, "logs", "log.txt"))
     log = open(os.path.join(base, "logs", "log.txt")).read()
     assert "[1] Diff:" in log and "[3] Diff:" in log and "Models saved" in log
+    # the reference line unchanged, then img/s and MFMA% on a line of its own
+    import re
+    perf = re.findall(r"^\[(\d+)\] img/s: ([0-9.]+) MFMA%: ([0-9.]+)$", log, re.M)
+    assert perf and all(float(v) > 0 for _, v, _ in perf), log[-400:]
     for i in (0, 2):
         img = np.asarray(Image.open(os.path.join(base, "images", "fake_samples_iter%05d.png" % i)))
         assert img.shape == (32 + 2 + 2, 8 * (32 + 2) + 2, 3)  # make_grid: 8 per row, padding 2

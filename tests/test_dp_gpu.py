@@ -53,10 +53,10 @@ def _capture(t, store):
 N_ITER = {"ralsgan_pac2": 1}
 
 
-def _run(name, world, rank, n_iter=None, device="cuda:0", batch_D=None, batch_G=None):
+def _run(name, world, rank, n_iter=None, device="cuda:0", batch_D=None, batch_G=None, overrides=None):
     n_iter = n_iter or N_ITER.get(name, 2)
     from relativisticgan_amd.train import Trainer
-    p = param_for(name)
+    p = param_for(name, **(overrides or {}))
     p.rgan_rng = "host"
     p.rgan_batch_D = batch_D
     if batch_G is not None:
@@ -74,7 +74,7 @@ def _run(name, world, rank, n_iter=None, device="cuda:0", batch_D=None, batch_G=
 
 
 def _worker(rank, world, port, name, path, sync_bn=True, n_iter=None, backend="gloo", batch_D=None, batch_G=None,
-            force=False):
+            force=False, overrides=None):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dev = rank if backend == "nccl" else 0  # RCCL: one GPU per rank; gloo: both ranks on cuda:0
@@ -83,7 +83,8 @@ def _worker(rank, world, port, name, path, sync_bn=True, n_iter=None, backend="g
     from relativisticgan_amd import dp
     dp.setup(sync_bn=sync_bn, force=force)
     try:
-        res = _run(name, world, rank, n_iter, device=f"cuda:{dev}", batch_D=batch_D, batch_G=batch_G)
+        res = _run(name, world, rank, n_iter, device=f"cuda:{dev}", batch_D=batch_D, batch_G=batch_G,
+                   overrides=overrides)
         # gather the per-rank D outputs so rank 0 holds the global vectors
         for st in res:
             for k in ("y_pred", "y_pred_fake"):
@@ -102,12 +103,14 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
-def _spawn(name, sync_bn=True, n_iter=None, backend="gloo", batch_D=None, world=2, batch_G=None, force=False):
+def _spawn(name, sync_bn=True, n_iter=None, backend="gloo", batch_D=None, world=2, batch_G=None, force=False,
+           overrides=None):
     path = os.path.join(tempfile.mkdtemp(), "dp.pt")
     ctx = mp.get_context("spawn")
     port = _free_port()
     procs = [ctx.Process(target=_worker,
-                         args=(r, world, port, name, path, sync_bn, n_iter, backend, batch_D, batch_G, force))
+                         args=(r, world, port, name, path, sync_bn, n_iter, backend, batch_D, batch_G, force,
+                               overrides))
              for r in range(world)]
     for pr in procs:
         pr.start()
@@ -158,11 +161,11 @@ def test_dp1_rccl_forced_matches_single_process(name, sync_bn):
     _compare(name, dpres, single)
 
 
-def _oracle_data_parallel(name, shards, n_iter=1):
+def _oracle_data_parallel(name, shards, n_iter=1, overrides=None):
     """The reference's --n_gpu data_parallel step (GLI:393, GLI:455) on the CPU oracle."""
     from oracle.reference_cpu import Trainer as OracleTrainer
     torch.set_num_threads(8)
-    p = param_for(name, dp_shards=shards)
+    p = param_for(name, dp_shards=shards, **(overrides or {}))
     holder, out = {}, []
 
     def hooks(tag, r):
@@ -215,6 +218,28 @@ def test_dp4_per_shard_bn_matches_reference_data_parallel(name):
     dpres = _spawn(name, sync_bn=False, n_iter=1, world=4)
     ref = _oracle_data_parallel(name, 4)
     _compare(name, dpres, ref)
+
+
+# configs[2]'s shape in miniature: 8 ranks (8 x MI355X), 2 samples each of a global batch of 16
+DP8 = {"batch_size": 16}
+
+
+def test_dp8_per_shard_bn_matches_reference_data_parallel():
+    """8 ranks sharing cuda:0 (gloo) with per-shard BatchNorm -- what bench.py's N = 8 line runs
+    (config.batchnorm) -- against the oracle's data_parallel over 8 replicas (GLI:393-394,
+    455-456 with --n_gpu 8): the 8-chunk scatter, per-replica BN statistics, replica 0's running
+    statistics, 8-rank bucket sequencing and the 8-way distributed heads."""
+    dpres = _spawn("ralsgan", sync_bn=False, n_iter=1, world=8, overrides=DP8)
+    ref = _oracle_data_parallel("ralsgan", 8, overrides=DP8)
+    _compare("ralsgan", dpres, ref)
+
+
+def test_dp8_syncbn_matches_single_process():
+    """8 ranks with SyncBN: the rank-ordered merge of 8 ranks' BatchNorm moments equals the
+    single-process global-batch step."""
+    dpres = _spawn("ralsgan", world=8, overrides=DP8)
+    single = _run("ralsgan", 1, 0, overrides=DP8)
+    _compare("ralsgan", dpres, single)
 
 
 @pytest.mark.parametrize("sync_bn", [True, False])

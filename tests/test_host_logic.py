@@ -59,3 +59,16 @@ def test_batch_G_flag():
     assert make_param().rgan_batch_G is None
     p = parse(["--rgan_batch_G", "False"])
     assert p.rgan_batch_G is False
+
+
+def test_throughput_meter_line():
+    """train.main's SURVEY §5 log suffix: img/s of the global batch and MFMA% of one GPU from
+    the conv FLOPs of an iteration (the same count bench.py uses)."""
+    from relativisticgan_amd import perf
+
+    m = perf.ThroughputMeter.__new__(perf.ThroughputMeter)
+    m.flops, m.images, m.t0, m.i0 = 1.573e12, 32, None, None
+    assert m.tick(0, 10.0) is None          # first point: nothing to report yet
+    line = m.tick(10, 12.0)                 # 10 iterations in 2 s = 5 it/s
+    assert line == "[10] img/s: 160.0 MFMA%%: %.1f" % (100.0 * 5 * 1.573e12 / perf.FP32_MFMA_PEAK)
+    assert perf.FP32_MFMA_PEAK == 157.3e12  # (the meter on a real trainer: tests/test_cli_gpu.py)
