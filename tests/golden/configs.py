@@ -79,6 +79,11 @@ CONFIGS = {
     "rahinge_spectral_c5": {"args": {"image_size": 128, "batch_size": 32, "z_size": 128, "G_h_size": 128,
                                      "D_h_size": 128, "loss_D": 8, "spectral": "True", "n_iter": 2},
                             "seed": 1, "n_images": 64, "threads": 8},
+    # C4 = configs[3] on the reference's "standard CNN" (arch 1, 32x32 only: GLI:186-319) at the
+    # bench's batch 32, z = 128 -- the bench's C4 workload at full size (round 5; the arch-1
+    # configs above run B = 8)
+    "wgangp_c4": {"args": {"image_size": 32, "batch_size": 32, "z_size": 128, "loss_D": 3, "arch": 1,
+                           "n_iter": 2}, "seed": 1, "n_images": 64, "threads": 8},
     # C3 = the per-GPU shard of configs[2] (the bench's headline workload): RaLSGAN DCGAN
     # 256x256, batch 32, h = z = 128 (GLI:329 mult = S/8 -> 5 middle layers per net; heads
     # GLI:639, 705).  ~2.5 min of reference CPU time per iteration at 8 threads.
@@ -88,7 +93,7 @@ CONFIGS = {
 }
 
 # full-size configs: minutes of CPU oracle time each (GPU parity runs them with all host cores)
-FULL_SIZE = ("ralsgan_c1", "rasgan_c2", "wgangp_c4p", "rahinge_spectral_c5", "ralsgan_c3")
+FULL_SIZE = ("ralsgan_c1", "rasgan_c2", "wgangp_c4p", "wgangp_c4", "rahinge_spectral_c5", "ralsgan_c3")
 # configs too slow for the default CPU suite's bitwise oracle pin (RGAN_SLOW=1 runs them)
 SLOW_PIN = ("ralsgan_c3",)
 
