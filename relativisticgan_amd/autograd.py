@@ -37,33 +37,15 @@ class owning_grads:
     ``torch.autograd.grad`` call, which must not touch ``.grad`` -- autograd's own
     accumulation is used."""
     active = False
-    # Weight gradients written into .grad (the _own_grad path) may run on a second stream,
-    # overlapping the data-gradient chain below them; the context's exit joins it back, so
-    # .grad is complete for whatever follows the backward (Adam, a test reading it).
-    side_stream = False
-    _streams = {}
+    # (Round 4 also ran these weight gradients on a second stream overlapping the data-gradient
+    # chain: bitwise equal and slower everywhere -- C1 -5 %, C3 -1.7 %, DESIGN §3 -- and removed
+    # in round 5.)
 
     def __enter__(self):
         self.prev, owning_grads.active = owning_grads.active, True
 
     def __exit__(self, *exc):
         owning_grads.active = self.prev
-        s = owning_grads._used
-        if s is not None:
-            owning_grads._used = None
-            torch.cuda.current_stream(s.device).wait_stream(s)
-
-    _used = None
-
-    @staticmethod
-    def wgrad_stream(device):
-        """The weight-gradient stream for ``device``, forked from the current stream."""
-        s = owning_grads._streams.get(device)
-        if s is None:
-            s = owning_grads._streams[device] = torch.cuda.Stream(device)
-        s.wait_stream(torch.cuda.current_stream(device))
-        owning_grads._used = s
-        return s
 
 ACT_TRACE = None
 ACT_TAGS = []      # per ACT_TRACE entry: the net that produced it ("G" / "D", set by nets._Net)
@@ -366,9 +348,10 @@ class ConvLayerFn(torch.autograd.Function):
                 done = None  # the GEMM above wrote the plain gradient
             elif done[0] != da.data_ptr():
                 # the layer above applied this layer's act' / BatchNorm sums to the gradient it
-                # produced, but a different tensor arrived here (a cast, a hook, a second
-                # consumer re-materialised it): running the first pass again would be silently
-                # wrong, so refuse
+                # produced, but a different tensor arrived here.  Links exist only between
+                # consecutive layers inside one nets._Net call, whose intermediate activations
+                # never leave the call (no user hook or second consumer can reach them), so this
+                # is an internal assertion: running the first pass again would be silently wrong
                 raise RuntimeError("LayerLink: the fused output gradient was replaced before this layer's "
                                    "backward (hook / cast / second consumer of the activation)")
         # ... and this layer's data gradient may carry the layer below's first pass
@@ -443,22 +426,6 @@ class ConvLayerFn(torch.autograd.Function):
                     u, v, inv_sigma = sn
                     dwe, _ = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape))
                     g = K.spectral_backward(w, dwe, u, v, inv_sigma, spec.geom.transposed, out=acc)
-                elif owning_grads.side_stream:
-                    # on the weight-gradient stream: x, dy and .grad stay allocated until it
-                    # has read / written them (record_stream); the context's exit joins it
-                    main = torch.cuda.current_stream(w.device)
-                    ws = owning_grads.wgrad_stream(w.device)
-                    with torch.cuda.stream(ws):
-                        x.record_stream(ws)
-                        dy.record_stream(ws)
-                        if acc is not None:
-                            acc.record_stream(ws)
-                        if ctx.g1:
-                            g = K.g1_wgrad(x, dy, tuple(w.shape), out=acc)
-                        else:
-                            g, _ = K.conv_wgrad(x, dy, spec.geom, tuple(w.shape), out=acc)
-                    if acc is None:
-                        g.record_stream(main)
                 elif ctx.g1:
                     g = K.g1_wgrad(x, dy, tuple(w.shape), out=acc)
                 else:
