@@ -95,6 +95,13 @@ struct GemmArgs {
   int xgroup, nph;        // XCD-grouped tile order (1: blocks sharing A rows on one XCD, 2: sharing weight columns); phases
   double* bnp;            // nullable: BatchNorm moments of every 64-row output segment (vector epilogue)
   int accum;              // WGRAD: add into C (gradient accumulation) instead of overwriting it
+  // FAST conv WGRAD with a bias (rgan_conv_wgrad dbias): the bias gradient sum_p dy[p][m] is
+  // formed from the A tiles the GEMM stages anyway (the n-tile-0 blocks); unsplit: written to
+  // dbias (added when db_accum), split: per-split doubles dbp[split][M], summed in split order
+  // by the WGRAD reduce
+  double* dbp;
+  float* dbias;
+  int db_accum;
   // Post-op for the layer that PRODUCED this GEMM's output operand (rgan_conv_post: a data
   // gradient, or G's image-layer gradient GEMM), applied where the value is final (unsplit
   // epilogue or split-K reduce); px has C's layout (host-checked):
@@ -577,10 +584,20 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
     }
   };
 
+  // bias gradient of a FAST conv WGRAD (GemmArgs::dbias): this thread's 4 channels (m0 + 4 q
+  // .. + 3, q = sw_q(BM)) summed in double over the pixels it stages
+  const bool db_on = SWZ && g.dbias != nullptr && tn_i == 0;
+  double dbs[4] = {0.0, 0.0, 0.0, 0.0};
   auto store_tiles = [&](int buf) {
     float* As = smem + buf * STAGE;
     float* Bs = As + A_SZ;
     if constexpr (SWZ) {
+      if (db_on) {
+#pragma unroll
+        for (int i = 0; i < FA_N; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dbs[j] += (double)ra[4 * i + j];
+      }
       // element (row, k) at row * 32 + 4 ((k >> 2) ^ ((row >> 1) & 7)) + (k & 3)
       auto put = [&](float* T, int R, const float* v, int nld) {
         const int q = sw_q(R);
@@ -866,6 +883,32 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
 
   const bool split_out = g.splits > 1;  // partial sums for a separate splitk_reduce
 
+  if constexpr (SWZ) {
+    if (db_on) {
+      // the 8 threads staging the same channel quad (pixel slots t8 = ((tid >> 3) & 3) +
+      // 4 (tid >> 7)) -> one double per channel, t8 in order (the main loop's last barrier has
+      // retired every stage read; the epilogue reuses smem after the second barrier)
+      double* dsh = reinterpret_cast<double*>(smem);
+      constexpr int NT8 = 1024 / BM;  // threads staging one channel quad
+      const int q = sw_q(BM), t8 = ((tid >> 3) & 3) + 4 * ((tid >> 5) / (BM / 32));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dsh[t8 * BM + 4 * q + j] = dbs[j];
+      __syncthreads();
+      if (tid < BM && m0 + tid < g.M) {
+        double v = 0.0;
+#pragma unroll
+        for (int t = 0; t < NT8; ++t) v += dsh[t * BM + tid];
+        if (split_out) {
+          g.dbp[(size_t)split * g.M + m0 + tid] = v;
+        } else {
+          float* dst = g.dbias + m0 + tid;
+          *dst = g.db_accum ? *dst + (float)v : (float)v;
+        }
+      }
+      __syncthreads();
+    }
+  }
+
   // ---------------- epilogue ----------------
   if constexpr (VEC_EPI) {
     // Vector epilogue (FAST, 64x64 per wave): each wave stages its finished sub-tile in LDS
@@ -1134,8 +1177,20 @@ __device__ __forceinline__ void red_sum(const float* s, size_t stride, int split
     for (int i = 0; i < V; ++i) v[i] = sp == 0 ? s[(size_t)sp * stride + i] : v[i] + s[(size_t)sp * stride + i];
 }
 
+// split FAST conv WGRAD with a bias: dbias[m] (+)= sum over splits of dbp[split][m] in split
+// order (double), by the first block of the WGRAD reduce
+__device__ __forceinline__ void wgrad_db_finish(const GemmArgs& g) {
+  if (g.dbias == nullptr || blockIdx.x != 0 || blockIdx.y != 0) return;
+  for (int m = threadIdx.x; m < g.M; m += blockDim.x) {
+    double v = 0.0;
+    for (int sp = 0; sp < g.splits; ++sp) v += g.dbp[(size_t)sp * g.M + m];
+    g.dbias[m] = g.db_accum ? g.dbias[m] + (float)v : (float)v;
+  }
+}
+
 template <int MODE, int KIND>
 __global__ __launch_bounds__(256) void splitk_reduce(GemmArgs g, FastDiv fdiv, uint32_t per_phase) {
+  if constexpr (MODE == MODE_WGRAD) wgrad_db_finish(g);
   const int phase = blockIdx.y;
   const size_t MN = (size_t)g.M * g.N;
   const float* base = g.slab + (size_t)phase * g.splits * MN;
@@ -1206,6 +1261,7 @@ __global__ __launch_bounds__(256) void splitk_reduce(GemmArgs g, FastDiv fdiv, u
 constexpr int REDW_OUT = 16, REDW_LANES = 16;
 template <int MODE>
 __global__ __launch_bounds__(256) void splitk_reduce_wide(GemmArgs g, FastDiv fdiv, uint32_t per_phase) {
+  if constexpr (MODE == MODE_WGRAD) wgrad_db_finish(g);
   __shared__ float sh[REDW_LANES][REDW_OUT + 1];
   const int phase = blockIdx.y, ob = threadIdx.x % REDW_OUT, l = threadIdx.x / REDW_OUT;
   const size_t MN = (size_t)g.M * g.N;
@@ -3731,8 +3787,9 @@ extern "C" size_t rgan_conv_workspace(const RganConv* d, int which, int prepacke
   if (rc) return 0;
   if (prepacked && which != 2) p.prepacked = dummy;
   size_t extra = 0;
-  if (which == 2)  // bias-gradient reduction scratch (rgan_channel_sum), after the plan's
-    extra = align_up(rgan_bn_partial_bytes((long long)d->batch * d->hout * d->wout, d->cout), 256);
+  if (which == 2)  // bias-gradient reduction scratch (rgan_channel_sum, or the fused per-split sums), after the plan's
+    extra = align_up(std::max(rgan_bn_partial_bytes((long long)d->batch * d->hout * d->wout, d->cout),
+                              (size_t)p.g.splits * p.g.M * sizeof(double) + 256), 256);
   return align_up(plan_ws_bytes(p), 256) + extra + 256;  // never 0 for a valid descriptor
 }
 
@@ -4026,12 +4083,11 @@ extern "C" int rgan_conv_wgrad(const RganConv* d, const float* x, const float* d
   p.g.accum = accumulate ? 1 : 0;
   p.da.accum = p.g.accum;
   const size_t plan_bytes = align_up(plan_ws_bytes(p), 256);
-  rc = run_plan(p, ws, ws_bytes, (hipStream_t)stream);
-  if (rc) return rc;
+  // per-output-channel sum of dy (Conv2d and ConvTranspose2d alike: dy has cout channels),
+  // checked before anything is launched
+  const long long P = (long long)d->batch * d->hout * d->wout;
+  long long sp = 0;
   if (dbias) {
-    // per-output-channel sum of dy (Conv2d and ConvTranspose2d alike: dy has cout channels)
-    const long long P = (long long)d->batch * d->hout * d->wout;
-    long long sp;
     if ((long long)d->hout * d->wout == 1) {
       sp = d->ys[0];
     } else {
@@ -4042,8 +4098,20 @@ extern "C" int rgan_conv_wgrad(const RganConv* d, const float* x, const float* d
     }
     const size_t need = plan_bytes + rgan_bn_partial_bytes(P, d->cout);
     if (!ws || ws_bytes < need) return RGAN_EINVAL;
-    return rgan_channel_sum(dy, P, d->cout, sp, d->ys[1], dbias, accumulate, (char*)ws + plan_bytes, stream);
   }
+  // a FAST Conv2d weight gradient stages dy as its A operand: the GEMM sums the bias
+  // gradient from those tiles (GemmArgs::dbias) instead of a channel-sum pass over dy
+  const bool bias_fused = dbias && p.mode == MODE_WGRAD && p.fast && !d->transposed && ws_bytes >= plan_bytes &&
+                          (p.g.splits == 1 || (size_t)p.g.splits * p.g.M * sizeof(double) <= ws_bytes - plan_bytes);
+  if (bias_fused) {
+    p.g.dbias = dbias;
+    p.g.db_accum = accumulate ? 1 : 0;
+    p.g.dbp = p.g.splits > 1 ? reinterpret_cast<double*>((char*)ws + plan_bytes) : nullptr;
+  }
+  rc = run_plan(p, ws, ws_bytes, (hipStream_t)stream);
+  if (rc) return rc;
+  if (dbias && !bias_fused)
+    return rgan_channel_sum(dy, P, d->cout, sp, d->ys[1], dbias, accumulate, (char*)ws + plan_bytes, stream);
   return 0;
 }
 

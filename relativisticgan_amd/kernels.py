@@ -106,9 +106,21 @@ class _PackCache:
         reuse = ent is not None and ent[0]() is base and ent[2].numel() == n
         buf = ent[2] if reuse else torch.empty(n, dtype=torch.float32, device=w.device)
         L.check(lib.rgan_conv_pack(ctypes.byref(d), which, L.ptr(w), L.ptr(buf), L.stream()), "rgan_conv_pack")
-        # (the descriptor, layout and a weak reference to w itself let refresh() repack it)
-        self.entries[key] = (weakref.ref(base, self._drop(key)), ver, buf, w.data_ptr(), d, which, weakref.ref(w))
+        # (the descriptor, layout and w's view geometry on its base let refresh() and the
+        # optimizer's layout writer find the weight again: a view such as arch 1's dense layers
+        # viewed as convolutions is a new tensor object at every call, so a weak reference to it
+        # would die with the call and its layout would be repacked at every use)
+        geo = None if w is base else (tuple(w.shape), tuple(w.stride()), w.storage_offset())
+        self.entries[key] = (weakref.ref(base, self._drop(key)), ver, buf, w.data_ptr(), d, which, geo)
         return buf
+
+    @staticmethod
+    def _weight(ent):
+        """The packed weight of an entry (its base parameter, or the view of it that was packed)."""
+        base = ent[0]()
+        if base is None or ent[6] is None:
+            return base
+        return base.as_strided(*ent[6])
 
     def refresh(self, params):
         """Repack, in one batched launch, every cached layout of ``params`` whose weight
@@ -117,7 +129,7 @@ class _PackCache:
         ids = {id(p) for p in params}
         todo = []
         for key, ent in self.entries.items():
-            base, w = ent[0](), ent[6]()
+            base, w = ent[0](), self._weight(ent)
             if base is None or w is None or id(base) not in ids:
                 continue
             if ent[1] == w._version and ent[3] == w.data_ptr():
@@ -142,7 +154,7 @@ class _PackCache:
         idx = {id(p): i for i, p in enumerate(params)}
         out = []
         for key, ent in self.entries.items():
-            base, w = ent[0](), ent[6]()
+            base, w = ent[0](), self._weight(ent)
             if base is None or w is None or id(base) not in idx or w.data_ptr() != params[idx[id(base)]].data_ptr():
                 continue
             if w.numel() != params[idx[id(base)]].numel():
@@ -153,7 +165,7 @@ class _PackCache:
     def mark_current(self, layouts):
         """The listed layouts were rewritten from their weights' current values."""
         for _, key, ent in layouts:
-            w = ent[6]()
+            w = self._weight(ent)
             if w is not None and self.entries.get(key) is ent:
                 self.entries[key] = (ent[0], w._version, ent[2], w.data_ptr()) + ent[4:]
 

@@ -164,6 +164,40 @@ def test_conv_bias_act(K):
     assert _rel(db, dy.double().sum((0, 2, 3))) < 1e-6
 
 
+# arch 1's Conv2d layers with a bias (GLI:202-223, 260-302) at the C4 bench shapes (2B = 64):
+# FAST weight gradients, split-K and unsplit, 128 x 128 and 128 x 64 tiles
+WGRAD_BIAS = [(64, 64, 128, 16, 3, 1, 1), (64, 64, 64, 32, 4, 2, 1), (64, 256, 512, 4, 3, 1, 1),
+              (64, 128, 256, 8, 3, 1, 1), (2, 64, 128, 4, 3, 1, 1), (8, 128, 128, 32, 4, 2, 1)]
+
+
+@pytest.mark.parametrize("case", WGRAD_BIAS)
+def test_conv_wgrad_fused_bias(K, case):
+    """The bias gradient a FAST Conv2d weight-gradient GEMM forms from its staged dy tiles
+    (GemmArgs::dbias: unsplit written directly, split summed by the WGRAD reduce in split
+    order), written and accumulated, vs torch fp64 -- and the weight gradient beside it."""
+    B, cin, cout, H, k, s, p = case
+    g = K.ConvGeom(k, s, p, False)
+    torch.manual_seed(cin + cout + H)
+    x = _nhwc(torch.randn(B, cin, H, H, device=DEV))
+    Ho = (H + 2 * p - k) // s + 1
+    dy = _nhwc(torch.randn(B, cout, Ho, Ho, device=DEV))
+    w_shape = (cout, cin, k, k)
+    x64 = x.double().requires_grad_(True)
+    w64 = torch.zeros(w_shape, dtype=torch.float64, device=DEV, requires_grad=True)
+    b64 = torch.zeros(cout, dtype=torch.float64, device=DEV, requires_grad=True)
+    with torch.backends.cudnn.flags(enabled=False):
+        F.conv2d(x64, w64, b64, stride=s, padding=p).backward(dy.double())
+    dw, db = K.conv_wgrad(x, dy, g, w_shape, with_bias=True)
+    assert _rel(dw, w64.grad) < 1e-5
+    assert _rel(db, b64.grad) < 1e-6
+    # accumulation into existing gradients (autograd's second backward of heads 1-4 / WGAN-GP)
+    dw0, db0 = torch.randn_like(dw), torch.randn_like(db)
+    dwa, dba = dw0.clone(), db0.clone()
+    K.conv_wgrad(x, dy, g, w_shape, with_bias=True, out=dwa, out_bias=dba)
+    assert _rel(dwa, dw0.double() + w64.grad) < 1e-5
+    assert _rel(dba, db0.double() + b64.grad) < 1e-6
+
+
 @pytest.mark.parametrize("case", [(64, 2048, 4, "nhwc"), (3, 20, 5, "nhwc"), (5, 7, 3, "nchw"), (1, 1, 1, "nchw")])
 def test_conv_dense_one_output(K, case):
     """D's closing Conv2d(C, 1, k, 1, 0) over a k x k map (dense1 kernels): fwd with bias,
@@ -814,7 +848,7 @@ def test_pack_batch_refresh(K):
     ids = {id(p) for p in params}
     checked = 0
     for ent in list(K.PACKS.entries.values()):
-        base, w = ent[0](), ent[6]()
+        base, w = ent[0](), K.PACKS._weight(ent)
         if base is None or id(base) not in ids:
             continue
         assert ent[1] == w._version
@@ -823,6 +857,28 @@ def test_pack_batch_refresh(K):
         assert torch.equal(fresh, ent[2])
         checked += 1
     assert checked >= 17
+
+
+def test_pack_cache_keeps_views_current(K):
+    """A weight packed through a view (arch 1's dense layers run as convolutions on
+    p.view(...), GLI:186-319): the layout stays listed for the optimizer after the call
+    (layouts_of), Adam rewrites it, and the next call reuses it without a repack."""
+    from relativisticgan_amd.optim import Adam
+    torch.manual_seed(11)
+    p = torch.nn.Parameter(torch.randn(1, 512 * 16, device=DEV) * 0.02)
+    g = K.ConvGeom(4, 1, 0, False)
+    x = _nhwc(torch.randn(8, 512, 4, 4, device=DEV))
+    y0 = K.conv_fwd(x, p.view(1, 512, 4, 4), g, cache=True)
+    lay = K.PACKS.layouts_of([p])
+    assert len(lay) == 1
+    p.grad = torch.randn_like(p)
+    Adam([p], lr=1e-3, betas=(0.5, 0.999)).step()
+    ent = K.PACKS.layouts_of([p])[0][2]
+    assert ent[1] == p._version  # rewritten from the stepped values: current
+    y1 = K.conv_fwd(x, p.view(1, 512, 4, 4), g, cache=True)
+    with torch.backends.cudnn.flags(enabled=False):
+        ref = F.conv2d(x.double(), p.detach().double().view(1, 512, 4, 4))
+    assert _rel(y1, ref) < 2e-6 and not torch.equal(y0, y1)
 
 
 def test_adam_writes_packed_layouts(K):
@@ -891,7 +947,7 @@ def test_adam_writes_packed_layouts(K):
         lay = K.PACKS.layouts_of(params)
         assert len(lay) == before
         for _, _, ent in lay:
-            w = ent[6]()
+            w = K.PACKS._weight(ent)
             assert ent[1] == w._version  # current: the next conv reuses it
             fresh = torch.empty_like(ent[2])
             L.check(L.lib().rgan_conv_pack(ctypes.byref(ent[4]), ent[5], L.ptr(w), L.ptr(fresh), L.stream()), "pack")
