@@ -1,8 +1,8 @@
 // Host-side fuzz of the C-ABI (include/rgan.h) under AddressSanitizer + UBSan, CPU only.
 //
-// Built by tests/test_host_asan.py from the product's own csrc/*.hip with the host half only
-// (hipcc --cuda-host-only: no device code is compiled or launched) and -fsanitize=address,
-// undefined on the host.  What runs is every host-side planner / validator the entry points
+// Built by tests/test_host_asan.py from the product's own csrc/*.hip with -fsanitize=address,
+// undefined on the host half only (hipcc -Xarch_host; the device half is compiled normally and
+// never launched).  What runs is every host-side planner / validator the entry points
 // reach before a launch: descriptor checks (desc_ok), the GEMM planners (plan_fwd / dgrad /
 // wgrad, choose_tiling, set_fast, the narrow / dense / 3x3 planners), workspace / pack / BN
 // segment sizing, and the RGAN_EINVAL paths of the compute entry points.  No call here may
