@@ -50,7 +50,10 @@ direct error, the envelope errors when used, and whether a flip relaxed it.
   Parameters after Adam: max|p_gpu - p_exact| <= 2.02 x the largest update the exact or
   the oracle step makes in the tensor (Adam's first steps are sign steps, so a near-zero
   gradient may flip: 2*lr at step 1) and at most max(1%, 2x the oracle's own share + 0.5%) of elements off by more
-  than 1e-6.
+  than 1e-6.  Where a mask-forced step exists, the post-Adam parameters are measured against
+  it as well and the closer of the two counts (as for gradients: after a flip the GPU's
+  gradient is the forced step's, and Adam's sign steps turn every near-zero gradient element
+  the flip moved into a full-size parameter difference from the exact step).
 """
 import copy
 import json
@@ -434,6 +437,13 @@ def compare(p, st, got, exact, report, reach=frozenset(), forced=None):
                 continue
             d = (g.double() - x.double()).abs()
             dref = (o.double() - x.double()).abs()
+            xf = _lookup(forced, f"{label}.{k}") if forced is not None else None
+            frac_f = None
+            if xf is not None:  # the GPU's own branches, computed exactly, then the same Adam step
+                df = (g.double() - xf.double()).abs()
+                frac_f = (df > 1e-6).double().mean().item()
+                if frac_f < (d > 1e-6).double().mean().item():
+                    d = df
             # a sign-flipped Adam update moves an element by at most 2x the largest update
             # made in this tensor (2*lr at step 1); for biases feeding BN the exact update is
             # 0 while the oracle's own fp32 step moves them by +-lr, so both count
@@ -444,7 +454,8 @@ def compare(p, st, got, exact, report, reach=frozenset(), forced=None):
                 errs.append(f"{label}.{k}: max|dp| {d.max().item():.3e} > {bound:.3e}")
             frac, fref = (d > 1e-6).double().mean().item(), (dref > 1e-6).double().mean().item()
             report.append({"tensor": f"it{i}.{label}.{k}", "adam_max_dp": d.max().item(), "adam_bound": bound,
-                           "frac_off": frac, "oracle_frac_off": fref, "flip_reachable": f"{label}.{k}" in reach})
+                           "frac_off": frac, "oracle_frac_off": fref, "frac_off_vs_forced": frac_f,
+                           "flip_reachable": f"{label}.{k}" in reach})
             if frac > max(0.05 if f"{label}.{k}" in reach else 0.01, 2 * fref + 0.005):
                 errs.append(f"{label}.{k}: {frac:.2%} of elements off by >1e-6 (oracle fp32: {fref:.2%})")
     for k, o in st["postD_G"].items():  # D buffers after the G step (BN stats / spectral u,v move there too)
