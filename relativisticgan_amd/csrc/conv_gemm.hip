@@ -187,7 +187,8 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   // stages (83 KB) left one resident block per CU; one stage (41.5 KB) gives three.  The
   // 128x64 tile (CFG_M) likewise (two -> five blocks; C3h32 -1.6 %, C1 / C4 unchanged).  The
   // 128x128 tile keeps two stages (single-buffered it lost 9 %: its vector epilogue needs the
-  // LDS, and two blocks per CU already hide the one barrier)
+  // LDS, and two blocks per CU already hide the one barrier).  The 64x64 tile (CFG_S: small
+  // forward / data-gradient GEMMs, one 32x32 accumulator per wave) keeps two stages (36 KB)
   constexpr bool GEMM_SB = !EMU && ((BM == 256 && BN == 32) || (BM == 128 && BN == 64));
   constexpr int EPI_SZ = KROW ? 4 * (GEMM_SB ? 32 : 64) * 72 : 0;  // vector epilogue staging (4 waves x rows x 72)
   // EMU: one (single-buffered) stage of six bf16 planes (A hi/mid/lo, B hi/mid/lo), rows of
@@ -2740,7 +2741,7 @@ __device__ __forceinline__ void adam_pack_flat(const AdamPackBatch& b, const Ada
 }
 
 // ---------------------------------------------------------------- host planning
-enum { CFG_L = 0, CFG_M = 1, CFG_N = 2 };
+enum { CFG_L = 0, CFG_M = 1, CFG_N = 2, CFG_S = 3 };
 
 struct Plan {
   int mode = MODE_CONV;
@@ -2776,8 +2777,8 @@ struct Plan {
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 static void tile_dims(int cfg, int& bm, int& bn) {
-  bm = cfg == CFG_N ? 256 : 128;
-  bn = cfg == CFG_L ? 128 : (cfg == CFG_M ? 64 : 32);
+  bm = cfg == CFG_N ? 256 : (cfg == CFG_S ? 64 : 128);
+  bn = cfg == CFG_L ? 128 : (cfg == CFG_M || cfg == CFG_S ? 64 : 32);
 }
 
 // fewest k steps (of BK) per split (round-4 A/B against 2 / 8 / 16: profiles/round4_split_planner_ab.txt)
@@ -2787,24 +2788,32 @@ constexpr int SPLIT_MINK = 4;
 static std::atomic<int> g_emu{0};
 static bool emu_bf16x6() { return g_emu.load(std::memory_order_relaxed) == 1; }
 
-// below SMALL_GEMM_FLOPS, 128 x 64 tiles instead of a >= SMALL_SPLITS-way split of 128 x 128
-// ones, weight gradients included (C4 3.93 -> 3.85 ms/step, run r4v)
+// below SMALL_GEMM_FLOPS, smaller tiles instead of a >= SMALL_SPLITS-way split of 128 x 128
+// ones: 64 x 64 for the forward / data gradients (round 5: four times the tiles, a quarter of
+// the splits, half the slab bytes per output; C4 3.74 -> 3.53 ms/step, run r5q), 128 x 64 for
+// the weight gradients (C4 3.93 -> 3.85 ms/step, run r4v)
 constexpr double SMALL_GEMM_FLOPS = 4e9;
 constexpr int SMALL_SPLITS = 4;
 
 static void choose_tiling(Plan& p) {
   GemmArgs& g = p.g;
   p.cfg = g.N <= 32 ? CFG_N : (g.N <= 64 ? CFG_M : CFG_L);
+  // small forward / data-gradient GEMMs with N <= 64: 64 x 64 tiles, twice the tiles of
+  // 128 x 64 and half its splits (C4 3.535 -> 3.43 ms/step, run r5r; weight gradients stay
+  // on 128 x 64: 3.535 -> 3.55 with them moved too)
+  if (p.cfg == CFG_M && p.mode != MODE_WGRAD && 2.0 * g.M * g.N * g.K * p.phases < SMALL_GEMM_FLOPS && !emu_bf16x6())
+    p.cfg = CFG_S;
   if (p.cfg == CFG_L) {
     const long long t = (long long)ceil_div(g.M, 128) * ceil_div(g.N, 128) * p.phases;
     const int nk = ceil_div(g.K, BK);
-    // small GEMMs (arch 1 at 32x32: 0.1-1.5 GFLOP) that would split K 4+ ways: twice the
-    // tiles, a quarter of the splits and their reduce (C4 4.03 -> 3.92 ms/step, run r4t);
-    // at C1's 8.6-GFLOP GEMMs the same swap loses (round-4 run r4c)
+    // small GEMMs (arch 1 at 32x32: 0.1-1.5 GFLOP) that would split K 4+ ways: more tiles,
+    // fewer splits and less reduce (128 x 64: C4 4.03 -> 3.92 ms/step, run r4t; 64 x 64 for
+    // CONV / CONVT2: 3.74 -> 3.53, run r5q); at C1's 8.6-GFLOP GEMMs the same swap loses
+    // (round-4 run r4c)
     const double flops = 2.0 * g.M * g.N * g.K * p.phases;
     // (not under the bf16x6 emulation, whose kernels are 128 x 128)
     if (flops < SMALL_GEMM_FLOPS && t * SMALL_SPLITS <= SPLIT_TARGET && nk >= 4 * SMALL_SPLITS && !emu_bf16x6())
-      p.cfg = CFG_M;
+      p.cfg = p.mode == MODE_WGRAD ? CFG_M : CFG_S;
   }
   int bm, bn;
   tile_dims(p.cfg, bm, bn);
@@ -3363,6 +3372,9 @@ static void launch_mode(const Plan& p, dim3 grid, hipStream_t s) {
   switch (p.cfg) {
     case CFG_L: launch_cfg<MODE, 128, 128, 2, 2>(p, grid, s); break;
     case CFG_M: launch_cfg<MODE, 128, 64, 2, 2>(p, grid, s); break;
+    case CFG_S:
+      if constexpr (MODE != MODE_WGRAD) launch_cfg<MODE, 64, 64, 2, 2>(p, grid, s);
+      break;
     default: launch_cfg<MODE, 256, 32, 4, 1>(p, grid, s); break;
   }
 }
@@ -3384,9 +3396,13 @@ static std::vector<ProfRec> g_recs;
 static std::vector<std::string> g_kernel_names;
 static double g_cur_flops = 0.0;
 
-constexpr int N_KERNEL_IDS = 59;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in + 2 bf16x6 + 2 post + 2 post bf16x6 + 2 narrow 3x3
+constexpr int N_KERNEL_IDS = 74;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in + 2 bf16x6 + 2 post + 2 post bf16x6 + 2 narrow 3x3 + 12 (mode, av, bv) + 3 FAST (mode) of the 64x64 tile
 
 static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
+  if (cfg == CFG_S && mode <= MODE_WGRAD) {
+    kernel_id(MODE_NARROW_T, 0, false, false);  // fills the name table
+    return fast ? 71 + mode : 59 + mode * 4 + (av ? 2 : 0) + (bv ? 1 : 0);
+  }
   const int id = mode == MODE_NARROW_T ? 45
                  : mode == MODE_NARROW_IN ? 46
                  : mode == MODE_DENSE1 ? 47 + cfg
@@ -3427,6 +3443,18 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
     g_kernel_names[56] = "void rgan::gemm_post_bf16x6<1>(rgan::GemmArgs)";
     g_kernel_names[57] = "void rgan::conv3_narrow_out<NC>(rgan::NarrowArgs)";
     g_kernel_names[58] = "void rgan::wgrad3_narrow<NC>(rgan::NarrowArgs, int, int)";
+    for (int m = 0; m < 3; ++m) {
+      for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {
+          char buf[160];
+          snprintf(buf, sizeof(buf), "void rgan::gemm_kernel<%d, 64, 64, 2, 2, %s, %s, false>(rgan::GemmArgs)", m,
+                   a ? "true" : "false", b ? "true" : "false");
+          g_kernel_names[59 + m * 4 + a * 2 + b] = buf;
+        }
+      char buf[160];
+      snprintf(buf, sizeof(buf), "void rgan::gemm_kernel<%d, 64, 64, 2, 2, true, true, true>(rgan::GemmArgs)", m);
+      g_kernel_names[71 + m] = buf;
+    }
   }
   return id;
 }

@@ -86,11 +86,13 @@ def test_conv_fwd_dgrad_wgrad_small(K, case, layout):
 
 
 @pytest.mark.parametrize("case", [(32, 128, 128, 16, 4, 2, 1, False), (32, 256, 128, 8, 4, 2, 1, True),
-                                  (32, 128, 256, 8, 3, 1, 1, False)])
+                                  (32, 128, 256, 8, 3, 1, 1, False), (32, 64, 64, 32, 4, 2, 1, False),
+                                  (32, 128, 64, 8, 4, 2, 1, True)])
 def test_small_gemm_tiles(K, case):
-    """Arch 1's small GEMMs (< 4 GFLOP that would split K 4+ ways on 128x128 tiles) run on
-    128x64 tiles with fewer splits (conv_gemm.hip choose_tiling): forward, data and weight
-    gradients vs torch fp64, and the 128x64 kernels are the ones that ran."""
+    """Arch 1's small GEMMs (< 4 GFLOP that would split K 4+ ways on 128x128 tiles, or with
+    N <= 64) run on smaller tiles with fewer splits (conv_gemm.hip choose_tiling): the forward
+    and data gradient on 64x64 tiles, the weight gradient on 128x64 -- vs torch fp64, and those
+    kernels are the ones that ran."""
     B, cin, cout, H, k, s, p, tr = case
     g = K.ConvGeom(k, s, p, tr)
     torch.manual_seed(3)
@@ -110,8 +112,8 @@ def test_small_gemm_tiles(K, case):
     y, fwd = gemm_names(lambda: K.conv_fwd(x, w, g))
     dx = K.conv_dgrad(dy, w, g, x.shape, like=x)  # tiling depends on its own K (not asserted)
     (dw, _), wgr = gemm_names(lambda: K.conv_wgrad(x, dy, g, tuple(w.shape)))
-    for names in (fwd, wgr):
-        assert len(names) == 1 and "128, 64, 2, 2" in names[0], names
+    assert len(fwd) == 1 and "64, 64, 2, 2" in fwd[0], fwd
+    assert len(wgr) == 1 and "128, 64, 2, 2" in wgr[0], wgr
     assert _rel(y, out64.detach()) < 2e-6
     assert _rel(dx, x64.grad) < 2e-6
     assert _rel(dw, w64.grad) < 2e-6
