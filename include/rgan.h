@@ -26,8 +26,9 @@ extern "C" {
 #define RGAN_EINVAL 1001
 
 /* ABI revision.  2: rgan_adam_packed takes step = device float[2] (step[1] is the
- * call's uint32 arrival ticket, zero before the first call); revision 1 took float[1]. */
-#define RGAN_ABI_VERSION 2
+ * call's uint32 arrival ticket, zero before the first call); revision 1 took float[1].
+ * 3: adds rgan_conv_wgrad_rows. */
+#define RGAN_ABI_VERSION 3
 
 /* Activation codes fused into epilogues (GLI:345,370,388,417,437,450; SELU GLI:338). */
 enum {
@@ -155,6 +156,12 @@ int rgan_g1_wgrad(const float* z, int B, int Cin, const float* dy, int Cout, flo
  * instead of a separate add pass). */
 int rgan_conv_wgrad(const RganConv* d, const float* x, const float* dy, float* dw, float* dbias,
                     int accumulate, void* ws, size_t ws_bytes, void* stream);
+/* The same with dbias summed over the pixel rows p >= dbias_row0 only (p = (b, h, w) in
+ * order; 0 <= dbias_row0 < batch*hout*wout): the WGAN-GP double backward's weight gradient
+ * runs one GEMM over [adjoint; forward] row pairs while the bias gradient is the forward
+ * half's alone.  rgan_conv_wgrad(...) == rgan_conv_wgrad_rows(..., 0, ...). */
+int rgan_conv_wgrad_rows(const RganConv* d, const float* x, const float* dy, float* dw, float* dbias,
+                         long long dbias_row0, int accumulate, void* ws, size_t ws_bytes, void* stream);
 
 /* ---- --NN_conv blocks: Upsample(scale_factor=2, nearest) + Conv2d(k3, s1, p1) ----
  * (GLI:351-356 middle, GLI:377-382 end).  conv3x3(up2(x), W) equals a k4 s2 p1

@@ -67,6 +67,8 @@ _SIGS = {
     "rgan_g1_wgrad": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp]),
     "rgan_conv_dgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_sz, c_vp]),
     "rgan_conv_wgrad": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_sz, c_vp]),
+    "rgan_conv_wgrad_rows": (c_int, [ctypes.POINTER(RganConv), c_vp, c_vp, c_vp, c_vp, ctypes.c_longlong, c_int, c_vp,
+                                     c_sz, c_vp]),
     "rgan_nn_fold_weight": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
     "rgan_patches_k4s2": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "rgan_patch_weight": (c_int, [c_vp, c_int, c_int, c_ll, c_ll, c_vp, c_vp]),

@@ -102,6 +102,7 @@ struct GemmArgs {
   double* dbp;
   float* dbias;
   int db_accum;
+  int db_k0;              // first pixel row summed into dbias (a multiple of BK; rgan_conv_wgrad_rows)
   // Post-op for the layer that PRODUCED this GEMM's output operand (rgan_conv_post: a data
   // gradient, or G's image-layer gradient GEMM), applied where the value is final (unsplit
   // epilogue or split-K reduce); px has C's layout (host-checked):
@@ -315,6 +316,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
   int aoff[FAST ? FA_N : 1], boff[FAST ? FB_N : 1];
   int f_tap = 0, f_c0 = 0, f_cin = 1, w_tab = 0;
   int w_ntap = 1, w_tq = 0, w_qb = 0;  // WGRAD FAST: taps per n tile; this thread's tap, channel byte offset
+  int st_k0 = 0;                        // WGRAD FAST: first pixel row of the tile in the staging registers
   if constexpr (FAST) {
     if constexpr (MODE != MODE_WGRAD) {
       // packed weights [N][K]: rows n = n0 + (tid>>3) + 32i, k quad tid&7 (like A)
@@ -410,6 +412,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
         rb[4 * i + 2] = __uint_as_float(v.z); rb[4 * i + 3] = __uint_as_float(v.w);
       }
     } else if constexpr (FAST) {
+      st_k0 = k0;
       const int so = k0 * (int)g.a.sw * 4;
 #pragma unroll
       for (int i = 0; i < FA_N; ++i) {
@@ -593,7 +596,7 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
     float* As = smem + buf * STAGE;
     float* Bs = As + A_SZ;
     if constexpr (SWZ) {
-      if (db_on) {
+      if (db_on && st_k0 >= g.db_k0) {  // tile-uniform: db_k0 is a multiple of BK
 #pragma unroll
         for (int i = 0; i < FA_N; ++i)
 #pragma unroll
@@ -4103,6 +4106,11 @@ extern "C" int rgan_conv_post(const RganConv* d, int which, const float* in, con
 
 extern "C" int rgan_conv_wgrad(const RganConv* d, const float* x, const float* dy, float* dw,
                                float* dbias, int accumulate, void* ws, size_t ws_bytes, void* stream) {
+  return rgan_conv_wgrad_rows(d, x, dy, dw, dbias, 0, accumulate, ws, ws_bytes, stream);
+}
+
+extern "C" int rgan_conv_wgrad_rows(const RganConv* d, const float* x, const float* dy, float* dw, float* dbias,
+                                    long long dbias_row0, int accumulate, void* ws, size_t ws_bytes, void* stream) {
   if (!x || !dy || !dw) return RGAN_EINVAL;
   g_cur_flops = conv_flops(d);
   Plan p;
@@ -4111,11 +4119,12 @@ extern "C" int rgan_conv_wgrad(const RganConv* d, const float* x, const float* d
   p.g.accum = accumulate ? 1 : 0;
   p.da.accum = p.g.accum;
   const size_t plan_bytes = align_up(plan_ws_bytes(p), 256);
-  // per-output-channel sum of dy (Conv2d and ConvTranspose2d alike: dy has cout channels),
-  // checked before anything is launched
+  // per-output-channel sum of dy over pixel rows [dbias_row0, P) (Conv2d and ConvTranspose2d
+  // alike: dy has cout channels), checked before anything is launched
   const long long P = (long long)d->batch * d->hout * d->wout;
   long long sp = 0;
   if (dbias) {
+    if (dbias_row0 < 0 || dbias_row0 >= P) return RGAN_EINVAL;
     if ((long long)d->hout * d->wout == 1) {
       sp = d->ys[0];
     } else {
@@ -4124,22 +4133,26 @@ extern "C" int rgan_conv_wgrad(const RganConv* d, const float* x, const float* d
         return RGAN_EINVAL;
       sp = d->cout;
     }
-    const size_t need = plan_bytes + rgan_bn_partial_bytes(P, d->cout);
+    const size_t need = plan_bytes + rgan_bn_partial_bytes(P - dbias_row0, d->cout);
     if (!ws || ws_bytes < need) return RGAN_EINVAL;
   }
   // a FAST Conv2d weight gradient stages dy as its A operand: the GEMM sums the bias
-  // gradient from those tiles (GemmArgs::dbias) instead of a channel-sum pass over dy
+  // gradient from those tiles (GemmArgs::dbias, from the BK-aligned pixel row db_k0 on)
+  // instead of a channel-sum pass over dy
   const bool bias_fused = dbias && p.mode == MODE_WGRAD && p.fast && !d->transposed && ws_bytes >= plan_bytes &&
+                          dbias_row0 % BK == 0 && dbias_row0 <= (long long)INT32_MAX &&
                           (p.g.splits == 1 || (size_t)p.g.splits * p.g.M * sizeof(double) <= ws_bytes - plan_bytes);
   if (bias_fused) {
     p.g.dbias = dbias;
     p.g.db_accum = accumulate ? 1 : 0;
+    p.g.db_k0 = (int)dbias_row0;
     p.g.dbp = p.g.splits > 1 ? reinterpret_cast<double*>((char*)ws + plan_bytes) : nullptr;
   }
   rc = run_plan(p, ws, ws_bytes, (hipStream_t)stream);
   if (rc) return rc;
   if (dbias && !bias_fused)
-    return rgan_channel_sum(dy, P, d->cout, sp, d->ys[1], dbias, accumulate, (char*)ws + plan_bytes, stream);
+    return rgan_channel_sum(dy + dbias_row0 * sp, P - dbias_row0, d->cout, sp, d->ys[1], dbias, accumulate,
+                            (char*)ws + plan_bytes, stream);
   return 0;
 }
 

@@ -261,6 +261,13 @@ class GPEngine:
         gw = _grad_buf(r.wparam)
         gw = gw.view(*r.layer.w_view) if r.layer.w_view is not None else gw
         sn = r.sn
+        bias_on = r.bias is not None and ybar is not None
+        if sn is None and bias_on and not AG.ConvLayerFn._patch_conv(spec, r.h_in):
+            # bias += sum(ybar): the forward half's rows of the pair -- summed by the weight
+            # gradient GEMM itself from the staged rows >= B * Ho * Wo (rgan_conv_wgrad_rows)
+            K.conv_wgrad(X, Y, spec.geom, tuple(r.w.shape), out=gw, with_bias=True, out_bias=_grad_buf(r.bias),
+                         bias_row0=B * Y.shape[2] * Y.shape[3])
+            return
         if AG.ConvLayerFn._patch_conv(spec, r.h_in):
             g1, _ = K.conv_wgrad(K.patches_k4s2(X), Y, K.G1X1, (r.w.shape[0], 64, 1, 1))
             if sn is None:

@@ -485,11 +485,12 @@ def g1_wgrad(x, dy, w_shape, out=None, into=None):
     return dw
 
 
-def conv_wgrad(x, dy, geom, w_shape, with_bias=False, out=None, out_bias=None, into=None):
+def conv_wgrad(x, dy, geom, w_shape, with_bias=False, out=None, out_bias=None, into=None, bias_row0=0):
     """(dw in torch layout, dbias or None).  ``out`` / ``out_bias`` given: the gradients are
     ADDED into them in the GEMM epilogue (autograd accumulation without an add pass);
     ``into``: dw is WRITTEN into that tensor (e.g. its slice of a data-parallel gradient
-    bucket, dp.grad_view) instead of a new one."""
+    bucket, dp.grad_view) instead of a new one.  ``bias_row0``: dbias sums dy's pixel rows
+    (b, h, w) from that one on (rgan_conv_wgrad_rows: the GP engine's [adjoint; forward] pairs)."""
     L.require_cuda(x, dy)
     _f32(x, dy)
     if into is not None:
@@ -502,7 +503,7 @@ def conv_wgrad(x, dy, geom, w_shape, with_bias=False, out=None, out_bias=None, i
         if out is not None:
             raise L.RganError("accumulating NN_conv weight gradients is not supported")
         cout, cin = w_shape[0], w_shape[1]
-        dwt, db = conv_wgrad(x, dy, NN_T, (cin, cout, 4, 4), with_bias=with_bias)
+        dwt, db = conv_wgrad(x, dy, NN_T, (cin, cout, 4, 4), with_bias=with_bias, bias_row0=bias_row0)
         return nn_unfold_grad(dwt, tuple(w_shape)), db
     acc = out is not None
     if acc and (tuple(out.shape) != tuple(w_shape) or not out.is_contiguous()):
@@ -521,8 +522,8 @@ def conv_wgrad(x, dy, geom, w_shape, with_bias=False, out=None, out_bias=None, i
     if nbytes == 0:
         raise L.RganError(f"unsupported conv wgrad {geom} for {tuple(x.shape)}")
     ws = L.workspace(nbytes, x.device)
-    L.check(lib.rgan_conv_wgrad(ctypes.byref(d), L.ptr(x), L.ptr(dy), L.ptr(dw), L.ptr(db), int(acc), L.ptr(ws),
-                                ws.numel(), L.stream()), "rgan_conv_wgrad")
+    L.check(lib.rgan_conv_wgrad_rows(ctypes.byref(d), L.ptr(x), L.ptr(dy), L.ptr(dw), L.ptr(db), int(bias_row0),
+                                     int(acc), L.ptr(ws), ws.numel(), L.stream()), "rgan_conv_wgrad_rows")
     return dw, db
 
 

@@ -198,6 +198,15 @@ def test_conv_wgrad_fused_bias(K, case):
     K.conv_wgrad(x, dy, g, w_shape, with_bias=True, out=dwa, out_bias=dba)
     assert _rel(dwa, dw0.double() + w64.grad) < 1e-5
     assert _rel(dba, db0.double() + b64.grad) < 1e-6
+    # bias over the second half of the batch only (rgan_conv_wgrad_rows: the GP engine's
+    # [adjoint; forward] pairs), fused where the row offset is tile-aligned, else the
+    # channel-sum fallback; the weight gradient still over every row
+    if B >= 2:
+        row0 = (B // 2) * Ho * Ho
+        dwr, dbr = dw0.clone(), db0.clone()
+        K.conv_wgrad(x, dy, g, w_shape, with_bias=True, out=dwr, out_bias=dbr, bias_row0=row0)
+        assert _rel(dwr, dw0.double() + w64.grad) < 1e-5
+        assert _rel(dbr, db0.double() + dy[B // 2:].double().sum((0, 2, 3))) < 1e-6
 
 
 @pytest.mark.parametrize("case", [(64, 2048, 4, "nhwc"), (3, 20, 5, "nhwc"), (5, 7, 3, "nchw"), (1, 1, 1, "nchw")])
