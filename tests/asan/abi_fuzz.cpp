@@ -150,6 +150,9 @@ static void malformed_compute(Rng& r, const RganConv& good) {
   expect_einval(rgan_conv_dgrad(&bad, p, p, nullptr, nullptr, p, ws, sizeof ws, nullptr), "conv_dgrad bad desc");
   expect_einval(rgan_conv_wgrad(d, nullptr, p, p, nullptr, 0, ws, sizeof ws, nullptr), "conv_wgrad x=0");
   expect_einval(rgan_conv_wgrad(&bad, p, p, p, nullptr, 0, ws, sizeof ws, nullptr), "conv_wgrad bad desc");
+  expect_einval(rgan_conv_wgrad_rows(d, p, p, p, p, -1, 0, ws, sizeof ws, nullptr), "conv_wgrad_rows row0<0");
+  expect_einval(rgan_conv_wgrad_rows(d, p, p, p, p, 1LL << 40, 0, ws, sizeof ws, nullptr), "conv_wgrad_rows row0>=P");
+  expect_einval(rgan_conv_wgrad_rows(d, nullptr, p, p, p, 0, 0, ws, sizeof ws, nullptr), "conv_wgrad_rows x=0");
   expect_einval(rgan_conv_post(d, 2, p, p, nullptr, nullptr, p, ws, sizeof ws, &post, &fused, nullptr), "conv_post which=2");
   post.mode = 3; post.x = p;
   expect_einval(rgan_conv_post(d, 1, p, p, nullptr, nullptr, p, ws, sizeof ws, &post, &fused, nullptr), "conv_post mode=3");
