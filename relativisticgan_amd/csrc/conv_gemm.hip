@@ -2793,8 +2793,10 @@ static bool emu_bf16x6() { return g_emu.load(std::memory_order_relaxed) == 1; }
 
 // below SMALL_GEMM_FLOPS, smaller tiles instead of a >= SMALL_SPLITS-way split of 128 x 128
 // ones: 64 x 64 for the forward / data gradients (round 5: four times the tiles, a quarter of
-// the splits, half the slab bytes per output; C4 3.74 -> 3.53 ms/step, run r5q), 128 x 64 for
-// the weight gradients (C4 3.93 -> 3.85 ms/step, run r4v)
+// the splits, half the slab bytes per output; C4 3.74 -> 3.53 ms/step, run r5q) and for the
+// weight gradients of <= 64 output channels (whose 128-row tiles were half empty: C4 9339 /
+// 9357 -> 9427 / 9443 img/s, run r5aa), 128 x 64 for the other weight gradients (C4 3.93 ->
+// 3.85 ms/step, run r4v; on 64 x 64 they measured slower, run r5r)
 constexpr double SMALL_GEMM_FLOPS = 4e9;
 constexpr int SMALL_SPLITS = 4;
 
@@ -2816,7 +2818,7 @@ static void choose_tiling(Plan& p) {
     const double flops = 2.0 * g.M * g.N * g.K * p.phases;
     // (not under the bf16x6 emulation, whose kernels are 128 x 128)
     if (flops < SMALL_GEMM_FLOPS && t * SMALL_SPLITS <= SPLIT_TARGET && nk >= 4 * SMALL_SPLITS && !emu_bf16x6())
-      p.cfg = p.mode == MODE_WGRAD ? CFG_M : CFG_S;
+      p.cfg = p.mode == MODE_WGRAD && g.M > 64 ? CFG_M : CFG_S;
   }
   int bm, bn;
   tile_dims(p.cfg, bm, bn);
@@ -3375,9 +3377,7 @@ static void launch_mode(const Plan& p, dim3 grid, hipStream_t s) {
   switch (p.cfg) {
     case CFG_L: launch_cfg<MODE, 128, 128, 2, 2>(p, grid, s); break;
     case CFG_M: launch_cfg<MODE, 128, 64, 2, 2>(p, grid, s); break;
-    case CFG_S:
-      if constexpr (MODE != MODE_WGRAD) launch_cfg<MODE, 64, 64, 2, 2>(p, grid, s);
-      break;
+    case CFG_S: launch_cfg<MODE, 64, 64, 2, 2>(p, grid, s); break;
     default: launch_cfg<MODE, 256, 32, 4, 1>(p, grid, s); break;
   }
 }
