@@ -22,9 +22,13 @@ Prints ONE JSON line (rank 0).  Extra fields:
                   a bounded sample of the same workload on this host (rank 0, N=1); C1's
                   own (>= 5 timed iterations) under extra_workloads.C1;
   dp_path_n1   -- (N=1) the workload (and C1) run exactly as each rank of an N>1 run does
-                  (separate D(x) / D(x_fake) passes, eager launches): the like-for-like
-                  baseline of the scaling runs.
-Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 under torch.distributed.run.
+                  (launch mode of the data-parallel path: eager above 50M parameters,
+                  piecewise graphs below): the like-for-like baseline of the scaling runs.
+Launch: python bench.py [--gpus N --steps K --warmup W].  N>1: either under
+``torch.distributed.run --nproc-per-node N`` (WORLD_SIZE must equal N), or plain
+``python bench.py --gpus N``, which starts the N ranks itself (torch.distributed.run as a
+child process, before anything touches the GPU) and relays rank 0's line (the
+reference's --n_gpu N, GLI:40, 393-394, 455-456).
 """
 import argparse
 import json
@@ -180,9 +184,9 @@ def restatement_check():
 def run_workload(name, steps, warmup, world, args, K, emu=False, dp_path=False, host_rng=False):
     """Train `steps` timed iterations of workload `name` (after `warmup`); returns the
     measurement (max over ranks).  emu: forward / data-gradient GEMMs on bf16x6.  dp_path:
-    run one process exactly as every rank of an N > 1 run does (separate D(x) / D(x_fake)
-    passes, eager launches, no HIP graph) -- the like-for-like N = 1 baseline of the scaling
-    runs.  host_rng: batches and z drawn on the host in the reference's order (numpy choice,
+    run one process in the launch mode every rank of an N > 1 run uses (eager above 50M
+    parameters, piecewise graphs below; batched D pass as at N = 1) -- the like-for-like
+    N = 1 baseline of the scaling runs.  host_rng: batches and z drawn on the host in the reference's order (numpy choice,
     torch CPU generator, seed 1: SURVEY §8(d) -- the oracle's exact draws), eager launches
     (a graph replay would repeat its capture's draws)."""
     prev_emu = K.set_gemm_emulation(emu)
@@ -197,7 +201,7 @@ def _run_workload(name, steps, warmup, world, args, K, dp_path=False, host_rng=F
     from relativisticgan_amd.train import Trainer, synthetic_images
     loss_D, size, bpg, h = WORKLOADS[name]
     spectral = name == "C5"
-    bd = False if dp_path else {"auto": None, "on": True, "off": False}[args.batch_d]
+    bd = {"auto": None, "on": True, "off": False}[args.batch_d]
     p = make_param(loss_D=loss_D, image_size=size, batch_size=bpg * world, G_h_size=h, D_h_size=h, seed=1,
                    print_every=10 ** 9, spectral=spectral, rgan_rng="host" if host_rng else "device",
                    arch=ARCH.get(name, 0), rgan_batch_D=bd)
@@ -223,10 +227,6 @@ def _run_workload(name, steps, warmup, world, args, K, dp_path=False, host_rng=F
     else:
         mode = args.graph if args.graph == "piecewise" else "eager"
     use_graph = mode in ("graph", "piecewise")
-    if mode == "piecewise" and bd is None or (dp_path and mode == "piecewise"):
-        # nothing to overlap with a deferred G step inside graphs: D(x) and D(x_fake) run as
-        # one batched pass, as on one GPU
-        t.batch_D = t.pac == 1 and t.D.segmentable
     # graph mode runs every iteration on one side stream: autograd's per-parameter
     # AccumulateGrad nodes keep the stream of the first backward, and the captured backward
     # must accumulate on the capturing stream
@@ -414,6 +414,32 @@ def describe(res):
             f"{', gradient penalty' if res['loss_D'] == 3 else ''}")
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, backend):
+    """``python bench.py --gpus N`` without a launcher: run this script as N ranks under
+    ``torch.distributed.run`` in a CHILD process (this process has not initialised the GPU
+    and never replaces itself), stream the ranks' output through, and return the launcher's
+    exit status (non-zero if any rank failed).  Rank 0 prints the JSON line."""
+    import subprocess
+    if backend == "nccl":
+        have = torch.cuda.device_count()  # counts devices without initialising HIP (this image)
+        if have < n:
+            print(f"bench.py: --gpus {n} over RCCL but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver
+    env["RGAN_BENCH_LAUNCHER"] = "bench.py --gpus (torch.distributed.run child)"
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -423,8 +449,8 @@ def main():
     ap.add_argument("--extra", default=",".join(EXTRA_WORKLOADS),
                     help="comma-separated workloads also measured on one GPU (extra_workloads); '' = none")
     ap.add_argument("--batch-d", default="auto", choices=("auto", "on", "off"),
-                    help="D(x), D(x_fake) as one batched pass (auto: on for 1 process, off under DP -- "
-                         "'off' at N=1 is the like-for-like baseline of the N>1 runs)")
+                    help="D(x), D(x_fake) as one batched pass (auto = on, also under DP; off = the "
+                         "reference's separate D(x) / D(x_fake) calls)")
     ap.add_argument("--graph", default="auto", choices=("auto", "on", "off", "piecewise"),
                     help="time replays of one iteration captured as a HIP graph (one process) or as graphs "
                          "cut at the collectives (piecewise, DP); auto: graph at N=1, under DP piecewise "
@@ -445,12 +471,23 @@ def main():
                          "the second communicator) even with one rank: a one-GPU rehearsal of the N > 1 "
                          "collectives over RCCL (RGAN_BENCH_BACKEND, default nccl)")
     args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {args.gpus}: need at least one GPU")
     # RGAN_BENCH_BACKEND=gloo + more ranks than GPUs: rehearsal of the N>1 path on one GPU
     backend = os.environ.get("RGAN_BENCH_BACKEND", "nccl")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # plain `python bench.py --gpus N`: this process never touches the GPU; it starts the
+        # N ranks and relays their output
+        sys.exit(launch_ranks(args.gpus, backend))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        # the reference's --n_gpu N is N devices under one data_parallel (GLI:40, 455-456);
+        # here one process per GPU: a mismatch would time the wrong job
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch with "
+                         f"torch.distributed.run --nproc-per-node {args.gpus}, or without a launcher "
+                         "(bench.py starts the ranks itself)")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     if backend != "nccl":
         local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
@@ -467,6 +504,11 @@ def main():
         else:
             dist.init_process_group(backend)
         dp.setup(sync_bn=args.sync_bn, force=args.force_dp)
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
+    pg = ({"backend": str(torch.distributed.get_backend()), "world_size": torch.distributed.get_world_size(),
+           "launcher": os.environ.get("RGAN_BENCH_LAUNCHER", "external (torch.distributed.run)")}
+          if distributed else None)
     res = run_workload(args.workload, args.steps, args.warmup, world, args, K)
     emu_res = None
     if world == 1 and not args.no_emu_extra:
@@ -509,7 +551,7 @@ def main():
                    "batched_D_step": res["batch_D"], "hip_graph": res["graph"], "launch_mode": res["mode"],
                    "graph_segments": res["segments"],
                    "batchnorm": "SyncBN" if args.sync_bn else "per-shard (reference DataParallel)",
-                   "forced_dp": bool(args.force_dp)},
+                   "forced_dp": bool(args.force_dp), "process_group": pg},
         "step_mfma_util": res["flops_iter"] * args.steps / res["elapsed"] / (world * FP32_MFMA_PEAK),
         "conv_tflop_per_step": res["flops_iter"] / 1e12,
         "roofline": roofline_of(res, args.workload),

@@ -62,7 +62,7 @@ def make_parser(script="GAN_losses_iter"):
     p.add_argument("--rgan_sync_bn", type="bool", default=False)
     p.add_argument("--rgan_batch_D", type="bool", default=None,
                    help="run the D step's D(x) and D(x_fake) as one batched pass (per-call BN kept); "
-                        "default: on for 1 process, off under data parallelism")
+                        "default: on (one process and data parallel)")
     p.add_argument("--rgan_batch_G", type="bool", default=None,
                    help="run the G step's D(G(z)) and D(x) (heads 5-8) as one batched pass (per-call BN "
                         "kept, gradient through the D(G(z)) half only); default: on")

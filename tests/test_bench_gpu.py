@@ -78,6 +78,25 @@ def test_bench_headline_two_rank_rehearsal():
     assert r.returncode == 0, r.stderr[-3000:]
     d = _line(r.stdout)
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 64 and d["config"]["launch_mode"] == "eager"
+    # one batched D(x) / D(x_fake) pass under DP too (round 6), as at N = 1
+    assert d["config"]["batched_D_step"] is True
+    assert d["value"] > 0
+
+
+def test_bench_gpus_flag_spawns_the_ranks():
+    """The driver's plain `python bench.py --gpus N` (no launcher): bench.py starts the N ranks
+    itself (torch.distributed.run as a child process) and relays rank 0's line, which records
+    the process group the ranks actually formed.  Two gloo ranks on the one GPU."""
+    env = _env()
+    env["RGAN_BENCH_BACKEND"] = "gloo"
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--workload", "C1", "--extra=", "--steps", "2",
+                        "--warmup", "1"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 64
+    pg = d["config"]["process_group"]
+    assert pg["world_size"] == 2 and pg["backend"] == "gloo" and pg["launcher"].startswith("bench.py --gpus")
     assert d["value"] > 0
 
 

@@ -129,11 +129,21 @@ def test_dp2_matches_single_process(name):
 
 @pytest.mark.parametrize("name", ["ralsgan", "sgan"])
 def test_dp2_batched_D_matches_single_process(name):
-    """--rgan_batch_D True under data parallelism (the piecewise-graph launch mode's
-    default): D(x) and D(x_fake) as one pass per rank, per-call BN statistics (SyncBN),
+    """--rgan_batch_D True under data parallelism (the default since round 6, every launch
+    mode): D(x) and D(x_fake) as one pass per rank, per-call BN statistics (SyncBN),
     distributed heads on the halves == the single-process global-batch step."""
     single = _run(name, 1, 0)
     dpres = _spawn(name, batch_D=True)
+    _compare(name, dpres, single)
+
+
+@pytest.mark.parametrize("name", ["ralsgan", "sgan"])
+def test_dp2_separate_D_passes_matches_single_process(name):
+    """--rgan_batch_D False under data parallelism: the reference's separate D(x) / D(x_fake)
+    calls per rank (the default is the batched pass since round 6), with G's deferred step
+    overlapping D(x) == the single-process global-batch step."""
+    single = _run(name, 1, 0)
+    dpres = _spawn(name, batch_D=False)
     _compare(name, dpres, single)
 
 
