@@ -27,8 +27,8 @@ extern "C" {
 
 /* ABI revision.  2: rgan_adam_packed takes step = device float[2] (step[1] is the
  * call's uint32 arrival ticket, zero before the first call); revision 1 took float[1].
- * 3: adds rgan_conv_wgrad_rows. */
-#define RGAN_ABI_VERSION 3
+ * 3: adds rgan_conv_wgrad_rows.  4: adds rgan_bn_segment_apply and rgan_bn_backward_sums_apply. */
+#define RGAN_ABI_VERSION 4
 
 /* Activation codes fused into epilogues (GLI:345,370,388,417,437,450; SELU GLI:338). */
 enum {
@@ -231,6 +231,15 @@ int rgan_bn_segment_stats_n(const double* part, long long s0, long long s1, int 
                             long long* num_batches_tracked, float* stats, void* stream);
 int rgan_bn_apply_segments(const float* y, long long P, int C, int nseg, const float* stats, const float* gamma,
                            const float* beta, int act, float act_alpha, float* a, void* stream);
+/* Both of the above in one call (ABI 4): stats[nseg][2C] of y's nseg equal row ranges from
+ * rgan_conv_fwd_bn's segment sums part[S][2][C] (P == S * seg_rows), running statistics in call
+ * order, and a = act(BN(y)).  A small layer (S / nseg <= 64 segments) runs as ONE launch whose
+ * blocks each merge their channels' segment sums in the same fixed order; a larger one as
+ * rgan_bn_segment_stats_n + rgan_bn_apply_segments.  Dense NHWC y and a, 16-byte aligned. */
+int rgan_bn_segment_apply(const double* part, long long S, int nseg, int seg_rows, const float* y, long long P,
+                          int C, float eps, float momentum, float* running_mean, float* running_var,
+                          long long* num_batches_tracked, const float* gamma, const float* beta, int act,
+                          float act_alpha, float* stats, float* a, void* stream);
 /* a = act(gamma * (y - mean) * invstd + beta)  (torch's alpha/beta form) */
 int rgan_bn_apply(const float* y, long long P, int C, long long sp, long long sc,
                   const float* stats, const float* gamma, const float* beta,
@@ -258,6 +267,16 @@ int rgan_bn_backward_segments(const float* da, const float* y, long long P, int 
 int rgan_bn_backward_parts(const float* g, const float* y, long long P, int C, int nseg, const float* stats,
                            const float* gamma, const float* beta, const double* part, long long S, int phases,
                            float* dy, float* dgamma, float* dbeta, double* sums, void* stream);
+/* The staged backward's sums and apply in one call (ABI 4; one process or per-shard BN): writes
+ * sums[2][C] = (sum g, sum g (y - mean)), g = da * act' (the WGAN-GP engine keeps them for the
+ * double backward), dy = BN-backward(g) + add (add nullable), dgamma / dbeta written or, with
+ * accumulate_affine, added into (nullable).  Dense NHWC da, y, dy, add.  P <= 2048 rows (C % 16
+ * == 0): one launch; otherwise rgan_bn_backward_sums + rgan_bn_backward_apply_ex.  partial:
+ * rgan_bn_partial_bytes(P, C). */
+int rgan_bn_backward_sums_apply(const float* da, const float* y, long long P, int C, const float* stats,
+                                const float* gamma, const float* beta, int act, float act_alpha, const float* add,
+                                float* dy, float* dgamma, float* dbeta, int accumulate_affine, double* sums,
+                                void* partial, void* stream);
 /* Backward through act(BN(y)): given da, produce dy, dgamma, dbeta. */
 int rgan_bn_backward(const float* da, long long dsp, long long dsc,
                      const float* y, long long P, int C, long long sp, long long sc,

@@ -55,6 +55,8 @@ _SIGS = {
     "rgan_bn_backward_segments": (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_f, c_vp, c_vp,
                                           c_vp, c_vp, c_vp]),
     "rgan_bn_apply_segments": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_f, c_vp, c_vp]),
+    "rgan_bn_segment_apply": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_ll, c_int, c_f, c_f, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp, c_int, c_f, c_vp, c_vp, c_vp]),
     "rgan_bn_segment_stats": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_f, c_f, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp]),
     "rgan_conv_post_segments": (c_ll, [ctypes.POINTER(RganConv), c_int, c_int, c_int, ctypes.POINTER(c_int)]),
@@ -94,6 +96,8 @@ _SIGS = {
     "rgan_bn_backward_apply_ex": (c_int, [c_vp, c_ll, c_ll, c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp, c_int,
                                           c_f, c_vp, c_ll, c_vp, c_vp, c_ll, c_ll, c_vp, c_vp, c_int, c_vp]),
     "rgan_bn_affine_grads": (c_int, [c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]),
+    "rgan_bn_backward_sums_apply": (c_int, [c_vp, c_vp, c_ll, c_int, c_vp, c_vp, c_vp, c_int, c_f, c_vp, c_vp, c_vp,
+                                            c_vp, c_int, c_vp, c_vp, c_vp]),
     "rgan_bn_dd_partial_bytes": (c_sz, [c_ll, c_int]),
     "rgan_bn_dd_sums": (c_int, [c_vp, c_vp, c_vp, c_ll, c_int, c_ll, c_ll, c_vp, c_vp, c_vp, c_int, c_f, c_int, c_vp,
                                 c_ll, c_vp, c_vp, c_vp]),

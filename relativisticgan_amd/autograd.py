@@ -248,29 +248,33 @@ class ConvLayerFn(torch.autograd.Function):
                 # G's first layer on its 1x1 input: conv + BatchNorm + act in one launch
                 y, a, stats = K.g1_fwd_bn(x, w, gamma, beta, spec.eps, spec.momentum, rm, rv, nbt, spec.act,
                                           spec.alpha, out=out)
+                part, S = None, 0
             elif training:
                 y, part, S = K.conv_fwd_bn(x, w, spec.geom, bias=bias, wscale=wscale, cache=True, segs=segs)
             else:
                 y, part, S = K.conv_fwd(x, w, spec.geom, bias=bias, wscale=wscale, cache=True), None, 0
             C = y.shape[1]
+            # statistics from the epilogue's segment sums + normalisation in one call (one
+            # launch for small layers): one process / per-shard BN, dense aligned NHWC
+            seg_fused = (training and part is not None and segs <= 2 and S % segs == 0 and not dp.sync_bn()
+                         and K.is_nhwc(y) and y.data_ptr() % 16 == 0 and C % 4 == 0
+                         and (out is None or (K.is_nhwc(out) and out.data_ptr() % 16 == 0)))
             if g1:
                 pass
+            elif seg_fused:
+                a = torch.empty_like(y) if out is None else out
+                stats = torch.empty((segs, 2 * C) if segs > 1 else (2 * C,), dtype=torch.float32, device=y.device)
+                K.bn_segment_apply(part, S, y, spec.eps, spec.momentum, rm, rv, nbt, gamma, beta, spec.act,
+                                   spec.alpha, stats.view(segs, 2 * C), a)
             elif training and segs > 1:
                 Bs = y.shape[0] // segs
                 a = torch.empty_like(y) if out is None else out
                 stats = torch.empty((segs, 2 * C), dtype=torch.float32, device=y.device)
-                if (part is not None and segs == 2 and S % 2 == 0 and not dp.sync_bn() and K.is_nhwc(y)
-                        and K.is_nhwc(a) and y.data_ptr() % 16 == 0 and a.data_ptr() % 16 == 0 and C % 4 == 0):
-                    # both calls' statistics (running stats in call order) and normalisation,
-                    # one launch each
-                    K.bn_segment_stats_n(part, S, 2, C, spec.eps, spec.momentum, rm, rv, nbt, out=stats)
-                    K.bn_apply_segments(y, stats, gamma, beta, spec.act, spec.alpha, out=a)
-                else:
-                    for s_ in range(segs):
-                        sl = slice(s_ * Bs, (s_ + 1) * Bs)
-                        seg = (part, s_ * S // segs, (s_ + 1) * S // segs) if part is not None else None
-                        _train_stats(y[sl], spec, rm, rv, nbt, seg, out=stats[s_])
-                        K.bn_apply(y[sl], stats[s_], gamma, beta, spec.act, spec.alpha, out=a[sl])
+                for s_ in range(segs):
+                    sl = slice(s_ * Bs, (s_ + 1) * Bs)
+                    seg = (part, s_ * S // segs, (s_ + 1) * S // segs) if part is not None else None
+                    _train_stats(y[sl], spec, rm, rv, nbt, seg, out=stats[s_])
+                    K.bn_apply(y[sl], stats[s_], gamma, beta, spec.act, spec.alpha, out=a[sl])
             else:
                 if training:
                     stats = _train_stats(y, spec, rm, rv, nbt, (part, 0, S) if part is not None else None)

@@ -487,6 +487,157 @@ extern "C" int rgan_bn_apply(const float* y, long long P, int C, long long sp, l
   return 0;
 }
 
+// ------------------------------------------------------------------ stats + apply, one launch
+// Small layers (<= SA_MAX_SEGS 64-row segments per batch segment): the conv epilogue's
+// segment sums part[S][2][C] (batch segment k = segments [k S/NSEG, (k+1) S/NSEG)) are merged
+// by EVERY block for its own channels -- lane (lc, rl) sums segments rl, rl + rp, ... of its
+// channel quad, then the rp lane sums are added in lane order through LDS: a fixed order, so
+// every block derives bitwise the same (mean, invstd) -- and the block normalises + activates
+// its rows as bn_apply_kernel does.  Blocks with blockIdx.y == 0 publish the stats (the
+// backward's) and update the running statistics in segment order; block (0, 0) counts
+// num_batches_tracked.  Replaces bn_seg_merge + bn_apply_kernel (two launches) where the
+// redundant merge reads (each block: S/4 bytes per channel, from L2) stay well under the
+// apply's own 8 B/element.
+constexpr long long SA_MAX_SEGS = 64;
+constexpr int SA_MAX_ROW_BLOCKS = 256;
+
+// One lane's share of a per-block merge: entries e = rl, rl + rp, ... < n, entry e = segment
+// seg_of(e) of part[S][2][C]; s1 / s2 += that segment's two sums of the channel quad at c0, in
+// entry order, with QM_UNR entries' 16-B loads in flight at once (the merge is a latency chain
+// of L2 round trips otherwise).
+constexpr int QM_UNR = 8;
+template <typename SegOf>
+__device__ __forceinline__ void quad_merge(const double* __restrict__ part, int C, int c0, int rl, int rp, int n,
+                                           SegOf seg_of, double (&s1)[4], double (&s2)[4]) {
+  auto load = [&](int e, double2 (&v)[4]) {
+    const double* r = part + (size_t)seg_of(e) * 2 * C + c0;
+    v[0] = reinterpret_cast<const double2*>(r)[0];
+    v[1] = reinterpret_cast<const double2*>(r)[1];
+    v[2] = reinterpret_cast<const double2*>(r + C)[0];
+    v[3] = reinterpret_cast<const double2*>(r + C)[1];
+  };
+  auto add = [&](const double2 (&v)[4]) {
+    s1[0] += v[0].x; s1[1] += v[0].y; s1[2] += v[1].x; s1[3] += v[1].y;
+    s2[0] += v[2].x; s2[1] += v[2].y; s2[2] += v[3].x; s2[3] += v[3].y;
+  };
+  int e = rl;
+  for (; e + (QM_UNR - 1) * rp < n; e += QM_UNR * rp) {
+    double2 v[QM_UNR][4];
+#pragma unroll
+    for (int u = 0; u < QM_UNR; ++u) load(e + u * rp, v[u]);
+#pragma unroll
+    for (int u = 0; u < QM_UNR; ++u) add(v[u]);
+  }
+  for (; e < n; e += rp) {
+    double2 v[4];
+    load(e, v);
+    add(v);
+  }
+}
+
+template <int NSEG>
+__global__ __launch_bounds__(256) void bn_seg_apply_kernel(const double* __restrict__ part, long long S, double seg_n,
+                                                           float eps, float momentum, float* running_mean,
+                                                           float* running_var, long long* nbt, float* stats_out,
+                                                           const float* __restrict__ y, long long P, int C,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta, int act, float alpha,
+                                                           float* __restrict__ a, int tpr) {
+  __shared__ double sh[2][256][4];
+  const int tid = threadIdx.x, lc = tid % tpr, rl = tid / tpr, rp = blockDim.x / tpr;
+  const int c0 = (blockIdx.x * tpr + lc) * 4;
+  const bool live = c0 < C;
+  const long long Sk = S / NSEG;
+  float al_s[NSEG][4], be_s[NSEG][4];
+#pragma unroll
+  for (int sg = 0; sg < NSEG; ++sg) {
+    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+    if (live) {
+      const long long k0 = sg * Sk;
+      quad_merge(part, C, c0, rl, rp, (int)Sk, [&](int e) { return k0 + e; }, s1, s2);
+    }
+    if (sg > 0) __syncthreads();  // the previous segment's lane sums are read
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { sh[0][tid][q] = s1[q]; sh[1][tid][q] = s2[q]; }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double S1 = 0.0, S2 = 0.0;
+      for (int r = 0; r < rp; ++r) { S1 += sh[0][r * tpr + lc][q]; S2 += sh[1][r * tpr + lc][q]; }
+      // bn_seg_merge's formulas: unshifted double sums of the 64-row segments
+      const double n = seg_n * (double)Sk, mean = S1 / n, m2 = fmax(S2 - S1 * mean, 0.0), var = m2 / n;
+      const float fmean = (float)mean, finv = (float)(1.0 / sqrt(var + (double)eps));
+      const int c = min(c0 + q, C - 1);
+      al_s[sg][q] = (gamma ? gamma[c] : 1.f) * finv;
+      be_s[sg][q] = (beta ? beta[c] : 0.f) - fmean * al_s[sg][q];
+      if (blockIdx.y == 0 && rl == 0 && live && c0 + q < C) {
+        float* st = stats_out + (size_t)sg * 2 * C;
+        st[c] = fmean;
+        st[C + c] = finv;
+        if (running_mean) running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * fmean;
+        if (running_var) {
+          const float unb = n > 1.0 ? (float)(m2 / (n - 1.0)) : (float)var;
+          running_var[c] = (1.f - momentum) * running_var[c] + momentum * unb;
+        }
+      }
+    }
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0 && nbt) nbt[0] += 1;
+  }
+  if (!live) return;
+  const long long seg_rows = P / NSEG;
+  const long long step = (long long)gridDim.y * rp;
+  auto out = [&](long long p, float (&v)[4]) {
+    const int sg = NSEG > 1 && p >= seg_rows ? 1 : 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = act_fwd(v[q] * al_s[sg][q] + be_s[sg][q], act, alpha);
+    *reinterpret_cast<float4*>(a + p * C + c0) = make_float4(v[0], v[1], v[2], v[3]);
+  };
+  long long p = (long long)blockIdx.y * rp + rl;
+  for (; p + (BN_UNR - 1) * step < P; p += BN_UNR * step) {
+    float v[BN_UNR][4];
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) load_q<4>(y, (p + u * step) * C + c0, v[u]);
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) out(p + u * step, v[u]);
+  }
+  for (; p < P; p += step) {
+    float v[4];
+    load_q<4>(y, p * C + c0, v);
+    out(p, v);
+  }
+}
+
+extern "C" int rgan_bn_segment_apply(const double* part, long long S, int nseg, int seg_rows, const float* y,
+                                     long long P, int C, float eps, float momentum, float* running_mean,
+                                     float* running_var, long long* num_batches_tracked, const float* gamma,
+                                     const float* beta, int act, float act_alpha, float* stats, float* a,
+                                     void* stream) {
+  RGAN_REQUIRE(act_ok(act));
+  RGAN_REQUIRE(part && y && a && stats && S > 0 && P > 0 && C > 0 && seg_rows > 0 && (nseg == 1 || nseg == 2) &&
+               S % nseg == 0 && P % nseg == 0 && P == S * (long long)seg_rows);
+  const BnGeo g = bn_geo(P, C, C, 1);
+  RGAN_REQUIRE(g.vec && ((uintptr_t)y & 15) == 0 && ((uintptr_t)a & 15) == 0);
+  if (S / nseg > SA_MAX_SEGS) {  // large layer: merge once, then apply
+    int rc = rgan_bn_segment_stats_n(part, 0, S, nseg, C, seg_rows, eps, momentum, running_mean, running_var,
+                                     num_batches_tracked, stats, stream);
+    if (rc) return rc;
+    return rgan_bn_apply_segments(y, P, C, nseg, stats, gamma, beta, act, act_alpha, a, stream);
+  }
+  const hipStream_t s = (hipStream_t)stream;
+  dim3 grid = apply_grid(g, P);
+  grid.y = std::min<unsigned>(grid.y, SA_MAX_ROW_BLOCKS);
+  if (nseg == 1)
+    bn_seg_apply_kernel<1><<<grid, 256, 0, s>>>(part, S, (double)seg_rows, eps, momentum, running_mean, running_var,
+                                                num_batches_tracked, stats, y, P, C, gamma, beta, act, act_alpha, a,
+                                                g.tpr);
+  else
+    bn_seg_apply_kernel<2><<<grid, 256, 0, s>>>(part, S, (double)seg_rows, eps, momentum, running_mean, running_var,
+                                                num_batches_tracked, stats, y, P, C, gamma, beta, act, act_alpha, a,
+                                                g.tpr);
+  RGAN_CHECK_LAUNCH();
+  return 0;
+}
+
 // ------------------------------------------------------------------ backward
 // partial [chunk][2][C] doubles: sum g, sum g*(y-mean);  g = da * act'(y*al + be)
 // NSEG 2: the batched D pass's two calls in one launch -- chunk x of segment x / chunks_seg
@@ -655,6 +806,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply(const float* __restrict__ da
 // by a fixed xor butterfly, the 8 waves by a fixed LDS sum, then every lane applies its rows
 // with bn_bwd_apply's constants and formula.  NSEG 2: rows [0, Ps) use stats / sums row 0,
 // [Ps, 2 Ps) row 1; the affine gradients are the segments' sum.
+// (round 6: 16 / NSEG cached rows per lane, was 8 / NSEG -- a 2048-row call re-read its last 8
+// rows per lane one dependent round trip at a time, 24-28 us per call at C = 128-256 in the
+// WGAN-GP engine; every row of a <= 2048-row single call now stays in registers, 128 VGPRs of
+// the 256 two waves per SIMD allow)
 constexpr int BNS_LANES = 128, BNS_CH = 16, BNS_THREADS = 512;
 constexpr long long BNS_MAX_ROWS = 2048;  // rows per segment
 template <int NSEG>
@@ -662,8 +817,10 @@ __global__ __launch_bounds__(BNS_THREADS) void bn_bwd_small(const float* __restr
                                                             long long Ps, int C, const float* __restrict__ stats,
                                                             const float* __restrict__ gamma,
                                                             const float* __restrict__ beta, int act, float alpha,
-                                                            float* __restrict__ dy, float* dgamma, float* dbeta) {
-  constexpr int RC = 8 / NSEG;  // rows per segment cached in registers
+                                                            float* __restrict__ dy, float* dgamma, float* dbeta,
+                                                            const float* __restrict__ add = nullptr,
+                                                            int accum_affine = 0, double* sums_out = nullptr) {
+  constexpr int RC = 16 / NSEG;  // rows per segment cached in registers
   constexpr int NW = BNS_THREADS / 64;
   __shared__ double sh[2][NSEG][NW][BNS_CH];
   const int tid = threadIdx.x, q = tid & 3, r = tid >> 2, lane = tid & 63, wv = tid >> 6;
@@ -754,10 +911,14 @@ __global__ __launch_bounds__(BNS_THREADS) void bn_bwd_small(const float* __restr
       const float dbs = (float)S1, dgs = (float)(S2 * iv);
       db = sg == 0 ? dbs : db + dbs;
       dg = sg == 0 ? dgs : dg + dgs;
+      if (sums_out && r == 0) {  // the sums themselves (the WGAN-GP engine keeps them)
+        sums_out[((size_t)sg * 2 + 0) * C + c0 + k] = S1;
+        sums_out[((size_t)sg * 2 + 1) * C + c0 + k] = S2;
+      }
     }
     if (r == 0) {
-      if (dbeta) dbeta[c0 + k] = db;
-      if (dgamma) dgamma[c0 + k] = dg;
+      if (dbeta) dbeta[c0 + k] = accum_affine ? dbeta[c0 + k] + db : db;
+      if (dgamma) dgamma[c0 + k] = accum_affine ? dgamma[c0 + k] + dg : dg;
     }
   }
   auto apply = [&](int sg, const float4& v4, const float4& g4, long long row) {
@@ -767,6 +928,10 @@ __global__ __launch_bounds__(BNS_THREADS) void bn_bwd_small(const float* __restr
     for (int k = 0; k < 4; ++k) {
       const float gz = gg[k] * act_grad_from_in(vv[k] * al[sg][k] + be[sg][k], act, alpha);
       vv[k] = al[sg][k] * (gz - k1[sg][k] - (vv[k] - mean[sg][k]) * k2[sg][k]);
+    }
+    if (add) {
+      const float4 w4 = *reinterpret_cast<const float4*>(add + row * C + c0);
+      vv[0] += w4.x; vv[1] += w4.y; vv[2] += w4.z; vv[3] += w4.w;
     }
     *reinterpret_cast<float4*>(dy + row * C + c0) = make_float4(vv[0], vv[1], vv[2], vv[3]);
   };
@@ -837,6 +1002,26 @@ extern "C" int rgan_bn_backward_apply_ex(const float* da, long long dsp, long lo
                                                     add, accumulate_affine);
   RGAN_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int rgan_bn_backward_sums_apply(const float* da, const float* y, long long P, int C, const float* stats,
+                                           const float* gamma, const float* beta, int act, float act_alpha,
+                                           const float* add, float* dy, float* dgamma, float* dbeta,
+                                           int accumulate_affine, double* sums, void* partial, void* stream) {
+  RGAN_REQUIRE(act_ok(act));
+  RGAN_REQUIRE(da && y && stats && dy && sums && partial && P > 0 && C > 0);
+  if (P <= BNS_MAX_ROWS && C % BNS_CH == 0 && dense_nhwc(C, 1, C, y) && dense_nhwc(C, 1, C, da) &&
+      dense_nhwc(C, 1, C, dy) && (!add || dense_nhwc(C, 1, C, add))) {  // small layers: one launch
+    bn_bwd_small<1><<<C / BNS_CH, BNS_THREADS, 0, (hipStream_t)stream>>>(da, y, P, C, stats, gamma, beta, act,
+                                                                         act_alpha, dy, dgamma, dbeta, add,
+                                                                         accumulate_affine, sums);
+    RGAN_CHECK_LAUNCH();
+    return 0;
+  }
+  int rc = rgan_bn_backward_sums(da, C, 1, y, P, C, C, 1, stats, gamma, beta, act, act_alpha, sums, partial, stream);
+  if (rc) return rc;
+  return rgan_bn_backward_apply_ex(da, C, 1, y, P, C, C, 1, stats, gamma, beta, act, act_alpha, sums, P, add, dy, C,
+                                   1, dgamma, dbeta, accumulate_affine, stream);
 }
 
 // dgamma (+)= (float)(sum g (y - mean) * invstd), dbeta (+)= (float)sum g from [2][C] sums --
@@ -951,6 +1136,90 @@ __global__ __launch_bounds__(1024) void bn_part_merge(const double* __restrict__
   }
 }
 
+// bn_part_merge + bn_bwd_apply (act = none: g already carries act') in one launch for small
+// layers (<= SA_MAX_SEGS post-op segments per batch segment): every block merges its channels'
+// segment sums in bn_part_merge's segment order with the fixed lane layout of
+// bn_seg_apply_kernel (bitwise the same sums in every block), blocks with blockIdx.y == 0
+// write the affine gradients, then the block applies its rows.
+template <int NSEG>
+__global__ __launch_bounds__(256) void bn_parts_apply_kernel(const float* __restrict__ g, const float* __restrict__ y,
+                                                             long long P, int C, const float* __restrict__ stats,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta,
+                                                             const double* __restrict__ part, int S, int phases,
+                                                             float* __restrict__ dy, float* dgamma, float* dbeta,
+                                                             int tpr) {
+  __shared__ double sh[2][256][4];
+  const int tid = threadIdx.x, lc = tid % tpr, rl = tid / tpr, rp = blockDim.x / tpr;
+  const int c0 = (blockIdx.x * tpr + lc) * 4;
+  const bool live = c0 < C;
+  const int Sp = S / phases, J = Sp / NSEG, cnt = phases * J;
+  const long long seg_rows = P / NSEG;
+  const double inv_pg = 1.0 / (double)seg_rows;
+  float mean_s[NSEG][4], al_s[NSEG][4], be_s[NSEG][4], k1_s[NSEG][4], k2_s[NSEG][4];
+  float db[4] = {0.f, 0.f, 0.f, 0.f}, dg[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int sg = 0; sg < NSEG; ++sg) {
+    double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+    if (live)
+      quad_merge(part, C, c0, rl, rp, cnt, [&](int i) { const int ph = i / J; return ph * Sp + sg * J + (i - ph * J); },
+                 s1, s2);
+    if (sg > 0) __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) { sh[0][tid][q] = s1[q]; sh[1][tid][q] = s2[q]; }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double S1 = 0.0, S2 = 0.0;
+      for (int r = 0; r < rp; ++r) { S1 += sh[0][r * tpr + lc][q]; S2 += sh[1][r * tpr + lc][q]; }
+      const int c = min(c0 + q, C - 1);
+      const float* st = stats + (size_t)sg * 2 * C;
+      const float inv = st[C + c];
+      mean_s[sg][q] = st[c];
+      al_s[sg][q] = (gamma ? gamma[c] : 1.f) * inv;
+      be_s[sg][q] = (beta ? beta[c] : 0.f) - mean_s[sg][q] * al_s[sg][q];
+      k1_s[sg][q] = (float)(S1 * inv_pg);
+      k2_s[sg][q] = (float)(S2 * (double)inv * (double)inv * inv_pg);
+      const float dbs = (float)S1, dgs = (float)(S2 * (double)inv);
+      db[q] = sg == 0 ? dbs : db[q] + dbs;
+      dg[q] = sg == 0 ? dgs : dg[q] + dgs;
+    }
+  }
+  if (!live) return;
+  if (blockIdx.y == 0 && rl == 0)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (c0 + q < C) {
+        if (dbeta) dbeta[c0 + q] = db[q];
+        if (dgamma) dgamma[c0 + q] = dg[q];
+      }
+  const long long step = (long long)gridDim.y * rp;
+  auto out = [&](long long p, float (&v)[4], const float (&gz)[4]) {
+    const int sg = NSEG > 1 && p >= seg_rows ? 1 : 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      v[q] = al_s[sg][q] * (gz[q] - k1_s[sg][q] - (v[q] - mean_s[sg][q]) * k2_s[sg][q]);
+    *reinterpret_cast<float4*>(dy + p * C + c0) = make_float4(v[0], v[1], v[2], v[3]);
+  };
+  long long p = (long long)blockIdx.y * rp + rl;
+  for (; p + (BN_UNR - 1) * step < P; p += BN_UNR * step) {
+    float v[BN_UNR][4], gz[BN_UNR][4];
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) {
+      load_q<4>(y, (p + u * step) * C + c0, v[u]);
+      load_q<4>(g, (p + u * step) * C + c0, gz[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < BN_UNR; ++u) out(p + u * step, v[u], gz[u]);
+  }
+  for (; p < P; p += step) {
+    float v[4], gz[4];
+    load_q<4>(y, p * C + c0, v);
+    load_q<4>(g, p * C + c0, gz);
+    out(p, v, gz);
+  }
+}
+
 extern "C" int rgan_bn_backward_parts(const float* g, const float* y, long long P, int C, int nseg,
                                       const float* stats, const float* gamma, const float* beta, const double* part,
                                       long long S, int phases, float* dy, float* dgamma, float* dbeta, double* sums,
@@ -962,6 +1231,18 @@ extern "C" int rgan_bn_backward_parts(const float* g, const float* y, long long 
   hipStream_t s = (hipStream_t)stream;
   const BnGeo ga = bn_geo(P, C, C, 1);
   RGAN_REQUIRE(ga.vec && dense_nhwc(C, 1, C, y) && dense_nhwc(C, 1, C, g) && dense_nhwc(C, 1, C, dy));
+  if (S / nseg <= SA_MAX_SEGS) {  // small layer: merge + apply in one launch
+    dim3 grid = apply_grid(ga, P);
+    grid.y = std::min<unsigned>(grid.y, SA_MAX_ROW_BLOCKS);
+    if (nseg == 1)
+      bn_parts_apply_kernel<1><<<grid, 256, 0, s>>>(g, y, P, C, stats, gamma, beta, part, (int)S, phases, dy, dgamma,
+                                                    dbeta, ga.tpr);
+    else
+      bn_parts_apply_kernel<2><<<grid, 256, 0, s>>>(g, y, P, C, stats, gamma, beta, part, (int)S, phases, dy, dgamma,
+                                                    dbeta, ga.tpr);
+    RGAN_CHECK_LAUNCH();
+    return 0;
+  }
   bn_part_merge<<<dim3(ceil_div(C, MERGE_CPB), nseg), 1024, 0, s>>>(part, (int)S, phases, C, sums);
   RGAN_CHECK_LAUNCH();
   const long long Ps = P / nseg;

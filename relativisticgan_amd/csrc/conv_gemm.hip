@@ -1109,6 +1109,37 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
         put([&](float v) { return act_fwd_curved(v, g.act, g.alpha); });
       }
     }
+  if constexpr (BM == 64 && BN == 64 && MODE != MODE_WGRAD) {
+    if (g.bnp) {
+      // BatchNorm segment sums of the 64 x 64 tile (unsplit, act none, n = channel, M % 64 ==
+      // 0: host bn_epilogue_ok): the tile's 64 rows are one segment.  Per column: the lane's 16
+      // rows in register order, then the two lane halves (xor 32), then the two waves of the
+      // column (wm = 0, 32) in order through LDS -- (sum y, sum y^2) in double of the values
+      // stored above, as the 128 x 128 vector epilogue writes them.
+      double s1 = 0.0, s2 = 0.0;
+      const int cl = wn + l32, col = n0 + cl;
+      const float bv = (g.bias && col < g.N) ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const double d = (double)(acc[0][0][r] * wsc + bv);
+        s1 += d;
+        s2 += d * d;
+      }
+      s1 += __shfl_xor(s1, 32);
+      s2 += __shfl_xor(s2, 32);
+      double* bsh = reinterpret_cast<double*>(noff + BN);  // [2 waves][2][64]
+      if (lk == 0) {
+        bsh[(wm / 32) * 128 + cl] = s1;
+        bsh[(wm / 32) * 128 + 64 + cl] = s2;
+      }
+      __syncthreads();
+      if (tid < 64 && n0 + tid < g.N && m0 < g.M) {
+        const size_t seg = (size_t)phase * (uint32_t)(g.M >> 6) + (uint32_t)(m0 >> 6);
+        g.bnp[(seg * 2) * g.N + n0 + tid] = bsh[tid] + bsh[128 + tid];
+        g.bnp[(seg * 2 + 1) * g.N + n0 + tid] = bsh[64 + tid] + bsh[192 + tid];
+      }
+    }
+  }
 }
 
 template <int MODE, int BM, int BN, int WM, int WN, bool AV, bool BV, bool FAST>
@@ -2808,6 +2839,9 @@ static void choose_tiling(Plan& p) {
   // on 128 x 64: 3.535 -> 3.55 with them moved too)
   if (p.cfg == CFG_M && p.mode != MODE_WGRAD && 2.0 * g.M * g.N * g.K * p.phases < SMALL_GEMM_FLOPS && !emu_bf16x6())
     p.cfg = CFG_S;
+  // the weight gradient of a thin input layer (N = taps x <= 3 channels <= 32, M = Cout <= 64:
+  // arch 1's Conv3x3 3 -> 64, GLI:260): a 256-row tile would be >= 75 % empty rows (round 6)
+  if (p.cfg == CFG_N && p.mode == MODE_WGRAD && g.M <= 64 && !emu_bf16x6()) p.cfg = CFG_S;
   if (p.cfg == CFG_L) {
     const long long t = (long long)ceil_div(g.M, 128) * ceil_div(g.N, 128) * p.phases;
     const int nk = ceil_div(g.K, BK);
@@ -3587,7 +3621,10 @@ static void run_dense1(const Plan& p, const float* packed, hipStream_t s) {
 static bool bn_epilogue_ok(const Plan& p) {
   const GemmArgs& g = p.g;
   if (p.mode != MODE_CONV && p.mode != MODE_CONVT2) return false;
-  if (!p.fast || p.cfg != CFG_L || g.splits != 1 || !g.vec_out || p.tap_stage) return false;
+  // the 128 x 128 vector epilogue, or the 64 x 64 tile's scalar epilogue (one segment per tile)
+  const bool l_vec = p.fast && p.cfg == CFG_L && g.vec_out;
+  const bool s_tile = p.cfg == CFG_S && g.act == RGAN_ACT_NONE;
+  if (!(l_vec || s_tile) || g.splits != 1 || p.tap_stage) return false;
   if (g.out.fnc.d != (uint32_t)g.N || g.M % 64 != 0 || p.bn_segs < 1) return false;
   if (p.bn_segs > 1 && (p.phases != 1 || g.M % p.bn_segs != 0 || (g.M / p.bn_segs) % 64 != 0)) return false;
   return true;

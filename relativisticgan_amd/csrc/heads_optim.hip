@@ -934,7 +934,7 @@ extern "C" int rgan_gather_images(const float* images, const long long* idx, int
   return 0;
 }
 
-extern "C" const char* rgan_version(void) { return "rgan-mi355x 0.2 gfx950 fp32-mfma abi3"; }
+extern "C" const char* rgan_version(void) { return "rgan-mi355x 0.2 gfx950 fp32-mfma abi4"; }
 extern "C" int rgan_abi_version(void) { return RGAN_ABI_VERSION; }
 
 }  // namespace rgan

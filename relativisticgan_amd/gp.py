@@ -133,10 +133,17 @@ class GPEngine:
             w = r.w  # the parameter (or its view) itself: the pack cache is keyed by the weight's base
             if spec.bn:
                 y, part, S = K.conv_fwd_bn(h, w, spec.geom, bias=r.bias, wscale=r.wscale, cache=True)
-                r.stats = AG._train_stats(y, spec, bn.running_mean, bn.running_var, bn.num_batches_tracked,
-                                          (part, 0, S) if part is not None else None)
                 r.y = y
-                r.a = K.bn_apply(y, r.stats, r.gamma, r.beta, spec.act, spec.alpha, out=out)
+                if part is not None and not dp.sync_bn() and y.shape[1] % 4 == 0 and out.data_ptr() % 16 == 0:
+                    # statistics + normalisation in one call (one launch for small layers)
+                    r.stats = torch.empty(2 * y.shape[1], dtype=torch.float32, device=self.dev)
+                    r.a = K.bn_segment_apply(part, S, y, spec.eps, spec.momentum, bn.running_mean, bn.running_var,
+                                             bn.num_batches_tracked, r.gamma, r.beta, spec.act, spec.alpha,
+                                             r.stats.view(1, -1), out)
+                else:
+                    r.stats = AG._train_stats(y, spec, bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                                              (part, 0, S) if part is not None else None)
+                    r.a = K.bn_apply(y, r.stats, r.gamma, r.beta, spec.act, spec.alpha, out=out)
             else:
                 r.y, r.stats = None, None
                 r.a = K.conv_fwd(h, w, spec.geom, bias=r.bias, act=spec.act, alpha=spec.alpha, wscale=r.wscale,
@@ -161,7 +168,11 @@ class GPEngine:
             if spec.bn or spec.act != "none":
                 C, Ho, Wo = r.a.shape[1], r.a.shape[2], r.a.shape[3]
                 r.yc = empty_nhwc(2 * B, C, Ho, Wo, self.dev)
-            if spec.bn:
+            if spec.bn and not dp.sync_bn():
+                # sums (kept for the double backward) + apply in one call
+                r.fs, r.dy = K.bn_backward_sums_apply(dh, r.y, r.stats, r.gamma, r.beta, spec.act, spec.alpha,
+                                                      out=r.yc[:B])
+            elif spec.bn:
                 fs, dh_c = K.bn_backward_sums(dh, r.y, r.stats, r.gamma, r.beta, spec.act, spec.alpha)
                 r.fs, _ = _global(fs)
                 r.dy, _, _ = K.bn_backward_apply(dh_c, r.y, r.stats, r.gamma, r.beta, spec.act, spec.alpha, r.fs,
@@ -221,7 +232,14 @@ class GPEngine:
             ydir = ydirs[li]
             ybar = None
             if gbar is not None:
-                if spec.bn:
+                if spec.bn and not dp.sync_bn():
+                    # BN backward of gbar + the double backward's direct term, one call
+                    _, ybar = K.bn_backward_sums_apply(gbar, r.y, r.stats, r.gamma, r.beta, spec.act, spec.alpha,
+                                                       add=ydir, out=r.yc[B:],
+                                                       dgamma=_grad_buf(r.gamma) if r.gamma is not None else None,
+                                                       dbeta=_grad_buf(r.beta) if r.beta is not None else None,
+                                                       accumulate_affine=True)
+                elif spec.bn:
                     sums, g_c = K.bn_backward_sums(gbar, r.y, r.stats, r.gamma, r.beta, spec.act, spec.alpha)
                     sums, sums_loc = _global(sums)
                     dgb = _grad_buf(r.gamma) if r.gamma is not None else None

@@ -597,6 +597,28 @@ def bn_backward_apply(da, y, stats, gamma, beta, act, alpha, sums, P_global, nee
     return dy, dgamma, dbeta
 
 
+def bn_backward_sums_apply(da, y, stats, gamma, beta, act, alpha, add=None, out=None, dgamma=None, dbeta=None,
+                           accumulate_affine=False):
+    """(sums double[2C], dy) of act(BN(y))'s backward in one call (rgan_bn_backward_sums_apply:
+    one launch for <= 2048 rows): sums as bn_backward_sums returns them, dy = BN-backward(da *
+    act') + add; dgamma / dbeta (given buffers) written or, with accumulate_affine, added into.
+    Dense NHWC da / y / out / add."""
+    if not is_nhwc(da):
+        da = da.contiguous(memory_format=torch.channels_last)
+    P, C, _, _ = _pc(y)
+    dy = torch.empty_like(y) if out is None else out
+    if not is_nhwc(dy) or (add is not None and not is_nhwc(add)):
+        raise L.RganError("bn_backward_sums_apply: out / add must be NHWC")
+    sums = torch.empty(2 * C, dtype=torch.float64, device=y.device)
+    lib = L.lib()
+    part = L.workspace(lib.rgan_bn_partial_bytes(P, C), y.device)
+    L.check(lib.rgan_bn_backward_sums_apply(L.ptr(da), L.ptr(y), P, C, L.ptr(stats), L.ptr(gamma), L.ptr(beta),
+                                            L.ACT[act], float(alpha), L.ptr(add), L.ptr(dy), L.ptr(dgamma),
+                                            L.ptr(dbeta), int(bool(accumulate_affine)), L.ptr(sums), L.ptr(part),
+                                            L.stream()), "rgan_bn_backward_sums_apply")
+    return sums, dy
+
+
 def bn_affine_grads(sums, stats, C, dgamma=None, dbeta=None, accumulate=False):
     """dgamma / dbeta (given buffers) from BatchNorm backward sums [2][C] (rgan_bn_affine_grads):
     written, or added into with ``accumulate``."""
@@ -610,6 +632,20 @@ def bn_segment_stats_n(part, S, nseg, C, eps, momentum, running_mean, running_va
     L.check(L.lib().rgan_bn_segment_stats_n(L.ptr(part), 0, int(S), int(nseg), C, 64, float(eps), float(momentum),
                                             L.ptr(running_mean), L.ptr(running_var), L.ptr(num_batches_tracked),
                                             L.ptr(out), L.stream()), "rgan_bn_segment_stats_n")
+    return out
+
+
+def bn_segment_apply(part, S, y, eps, momentum, running_mean, running_var, num_batches_tracked, gamma, beta, act,
+                     alpha, stats, out):
+    """bn_segment_stats_n + bn_apply_segments in one call (rgan_bn_segment_apply): nseg =
+    stats.shape[0] equal batch segments of y (dense NHWC, 16-byte aligned) and of conv_fwd_bn's
+    S segment sums; one launch for small layers."""
+    P, C, _, _ = _pc(y)
+    L.check(L.lib().rgan_bn_segment_apply(L.ptr(part), int(S), int(stats.shape[0]), 64, L.ptr(y), P, C, float(eps),
+                                          float(momentum), L.ptr(running_mean), L.ptr(running_var),
+                                          L.ptr(num_batches_tracked), L.ptr(gamma), L.ptr(beta), L.ACT[act],
+                                          float(alpha), L.ptr(stats), L.ptr(out), L.stream()),
+            "rgan_bn_segment_apply")
     return out
 
 

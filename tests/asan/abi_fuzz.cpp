@@ -199,6 +199,16 @@ static void malformed_compute(Rng& r, const RganConv& good) {
                 "bn_backward_segments C<=0");
   expect_einval(rgan_bn_backward_parts(p, p, 16, 8, 0, p, p, p, nullptr, 0, 1, p, p, p, nullptr, nullptr),
                 "bn_backward_parts nseg=0");
+  expect_einval(rgan_bn_segment_apply((double*)p, 4, 0, 64, p, 256, 8, 1e-5f, 0.1f, p, p, nullptr, p, p, 0, 0.f, p,
+                                      p, nullptr), "bn_segment_apply nseg=0");
+  expect_einval(rgan_bn_segment_apply((double*)p, 4, 1, 64, p, 255, 8, 1e-5f, 0.1f, p, p, nullptr, p, p, 0, 0.f, p,
+                                      p, nullptr), "bn_segment_apply P != S * seg_rows");
+  expect_einval(rgan_bn_segment_apply((double*)p, 4, 1, 64, p, 256, 8, 1e-5f, 0.1f, p, p, nullptr, p, p, 99, 0.f,
+                                      p, p, nullptr), "bn_segment_apply act=99");
+  expect_einval(rgan_bn_backward_sums_apply(p, p, Pn, 8, p, p, p, 0, 0.f, nullptr, p, p, p, 0, (double*)p, ws,
+                                            nullptr), "bn_backward_sums_apply P<0");
+  expect_einval(rgan_bn_backward_sums_apply(p, p, 16, 8, p, p, p, 0, 0.f, nullptr, p, p, p, 0, nullptr, ws,
+                                            nullptr), "bn_backward_sums_apply sums=0");
   expect_einval(rgan_act_backward(nullptr, p, 16, 1, 0.f, p, nullptr), "act_backward da=0");
   expect_einval(rgan_act_backward(p, p, -1, 1, 0.f, p, nullptr), "act_backward n<0");
   expect_einval(rgan_act_backward_ex(p, p, p, 16, 99, 0.f, p, nullptr), "act_backward_ex act=99");

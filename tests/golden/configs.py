@@ -99,9 +99,21 @@ SLOW_PIN = ("ralsgan_c3",)
 
 # 100-iteration scalar trajectories of the unmodified reference at several thread counts
 # (SURVEY §8(c)(iii)): the spread between thread counts is the drift envelope.  Keys of
-# TRAJECTORIES name a config of CONFIGS whose args are used with n_iter = TRAJ_ITERS.
+# TRAJECTORIES name a config of CONFIGS whose args are used with n_iter = traj_iters(name)
+# (TRAJ_ITERS, or the reduced count of TRAJ_ITERS_OF: C2 costs ~6 s per reference iteration at
+# 8 threads and ~40 s at 1).
 TRAJ_ITERS = 100
-TRAJECTORIES = {"ralsgan_c1": (1, 2, 4, 8)}
+TRAJECTORIES = {
+    "ralsgan_c1": (1, 2, 4, 8),           # north-star RaLSGAN 64^2 (GLI:639, 705)
+    "wgangp_c4": (1, 2, 4, 8),            # arch-1 WGAN-GP 32^2 (GLI:183-319, 646-658)
+    "rasgan_c2": (1, 4, 8),               # RaSGAN 128^2 B64 (GLI:636-637, 699-702), reduced iterations
+    "rahinge_spectral_c5": (1, 4, 8),     # spectral RaHinge 128^2 (GLI:408-446, 641, 709)
+}
+TRAJ_ITERS_OF = {"rasgan_c2": 30}
+
+
+def traj_iters(name):
+    return TRAJ_ITERS_OF.get(name, TRAJ_ITERS)
 
 
 # configs with a reference fixture (tests/golden/<name>.npz) pinning the oracle bitwise

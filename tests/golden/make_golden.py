@@ -273,11 +273,11 @@ def run_trajectory(name, threads, n_iter):
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "--trajectory":
         # --trajectory NAME [THREADS ...]: one fresh interpreter per thread count
-        from tests.golden.configs import TRAJ_ITERS, TRAJECTORIES
+        from tests.golden.configs import TRAJECTORIES, traj_iters
         name = sys.argv[2]
         threads = [int(t) for t in sys.argv[3:]] or list(TRAJECTORIES[name])
         if len(threads) == 1:
-            print(name, threads[0], "->", run_trajectory(name, threads[0], TRAJ_ITERS), flush=True)
+            print(name, threads[0], "->", run_trajectory(name, threads[0], traj_iters(name)), flush=True)
         else:
             import subprocess
             for th in threads:

@@ -39,7 +39,7 @@ def test_library_exports_every_declared_symbol():
     # rgan_adam_packed's float[2] step (count + arrival ticket) is ABI revision 2 (include/rgan.h)
     hdr = open(os.path.join(ROOT, "include", "rgan.h")).read()
     want = int(re.search(r"#define RGAN_ABI_VERSION (\d+)", hdr).group(1))
-    assert lib.rgan_abi_version() == want == 3
+    assert lib.rgan_abi_version() == want == 4
     assert lib.rgan_version().endswith(b"abi%d" % want)
 
 

@@ -8,9 +8,10 @@ GPU's errD/errG trajectory may not diverge from the float64 oracle trajectory fa
 the fp32 oracle itself does (the oracle is pinned bitwise to the reference).
   * steps 0-9: per-step relative gap <= max(5e-3, 10 x the fp32 oracle's own gap);
   * all 100 steps: mean gap <= 3 x the fp32 oracle's mean gap + 1e-3.
-At the north-star config itself (RaLSGAN 64^2, B=32, h=128) the envelope is the reference's
-own: its trajectories at 1, 2, 4 and 8 threads, recorded from the unmodified script
-(test_c1_100_step_drift_within_reference_thread_envelope; bounds in its docstring).
+At the full-size BASELINE configs (C1 RaLSGAN 64^2, C2 RaSGAN 128^2, C4 arch-1 WGAN-GP 32^2,
+C5 spectral RaHinge 128^2) the envelope is the reference's own: its trajectories at several
+thread counts, recorded from the unmodified script (test_drift_within_reference_thread_envelope;
+bounds in its docstring).
 """
 import numpy as np
 import pytest
@@ -68,10 +69,9 @@ def test_100_step_drift_within_fp32_envelope(name):
 
 
 # ---------------------------------------------------------------------------------------------
-# The north-star config against the reference's own envelope: 100 free-
-# running iterations of RaLSGAN 64^2, B=32, h=z=128 (GLI:560-714 x 100), host RNG, vs the
-# unmodified reference's trajectories at 1, 2, 4 and 8 intra-op threads
-# (tests/golden/traj_ralsgan_c1_t*.npz, make_golden.py --trajectory).  Thread counts change only
+# The full-size configs against the reference's own envelope: free-running
+# iterations (GLI:560-714 x 100; C2 x 30), host RNG, vs the unmodified reference's trajectories
+# at several intra-op threads (tests/golden/traj_<config>_t*.npz, make_golden.py --trajectory).  Thread counts change only
 # the fp32 summation order, so their spread is the reference's own run-to-run envelope.
 TRAJ_Q = ("errD", "errG", "D.y_pred", "D.y_pred_fake", "G.y_pred", "G.y_pred_fake")
 DRAWS = ("D.x", "D.z", "G.z", "G.x")
@@ -92,7 +92,7 @@ def _ref_trajectories(name):
     return out
 
 
-def gpu_c1_trajectory(name, n_iter):
+def gpu_trajectory(name, n_iter):
     from relativisticgan_amd.train import Trainer
     from tests.oracle_replay import dataset_for, param_for
     p = param_for(name)
@@ -127,10 +127,22 @@ def gpu_c1_trajectory(name, n_iter):
     return out
 
 
-def test_c1_100_step_drift_within_reference_thread_envelope():
-    """100 free-running C1 iterations on the GPU (host RNG: the reference's draws) against the
-    reference's own 1 / 2 / 4 / 8-thread trajectories.  Per quantity q (losses, mean D outputs
-    of both steps) with scale s_q = mean |q| over the 8-thread trajectory:
+def _ref_names():
+    from tests.golden.configs import TRAJECTORIES
+    return list(TRAJECTORIES)
+
+
+@pytest.mark.parametrize("name", _ref_names())
+def test_drift_within_reference_thread_envelope(name):
+    """Free-running iterations of a full-size BASELINE config on the GPU (host RNG: the
+    reference's draws) against the unmodified reference's own trajectories at several intra-op
+    thread counts (tests/golden/traj_<name>_t*.npz, make_golden.py --trajectory):
+      ralsgan_c1           RaLSGAN 64^2 B32 h128, 100 iterations, 1/2/4/8 threads (the north star);
+      wgangp_c4            WGAN-GP arch 1 32^2 B32, 100 iterations, 1/2/4/8 threads;
+      rasgan_c2            RaSGAN 128^2 B64 h128, 30 iterations, 1/4/8 threads;
+      rahinge_spectral_c5  spectral RaHinge 128^2 B32 h128, 100 iterations, 1/4/8 threads.
+    Per quantity q the reference records (losses, mean D outputs of both steps; heads 1-4 have
+    no G-step D(x)) with scale s_q = mean |q| over the 8-thread trajectory:
       * the draws (dataset indices, z) equal the reference's at every step;
       * step 0: |gpu - ref8| <= STEP_REL * s_q (one fp32 step, before any Adam update);
       * step k >= 1: |gpu - ref8| <= ENV_MULT * s_q * env(k + ENV_LAG) + STEP_REL * s_q, env(k)
@@ -140,24 +152,29 @@ def test_c1_100_step_drift_within_reference_thread_envelope():
         while any other fp32 summation order -- the GPU's -- flips the signs of near-zero
         gradients in Adam's first (sign) step; the thread counts' trajectories reach that
         divergence two steps later and grow alike from there;
-      * mean over the 100 steps of |gpu - ref8| <= MEAN_MULT x the mean thread spread."""
+      * mean over the iterations of |gpu - ref8| <= MEAN_MULT x the mean thread spread."""
     import json
     import os
-    from tests.golden.configs import TRAJ_ITERS
-    name = "ralsgan_c1"
+    from tests.golden.configs import traj_iters
     ref = _ref_trajectories(name)
-    g = gpu_c1_trajectory(name, TRAJ_ITERS)
     r8 = ref[8]
+    n_iter = traj_iters(name)
+    assert len(r8["errD"]) == n_iter
+    g = gpu_trajectory(name, n_iter)
     # the draws (dataset indices, z) follow the reference's RNG order at every step
     for k in DRAWS:
+        if np.all(np.isnan(r8[k])):
+            assert np.all(np.isnan(g[k])), k
+            continue
         np.testing.assert_allclose(g[k], r8[k], rtol=1e-12, atol=1e-9, err_msg=k)
+    qs = [q for q in TRAJ_Q if not np.all(np.isnan(r8[q]))]
     errs, report = [], {}
-    scale = {q: float(np.mean(np.abs(r8[q]))) for q in TRAJ_Q}
-    spread = {q: np.ptp(np.stack([ref[th][q] for th in ref]), 0) for q in TRAJ_Q}
-    env = np.maximum.accumulate(np.max([spread[q] / scale[q] for q in TRAJ_Q], axis=0))
+    scale = {q: float(np.mean(np.abs(r8[q]))) for q in qs}
+    spread = {q: np.ptp(np.stack([ref[th][q] for th in ref]), 0) for q in qs}
+    env = np.maximum.accumulate(np.max([spread[q] / scale[q] for q in qs], axis=0))
     n = len(env)
     lagged = env[np.minimum(np.arange(n) + ENV_LAG, n - 1)]
-    for q in TRAJ_Q:
+    for q in qs:
         d = np.abs(g[q] - r8[q])
         bound = ENV_MULT * scale[q] * lagged + STEP_REL * scale[q]
         bound[0] = STEP_REL * scale[q]
@@ -169,12 +186,12 @@ def test_c1_100_step_drift_within_reference_thread_envelope():
                         f"(gap {d[bad[0]]:.3e} vs bound {bound[bad[0]]:.3e})")
         if d.mean() > MEAN_MULT * spread[q].mean():
             errs.append(f"{q}: mean gap {d.mean():.3e} > {MEAN_MULT} x the mean thread spread {spread[q].mean():.3e}")
-    print("c1 drift:", {q: {k: f"{v:.3g}" for k, v in r.items()} for q, r in report.items()})
+    print(f"{name} drift:", {q: {k: f"{v:.3g}" for k, v in r.items()} for q, r in report.items()})
     out_dir = os.environ.get("RGAN_PARITY_AUDIT")
     if out_dir:
         os.makedirs(out_dir, exist_ok=True)
-        with open(os.path.join(out_dir, "drift_ralsgan_c1.json"), "w") as f:
+        with open(os.path.join(out_dir, f"drift_{name}.json"), "w") as f:
             json.dump({"report": report, "gpu": {k: v.tolist() for k, v in g.items()},
-                       "ref8": {k: r8[k].tolist() for k in TRAJ_Q}, "env": env.tolist(),
+                       "ref8": {k: r8[k].tolist() for k in qs}, "env": env.tolist(), "threads": sorted(ref),
                        "ENV_MULT": ENV_MULT, "ENV_LAG": ENV_LAG, "STEP_REL": STEP_REL, "MEAN_MULT": MEAN_MULT}, f)
     assert not errs, "\n".join(errs)

@@ -171,7 +171,8 @@ def test_conv_bias_act(K):
 # arch 1's Conv2d layers with a bias (GLI:202-223, 260-302) at the C4 bench shapes (2B = 64):
 # FAST weight gradients, split-K and unsplit, 128 x 128 and 128 x 64 tiles
 WGRAD_BIAS = [(64, 64, 128, 16, 3, 1, 1), (64, 64, 64, 32, 4, 2, 1), (64, 256, 512, 4, 3, 1, 1),
-              (64, 128, 256, 8, 3, 1, 1), (2, 64, 128, 4, 3, 1, 1), (8, 128, 128, 32, 4, 2, 1)]
+              (64, 128, 256, 8, 3, 1, 1), (2, 64, 128, 4, 3, 1, 1), (8, 128, 128, 32, 4, 2, 1),
+              (64, 3, 64, 32, 3, 1, 1)]  # arch 1's image input layer (N = 27: the 64 x 64 tile, round 6)
 
 
 @pytest.mark.parametrize("case", WGRAD_BIAS)
@@ -547,15 +548,38 @@ BN_EPI = [
 @pytest.mark.parametrize("case", BN_EPI)
 def test_conv_bn_epilogue_stats(K, case):
     """rgan_conv_fwd_bn + rgan_bn_segment_stats == rgan_conv_fwd + rgan_bn_stats (fp64 torch)."""
-    from relativisticgan_amd.kernels import ConvGeom
     B, cin, cout, H, tr, segs, expect_fused = case
+    _bn_epilogue_case(K, B, cin, cout, H, (4, 2, 1), tr, segs, expect_fused, bias=False)
+
+
+# the 64 x 64 tiles of arch 1's small GEMMs (C4; round 6: their scalar epilogue emits the
+# segment sums too): (B, cin, cout, H, (k, stride, pad), transposed, segs)
+BN_EPI_SMALL = [
+    (64, 64, 128, 16, (3, 1, 1), False, 2),   # D's 3x3 64 -> 128 at 16x16, batched halves
+    (32, 128, 64, 16, (4, 2, 1), True, 1),    # G's ConvT 128 -> 64, 16 -> 32 (4 phases)
+    (64, 3, 64, 32, (3, 1, 1), False, 2),     # D's image layer 3 -> 64 (K = 27)
+    (32, 64, 128, 16, (3, 1, 1), False, 1),   # the WGAN-GP D(x_hat) call of the first case
+]
+
+
+@pytest.mark.parametrize("case", BN_EPI_SMALL)
+def test_conv_bn_epilogue_stats_small_tiles(K, case):
+    """The same on the 64 x 64 tiles, with the arch-1 conv bias (GLI:260-302)."""
+    B, cin, cout, H, kgeo, tr, segs = case
+    _bn_epilogue_case(K, B, cin, cout, H, kgeo, tr, segs, True, bias=True)
+
+
+def _bn_epilogue_case(K, B, cin, cout, H, kgeo, tr, segs, expect_fused, bias):
+    from relativisticgan_amd.kernels import ConvGeom
     torch.manual_seed(11)
-    g = ConvGeom(4, 2, 1, tr)
+    k = kgeo[0]
+    g = ConvGeom(k, kgeo[1], kgeo[2], tr)
     x = _nhwc(torch.randn(B, cin, H, H, device=DEV))
-    w = torch.randn((cin, cout, 4, 4) if tr else (cout, cin, 4, 4), device=DEV) * 0.05 + 0.01
-    y, part, S = K.conv_fwd_bn(x, w, g, segs=segs)
+    w = torch.randn((cin, cout, k, k) if tr else (cout, cin, k, k), device=DEV) * 0.05 + 0.01
+    bvec = torch.randn(cout, device=DEV) * 0.1 if bias else None
+    y, part, S = K.conv_fwd_bn(x, w, g, bias=bvec, segs=segs)
     assert (part is not None) == expect_fused
-    y_ref = K.conv_fwd(x, w, g)
+    y_ref = K.conv_fwd(x, w, g, bias=bvec)
     assert torch.equal(y, y_ref)  # the epilogue statistics do not touch the stored output
     Bs = B // segs
     for k in range(segs):
@@ -1045,6 +1069,71 @@ def test_bn_two_segments_one_launch(K):
     a2 = K.bn_apply_segments(y, st2, gamma, beta, "lrelu", 0.2, out=torch.empty_like(y))
     assert torch.equal(st1, st2) and torch.equal(a1, a2)
     assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2) and int(n2.item()) == 2
+
+
+@pytest.mark.parametrize("B,cin,H,cout,tr,nseg", [
+    (16, 32, 8, 128, False, 2),     # 4x4 output, 2 x 2 segments: one launch
+    (16, 32, 8, 128, False, 1),
+    (16, 32, 32, 64, False, 2),     # 16x16 output, 2 x 32 segments: one launch
+    (32, 512, 4, 256, True, 1),     # ConvT (4 phase GEMMs; C4's G layer 1), 8x8 output, 32 segments
+    (32, 32, 64, 128, False, 2),    # 32x32 output, 2 x 256 segments: merge + apply launches
+])
+def test_bn_segment_apply_one_call(K, B, cin, H, cout, tr, nseg):
+    """rgan_bn_segment_apply (segment statistics + normalisation + LeakyReLU in one call; one
+    launch up to 64 segments per batch segment, whose blocks each merge their channels' sums)
+    == rgan_bn_segment_stats_n + rgan_bn_apply_segments: stats / output / running statistics
+    within 1e-6 (the one-launch merge adds the segments' double sums in another order: equal
+    after rounding to fp32 but for rare ties) and bitwise on the two-launch path;
+    num_batches_tracked counted once per batch segment."""
+    from relativisticgan_amd.kernels import ConvGeom
+    torch.manual_seed(29)
+    g = ConvGeom(4, 2, 1, tr)
+    x = _nhwc(torch.randn(B, cin, H, H, device=DEV))
+    w = torch.randn(cin, cout, 4, 4, device=DEV) * 0.05 if tr else torch.randn(cout, cin, 4, 4, device=DEV) * 0.05
+    y, part, S = K.conv_fwd_bn(x, w, g, segs=nseg)
+    assert part is not None
+    C = cout
+    gamma, beta = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+    rm1, rv1, n1 = torch.randn(C, device=DEV), torch.rand(C, device=DEV) + 0.5, torch.zeros((), dtype=torch.long, device=DEV)
+    rm2, rv2, n2 = rm1.clone(), rv1.clone(), n1.clone()
+    st1 = torch.empty(nseg, 2 * C, device=DEV)
+    K.bn_segment_stats_n(part, S, nseg, C, 1e-5, 0.1, rm1, rv1, n1, out=st1)
+    a1 = K.bn_apply_segments(y, st1, gamma, beta, "lrelu", 0.2, out=torch.empty_like(y))
+    st2 = torch.full((nseg, 2 * C), float("nan"), device=DEV)
+    a2 = K.bn_segment_apply(part, S, y, 1e-5, 0.1, rm2, rv2, n2, gamma, beta, "lrelu", 0.2, st2, torch.empty_like(y))
+    one_launch = S // nseg <= 64
+    same = (lambda a, b: torch.allclose(a, b, rtol=1e-6, atol=1e-6)) if one_launch else torch.equal
+    assert same(st1, st2) and same(a1, a2)
+    assert same(rm1, rm2) and same(rv1, rv2) and int(n2.item()) == nseg
+
+
+@pytest.mark.parametrize("C,B,H", [(256, 32, 4), (128, 32, 8), (64, 32, 16), (64, 32, 32), (36, 8, 8)])
+def test_bn_backward_sums_apply_one_call(K, C, B, H):
+    """rgan_bn_backward_sums_apply (the WGAN-GP engine's BatchNorm backward: sums kept, + add,
+    affine gradients accumulated) == rgan_bn_backward_sums + rgan_bn_backward_apply_ex: within
+    1e-6 on the one-launch small-layer kernel (<= 2048 rows, C % 16 == 0: its double sums
+    associate differently), bitwise on the two-call path."""
+    torch.manual_seed(31)
+    P = B * H * H
+    small = P <= 2048 and C % 16 == 0
+    same = (lambda a, b: torch.allclose(a, b, rtol=1e-6, atol=1e-6)) if small else torch.equal
+    for act, with_add in (("lrelu", True), ("relu", False), ("tanh", True)):
+        y = _nhwc(torch.randn(B, C, H, H, device=DEV))
+        da = _nhwc(torch.randn(B, C, H, H, device=DEV))
+        add = _nhwc(torch.randn(B, C, H, H, device=DEV)) if with_add else None
+        stats = torch.cat([torch.randn(C, device=DEV), torch.rand(C, device=DEV) + 0.5])
+        gamma, beta = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV)
+        g0, b0 = torch.randn(C, device=DEV), torch.randn(C, device=DEV)
+        dg1, db1 = g0.clone(), b0.clone()
+        sums1, da_c = K.bn_backward_sums(da, y, stats, gamma, beta, act, 0.2)
+        dy1 = K.bn_backward_apply_ex(da_c, y, stats, gamma, beta, act, 0.2, sums1, P,
+                                     add=add.clone() if add is not None else None, dgamma=dg1, dbeta=db1,
+                                     accumulate_affine=True)
+        dg2, db2 = g0.clone(), b0.clone()
+        out = add.clone() if add is not None else None  # in place over the addend, as the GP engine runs it
+        sums2, dy2 = K.bn_backward_sums_apply(da, y, stats, gamma, beta, act, 0.2, add=out, out=out, dgamma=dg2,
+                                              dbeta=db2, accumulate_affine=True)
+        assert same(sums1, sums2) and same(dy1, dy2) and same(dg1, dg2) and same(db1, db2), (act, with_add)
 
 
 @pytest.mark.parametrize("C,B,H", [(64, 8, 32), (64, 8, 16), (1024, 64, 4), (4096, 64, 4), (64, 16, 16), (36, 8, 8)])

@@ -39,6 +39,60 @@ def test_oracle_bitwise_matches_reference(name):
     assert not bad, f"{len(bad)} tensors differ, e.g. {bad[:8]}"
 
 
+# leading iterations of each reference trajectory the oracle replays in the CPU suite (seconds
+# each at 8 threads: C2 ~6 s per iteration, C5 ~3 s, C1 0.5 s, C4 0.2 s)
+TRAJ_PIN_ITERS = {"ralsgan_c1": 4, "wgangp_c4": 8, "rasgan_c2": 1, "rahinge_spectral_c5": 2}
+
+
+@pytest.mark.parametrize("name", sorted(TRAJ_PIN_ITERS))
+def test_oracle_matches_reference_trajectory(name):
+    """The drift tests' envelope comes from the unmodified reference's scalar trajectories
+    (tests/golden/traj_<name>_t<threads>.npz, make_golden.py --trajectory).
+    The oracle replays the leading iterations at 8 threads and reproduces the 8-thread
+    trajectory bitwise: losses, mean D outputs of both steps, the draws' sums and every net's
+    parameter sum after its Adam step -- the trajectories record what the oracle computes."""
+    import os
+    import torch
+    from oracle.reference_cpu import Trainer
+    from tests.golden.configs import TRAJECTORIES
+    from tests.oracle_replay import GOLDEN_DIR, dataset_for, param_for
+    assert 8 in TRAJECTORIES[name]
+    d = np.load(os.path.join(GOLDEN_DIR, f"traj_{name}_t8.npz"), allow_pickle=False)
+    n = TRAJ_PIN_ITERS[name]
+    torch.set_num_threads(8)
+    got = {k: np.full(n, np.nan) for k in d.files if k != "meta.json"}
+    cur = {}
+    holder = {}
+
+    def wsum(net):
+        return float(sum(q.detach().double().sum() for q in net.parameters()))
+
+    def hooks(tag, r):
+        i, t = cur["i"], holder["t"]
+        if tag == "D.post":
+            got["errD"][i] = float(r["errD"])
+            got["D.y_pred"][i] = float(r["y_pred"].double().mean())
+            got["D.y_pred_fake"][i] = float(r["y_pred_fake"].double().mean())
+            got["D.x"][i] = float(r["x"].double().sum())
+            got["D.z"][i] = float(r["z"].double().sum())
+            got["D.wsum"][i] = wsum(t.D)
+        elif tag == "G.post":
+            got["errG"][i] = float(r["errG"])
+            if "y_pred" in r:
+                got["G.y_pred"][i] = float(r["y_pred"].double().mean())
+                got["G.x"][i] = float(r["x"].double().sum())
+            got["G.y_pred_fake"][i] = float(r["y_pred_fake"].double().mean())
+            got["G.z"][i] = float(r["z"].double().sum())
+            got["G.wsum"][i] = wsum(t.G)
+    t = Trainer(param_for(name), dataset_for(name), hooks=hooks)
+    holder["t"] = t
+    for i in range(n):
+        cur["i"] = i
+        t.iteration(i)
+    for k, v in got.items():
+        np.testing.assert_array_equal(v, d[k][:n], err_msg=k)
+
+
 def test_oracle_pac2_semantics():
     """PacGAN-2 oracle (parity unpinned, see tests/golden/configs.py): D sees 2B samples
     packed channel-wise, z is drawn for 2B per step, and the G step reuses the D step's

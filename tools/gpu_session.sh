@@ -6,6 +6,9 @@
 #   pmc[=W]         FETCH_SIZE / WRITE_SIZE passes -> TAG/pmc[_W]/traffic.json
 #   convs[=W]       tools/conv_breakdown.py: per-call GEMM time by layer shape -> TAG/convs[_W].txt
 #   smoke           __graft_entry__.smoke()
+#   pytest=F~K      pytest tests/F -k K ('+' for spaces; gpu + gpu_emu markers) -> TAG/pytest_*.log
+#   trace=W         tools/abi_trace.py W: the C-ABI calls of one eager iteration -> TAG/trace_W.txt
+#   steady=W        rocprof at 10 and 30 eager steps -> TAG/steady_W.txt (dispatches per iteration)
 # Default steps: tests bench prof pmc.  Stops at the first step that faults, aborts,
 # segfaults or times out (each step has its own time limit).
 set -u
@@ -40,5 +43,25 @@ for s in $steps; do
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1
       rc=$?; echo "smoke rc=$rc"; tail -2 "$out/smoke.log"; stop $rc smoke ;;
+    pytest=*)
+      # pytest=FILE[::TEST]~KEXPR (tests/ prefix implied; ~ separates the -k expression)
+      spec=${s#pytest=}; k=${spec#*~}; [ "$k" = "$spec" ] && k=""; f=${spec%%~*}; k=${k//+/ }
+      n=$(echo "$f$k" | tr -c 'A-Za-z0-9_' '_' | cut -c1-60)
+      RGAN_PARITY_AUDIT=$out/parity timeout -k 10 900 python -u -m pytest "tests/$f" -m "gpu or gpu_emu" ${k:+-k "$k"} -v \
+        --timeout 300 --timeout-method thread -p no:cacheprovider --durations=15 > "$out/pytest_$n.log" 2>&1
+      rc=$?; echo "pytest $f ${k} rc=$rc"; grep -E "PASSED|FAILED|ERROR|SKIPPED" "$out/pytest_$n.log" | tail -40
+      tail -2 "$out/pytest_$n.log"; stop $rc pytest ;;
+    trace=*)
+      timeout -k 10 300 python -u tools/abi_trace.py $w > "$out/trace_$w.txt" 2>&1
+      rc=$?; echo "trace $w rc=$rc"; tail -1 "$out/trace_$w.txt"; stop $rc trace ;;
+    steady=*)
+      # steady-state dispatches / kernel time per iteration: rocprof at 10 and 30 eager steps
+      for n in 10 30; do
+        timeout -k 10 450 tools/profile_bench.sh "$out/prof${n}_$w" --steps $n --warmup 3 --no-cpu-baseline \
+          --no-emu-extra --no-dp-path --no-host-draws --no-hbm --graph off --extra= --workload $w
+        rc=$?; [ $rc = 0 ] || { echo "steady $w rc=$rc"; stop $rc steady; exit $rc; }
+      done
+      python3 tools/steady_dispatch.py "$out/prof10_$w/summary.txt" 10 "$out/prof30_$w/summary.txt" 30 \
+        > "$out/steady_$w.txt"; head -12 "$out/steady_$w.txt" ;;
   esac
 done
