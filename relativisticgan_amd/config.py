@@ -71,7 +71,8 @@ def make_parser(script="GAN_losses_iter"):
                    help="2 = PacGAN-2, the reference's code/GAN_losses_iter_PAC.py (D sees 2 samples packed "
                         "channel-wise)")
     p.add_argument("--rgan_perf_log", type="bool", default=True,
-                   help="after each reference log line, a line with img/s and MFMA%% since the previous one")
+                   help="after each reference log line, a line with img/s and MFMA%% of the training "
+                        "iterations since the previous one (sample PNGs, checkpoints and extra images excluded)")
     p.add_argument("--rgan_synthetic", type=int, default=0,
                    help="use N synthetic images instead of an image folder (no torchvision here)")
     return p

@@ -1010,7 +1010,10 @@ extern "C" int rgan_bn_backward_sums_apply(const float* da, const float* y, long
                                            int accumulate_affine, double* sums, void* partial, void* stream) {
   RGAN_REQUIRE(act_ok(act));
   RGAN_REQUIRE(da && y && stats && dy && sums && partial && P > 0 && C > 0);
-  if (P <= BNS_MAX_ROWS && C % BNS_CH == 0 && dense_nhwc(C, 1, C, y) && dense_nhwc(C, 1, C, da) &&
+  // one launch only with >= 64 channel-group blocks: at C = 128-256 (8-16 blocks, the WGAN-GP
+  // engine's arch-1 layers) bn_bwd_small measured 25-28 us per call against ~18 us for the
+  // three launches below (run r6d)
+  if (P <= BNS_MAX_ROWS && C % BNS_CH == 0 && C / BNS_CH >= 64 && dense_nhwc(C, 1, C, y) && dense_nhwc(C, 1, C, da) &&
       dense_nhwc(C, 1, C, dy) && (!add || dense_nhwc(C, 1, C, add))) {  // small layers: one launch
     bn_bwd_small<1><<<C / BNS_CH, BNS_THREADS, 0, (hipStream_t)stream>>>(da, y, P, C, stats, gamma, beta, act,
                                                                          act_alpha, dy, dgamma, dbeta, add,

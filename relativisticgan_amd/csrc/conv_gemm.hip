@@ -92,7 +92,8 @@ struct GemmArgs {
   // FAST paths (raw buffer loads, scalar per-tile offsets): descriptor sizes in bytes
   int a_bytes, im_bytes, bw_bytes;
   int vec_out;            // output n-quads contiguous and 16-B aligned (host-checked)
-  int xgroup, nph;        // XCD-grouped tile order (1: blocks sharing A rows on one XCD, 2: sharing weight columns); phases
+  int xgroup, nph;        // tile order (0: default; 2: blocks sharing weight columns on one XCD; 3: band order,
+                          // each XCD a contiguous eighth of the m tiles); phases
   double* bnp;            // nullable: BatchNorm moments of every 64-row output segment (vector epilogue)
   int accum;              // WGRAD: add into C (gradient accumulation) instead of overwriting it
   // FAST conv WGRAD with a bias (rgan_conv_wgrad dbias): the bias gradient sum_p dy[p][m] is
@@ -201,10 +202,11 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = (wid / WN) * (BM / WM), wn = (wid % WN) * (BN / WN);
-  // Tile order.  Default: x = (m tile, n tile), z = (phase, split).  xgroup: blocks are
-  // dispatched round-robin over the 8 XCDs, so the blocks that read the same A rows (the
-  // n tiles and sub-pixel phases of one m tile) are put 8 dispatch slots apart -- one XCD,
-  // one L2 -- instead of on 4-8 different L2s.  xgroup 2 (layers whose weights outweigh
+  // Tile order.  Default: x = (m tile, n tile), z = (phase, split).  Blocks are dispatched
+  // round-robin over the 8 XCDs, so blocks that read the same operand rows are put 8 dispatch
+  // slots apart -- one XCD, one L2 -- instead of on 4-8 different L2s.  (The first such
+  // order, xgroup 1 -- the n tiles and phases of one m tile on one XCD -- was superseded by
+  // the band order 3 below; tools/patches/xgroup1_row_grouping.diff.)  xgroup 2 (layers whose weights outweigh
   // their input: the deep D convs, G's deep data gradients / ConvTs): the blocks that read
   // the same weight columns (the m tiles and phases of one n tile) share an XCD instead, so
   // the weight is fetched into one L2 rather than into every L2 once per m tile.
@@ -224,14 +226,6 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
     const int b = blockIdx.x, r = b >> 3, per = g.tiles_n * g.nph;
     const int q = r % per;
     tm_i = (b & 7) * ((g.M + BM - 1) / BM / 8) + r / per;
-    tn_i = q % g.tiles_n;
-    phase = q / g.tiles_n;
-    split = blockIdx.z;
-    z = phase * g.splits + split;
-  } else if (g.xgroup) {
-    const int b = blockIdx.x, r = b >> 3, per = g.tiles_n * g.nph;
-    const int q = r % per;
-    tm_i = (r / per) * 8 + (b & 7);
     tn_i = q % g.tiles_n;
     phase = q / g.tiles_n;
     split = blockIdx.z;
@@ -889,8 +883,9 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
 
   if constexpr (SWZ) {
     if (db_on) {
-      // the 8 threads staging the same channel quad (pixel slots t8 = ((tid >> 3) & 3) +
-      // 4 (tid >> 7)) -> one double per channel, t8 in order (the main loop's last barrier has
+      // the NT8 = 1024 / BM threads staging the same channel quad (pixel slots t8 =
+      // ((tid >> 3) & 3) + 4 ((tid >> 5) / (BM / 32)): 8 slots for 128-row tiles, 16 for the
+      // 64-row ones) -> one double per channel, t8 in order (the main loop's last barrier has
       // retired every stage read; the epilogue reuses smem after the second barrier)
       double* dsh = reinterpret_cast<double*>(smem);
       constexpr int NT8 = 1024 / BM;  // threads staging one channel quad

@@ -116,11 +116,22 @@ class _PackCache:
 
     @staticmethod
     def _weight(ent):
-        """The packed weight of an entry (its base parameter, or the view of it that was packed)."""
+        """The packed weight of an entry (its base parameter, or the view of it that was packed),
+        or None when the entry is stale: the base is gone, or its storage no longer covers the
+        saved view (e.g. ``p.data = smaller``) -- such an entry is never a valid layout source."""
         base = ent[0]()
         if base is None or ent[6] is None:
             return base
-        return base.as_strided(*ent[6])
+        shape, stride, offset = ent[6]
+        extent = offset + 1 + sum((n - 1) * st for n, st in zip(shape, stride))  # elements, all n >= 1
+        if any(n == 0 for n in shape) or base.untyped_storage().nbytes() < extent * base.element_size():
+            return None
+        return base.as_strided(shape, stride, offset)
+
+    def _stale(self, key, ent):
+        """Drop an entry whose weight view can no longer be rebuilt (see _weight)."""
+        if ent[0]() is not None and self.entries.get(key) is ent:
+            del self.entries[key]
 
     def refresh(self, params):
         """Repack, in one batched launch, every cached layout of ``params`` whose weight
@@ -128,9 +139,12 @@ class _PackCache:
         current instead of packing one launch at a time."""
         ids = {id(p) for p in params}
         todo = []
-        for key, ent in self.entries.items():
+        for key, ent in list(self.entries.items()):
             base, w = ent[0](), self._weight(ent)
-            if base is None or w is None or id(base) not in ids:
+            if base is not None and w is None:
+                self._stale(key, ent)
+                continue
+            if base is None or id(base) not in ids:
                 continue
             if ent[1] == w._version and ent[3] == w.data_ptr():
                 continue
@@ -153,9 +167,12 @@ class _PackCache:
         rgan_adam_packed, which rewrites them with the new values)."""
         idx = {id(p): i for i, p in enumerate(params)}
         out = []
-        for key, ent in self.entries.items():
+        for key, ent in list(self.entries.items()):
             base, w = ent[0](), self._weight(ent)
-            if base is None or w is None or id(base) not in idx or w.data_ptr() != params[idx[id(base)]].data_ptr():
+            if base is not None and w is None:
+                self._stale(key, ent)
+                continue
+            if base is None or id(base) not in idx or w.data_ptr() != params[idx[id(base)]].data_ptr():
                 continue
             if w.numel() != params[idx[id(base)]].numel():
                 continue

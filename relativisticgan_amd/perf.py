@@ -59,12 +59,21 @@ class ThroughputMeter:
         self.images = trainer.p.batch_size  # global batch per iteration
         self.t0 = None
         self.i0 = None
+        self.excluded = 0.0
+
+    def exclude(self, seconds):
+        """Leave ``seconds`` of host-side output work (sample-grid PNGs, checkpoint files, the
+        extra-image dump: GLI:565, 729-770) out of the current interval, so the line reports
+        training throughput -- the same iterations bench.py times (the caller synchronises the
+        device before starting that clock, so no training work is excluded)."""
+        self.excluded += seconds
 
     def tick(self, i, now):
         line = None
-        if self.t0 is not None and i > self.i0 and now > self.t0:
-            it_s = (i - self.i0) / (now - self.t0)
+        span = (now - self.t0 - self.excluded) if self.t0 is not None else 0.0
+        if self.t0 is not None and i > self.i0 and span > 0:
+            it_s = (i - self.i0) / span
             # img/s of the whole job; MFMA% of this GPU (every rank runs the same share)
             line = "[%d] img/s: %.1f MFMA%%: %.1f" % (i, it_s * self.images, 100.0 * it_s * self.flops / FP32_MFMA_PEAK)
-        self.t0, self.i0 = now, i
+        self.t0, self.i0, self.excluded = now, i, 0.0
         return line

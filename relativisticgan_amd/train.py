@@ -481,12 +481,26 @@ def main(argv=None):
     meter = ThroughputMeter(t) if p.rgan_perf_log else None
     if meter is not None:
         meter.tick(iter_offset, time.time())
+    def output_clock():
+        """Start of host-side output work left out of the perf line's interval (the device
+        finishes the queued training work first, so none of it is excluded)."""
+        if meter is None:
+            return None
+        torch.cuda.synchronize()
+        return time.time()
+
+    def output_done(t_out):
+        if t_out is not None:
+            meter.exclude(time.time() - t_out)
+
     for i in range(iter_offset, p.n_iter):
         t.iteration(i)
         if i % p.print_every == 0:  # GLI:563-565 (the sample batch was drawn inside the iteration)
+            t_out = output_clock()
             grid = _gather_batch(t.fake_test)
             if lead:
                 save_image(grid, os.path.join(base, "images", "fake_samples_iter%05d.png" % i), normalize=True)
+            output_done(t_out)
         if (i + 1) % p.print_every == 0:
             say(t.log_line(i, time.time() - start))  # the reference's line, unchanged (GLI:723-726)
             if meter is not None:  # SURVEY §5: plus img/s and MFMA%, on a line of its own
@@ -494,6 +508,7 @@ def main(argv=None):
                 if perf:
                     say(perf)
         if (i + 1) % p.gen_every == 0:
+            t_out = output_clock()
             current_set_images += 1
             if p.save:
                 st = t.state(i + 1, current_set_images)  # collective under DP (z_test shards)
@@ -504,6 +519,7 @@ def main(argv=None):
             if p.gen_extra_images > 0:
                 t.flush()
                 generate_extra_images(t.G, p, "%s/%01d/" % (p.extra_folder, current_set_images))
+            output_done(t_out)
     t.flush()
     if log:
         log.close()

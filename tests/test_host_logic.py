@@ -68,7 +68,36 @@ def test_throughput_meter_line():
 
     m = perf.ThroughputMeter.__new__(perf.ThroughputMeter)
     m.flops, m.images, m.t0, m.i0 = 1.573e12, 32, None, None
+    m.excluded = 0.0
     assert m.tick(0, 10.0) is None          # first point: nothing to report yet
     line = m.tick(10, 12.0)                 # 10 iterations in 2 s = 5 it/s
     assert line == "[10] img/s: 160.0 MFMA%%: %.1f" % (100.0 * 5 * 1.573e12 / perf.FP32_MFMA_PEAK)
+    # host-side output work (sample PNG, checkpoint) is left out of the interval
+    m.exclude(1.5)
+    line = m.tick(20, 16.0)                 # 10 iterations in 4 s - 1.5 s = 4 it/s
+    assert line == "[20] img/s: 128.0 MFMA%%: %.1f" % (100.0 * 4 * 1.573e12 / perf.FP32_MFMA_PEAK)
     assert perf.FP32_MFMA_PEAK == 157.3e12  # (the meter on a real trainer: tests/test_cli_gpu.py)
+
+
+def test_pack_cache_drops_views_of_shrunk_storage():
+    """kernels._PackCache keeps, per packed view of a parameter (arch 1's dense layers viewed as
+    convolutions), the view's geometry on its base.  When the parameter's storage is later
+    swapped for a smaller one (``p.data = ...``), rebuilding that view would read past the
+    storage: _weight returns None and refresh / layouts_of drop the entry instead of raising
+    inside the optimizer step (advisor, round 5)."""
+    import weakref
+    from relativisticgan_amd import kernels as K
+    cache = K._PackCache()
+    p = torch.nn.Parameter(torch.randn(8192, 128))
+    view = p.view(512, 4, 4, 128)
+    geo = (tuple(view.shape), tuple(view.stride()), view.storage_offset())
+    key = ("k",)
+    ent = (weakref.ref(p), p._version, torch.empty(4), p.data_ptr(), None, 0, geo)
+    cache.entries[key] = ent
+    assert cache._weight(ent) is not None and tuple(cache._weight(ent).shape) == (512, 4, 4, 128)
+    p.data = torch.randn(16, 128)  # smaller storage under the same parameter
+    assert cache._weight(ent) is None
+    assert cache.layouts_of([p]) == [] and key not in cache.entries
+    cache.entries[key] = ent
+    cache.refresh([p])  # no lib call: nothing current to repack
+    assert key not in cache.entries
