@@ -115,3 +115,21 @@ def test_bench_forced_dp_over_rccl_one_rank(workload, mode):
     d = _line(r.stdout)
     assert d["n_gpus"] == 1 and d["config"]["forced_dp"] is True and d["config"]["launch_mode"] == mode
     assert d["value"] > 0
+
+
+def test_bench_configs2_job_shape_eight_ranks():
+    """BASELINE configs[2]'s job shape -- RaLSGAN 256^2, 8 ranks x 32 = batch 256, h = z = 128 --
+    through the driver's own command (plain `bench.py --gpus 8`, which starts the ranks), the
+    8 ranks sharing the one GPU over gloo (RCCL needs one device per rank): every rank builds
+    the 366M-parameter nets, runs the batched D pass and the bucketed gradient SUM all-reduce of
+    both nets, and rank 0 reports the 8-rank line (run r6f: 2.8 s per step on the shared GPU)."""
+    env = _env()
+    env["RGAN_BENCH_BACKEND"] = "gloo"
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "8", "--workload", "C3", "--extra=", "--steps", "2",
+                        "--warmup", "1"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=500)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "dp8" and d["config"]["global_batch"] == 256
+    assert d["config"]["image_size"] == 256 and d["config"]["G_h_size"] == 128 and d["config"]["batched_D_step"]
+    assert d["config"]["process_group"]["world_size"] == 8 and d["value"] > 0
