@@ -617,7 +617,11 @@ extern "C" int rgan_bn_segment_apply(const double* part, long long S, int nseg, 
                S % nseg == 0 && P % nseg == 0 && P == S * (long long)seg_rows);
   const BnGeo g = bn_geo(P, C, C, 1);
   RGAN_REQUIRE(g.vec && ((uintptr_t)y & 15) == 0 && ((uintptr_t)a & 15) == 0);
-  if (S / nseg > SA_MAX_SEGS) {  // large layer: merge once, then apply
+  // one launch only where it measured faster than the two (tools/bn_small_micro.py, run r6g, graph
+  // replays): a single batch segment of <= 2^18 elements (512 x 256: 6.1 vs 6.7 us; 2048 x 128:
+  // 6.4 vs 6.8); at 2048 x 256 (7.3 vs 6.8) and every two-segment call (1024-4096 rows: 9.8-12.5
+  // vs 9.3-9.6) the serial in-block merge costs more than the launch it saves
+  if (S / nseg > SA_MAX_SEGS || nseg != 1 || P * C > (1LL << 18)) {  // merge once, then apply
     int rc = rgan_bn_segment_stats_n(part, 0, S, nseg, C, seg_rows, eps, momentum, running_mean, running_var,
                                      num_batches_tracked, stats, stream);
     if (rc) return rc;
