@@ -1894,10 +1894,11 @@ __global__ __launch_bounds__(256) void conv3_narrow_out(NarrowArgs a) {
 // its 4 x NC outputs over the block's pixels in order from LDS.  The per-block partials go to a
 // slab in the WGRAD GEMM's [split][co][(kh, kw, ci)] layout, which splitk_reduce(_wide) adds in
 // block order into torch layout (and into .grad when accumulating).  As a GEMM this is M = NC:
-// a 128 x 128 tile >= 97 % padding (88 us per C4 call; 42 us here, incl. the reduce).  The
+// a 128 x 128 tile >= 97 % padding (88 us per C4 call; here 14.7 us + the reduce).  The
 // mirror case (<= 4 input channels, arch 1's input layer) stays on the GEMM: the same staging
 // measured 40 us per call against its 29 us (K = 9 NC is only short, M is full).
 constexpr int N3W_PIX = 128;
+constexpr int N3W_UNR = 8;  // x-halo float4 loads in flight per thread
 template <int NC>
 __global__ void wgrad3_narrow(NarrowArgs a, int CW, int R) {
   extern __shared__ __attribute__((aligned(16))) float sm3[];
@@ -1909,12 +1910,34 @@ __global__ void wgrad3_narrow(NarrowArgs a, int CW, int R) {
   const int tid = threadIdx.x, nt = blockDim.x;
   // stage: x rows oh0 - 1 .. oh0 + nr (zero outside the image), dy rows oh0 .. oh0 + nr - 1
   const int xn = (R + 2) * XW * CW;
-  for (int i = tid; i < xn; i += nt) {
-    const int c = i % CW, pix = i / CW, rr = pix / XW, cc = pix - rr * XW;
-    const int ih = oh0 - 1 + rr, iw = cc - 1;
-    xs[i] = (rr < nr + 2 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
-                ? a.x[(long long)b * a.xsb + (long long)c * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
-                : 0.f;
+  if (a.xsc == 1 && ((a.xsw | a.xsh | a.xsb) & 3) == 0 && ((uintptr_t)a.x & 15) == 0) {
+    // NHWC: float4 per (pixel, 4 channels), N3W_UNR loads in flight per thread before the LDS
+    // stores (round 6: the scalar loop below kept ~1 load in flight -- 33.6 us per C4 call)
+    const int CQ = CW / 4, xq = xn / 4;
+    for (int i0 = tid; i0 < xq; i0 += N3W_UNR * nt) {
+      float4 v[N3W_UNR];
+#pragma unroll
+      for (int u = 0; u < N3W_UNR; ++u) {
+        const int i = i0 + u * nt;
+        const int cq = i % CQ, pix = i / CQ, rr = pix / XW, cc = pix - rr * XW;
+        const int ih = oh0 - 1 + rr, iw = cc - 1;
+        v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (i < xq && rr < nr + 2 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+          v[u] = *reinterpret_cast<const float4*>(a.x + (long long)b * a.xsb + (long long)ih * a.xsh +
+                                                  (long long)iw * a.xsw + 4 * cq);
+      }
+#pragma unroll
+      for (int u = 0; u < N3W_UNR; ++u)
+        if (i0 + u * nt < xq) reinterpret_cast<float4*>(xs)[i0 + u * nt] = v[u];
+    }
+  } else {
+    for (int i = tid; i < xn; i += nt) {
+      const int c = i % CW, pix = i / CW, rr = pix / XW, cc = pix - rr * XW;
+      const int ih = oh0 - 1 + rr, iw = cc - 1;
+      xs[i] = (rr < nr + 2 && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W)
+                  ? a.x[(long long)b * a.xsb + (long long)c * a.xsc + (long long)ih * a.xsh + (long long)iw * a.xsw]
+                  : 0.f;
+    }
   }
   const int dn = nr * Wo * NC;
   for (int i = tid; i < dn; i += nt) {
