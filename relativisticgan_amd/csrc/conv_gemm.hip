@@ -1825,64 +1825,122 @@ __global__ __launch_bounds__(256, 2) void conv_narrow_in_mfma(NarrowArgs a) {
   }
 }
 
-// Conv2d 3x3 stride 1 with NC <= 4 output channels over an NHWC input of C channels (C % 16 ==
-// 0, C <= N3_MAXC): arch 1's image layer (GLI:222-223) and, reading the kernel transposed and
-// flipped, the data gradient of arch 1's 3-channel input layer (GLI:202, the WGAN-GP input
-// gradient).  As an implicit GEMM (N = NC) every MFMA would be >= 7/8 padding; here a thread =
-// one output pixel x a quarter of the channels (channels 16 j + 4 q: the four quarters of a
-// pixel read one 64-B run per step), 4 x NC FMAs per loaded float4 against the weights in LDS
-// ([tap][channel] -> float4 of the NC outputs, broadcast reads), then the four quarters are
-// added by a fixed xor butterfly (a + b == b + a: every lane of the group holds the same sum).
+// Conv2d 3x3 stride 1 with NC <= 4 output channels over an NHWC input of C channels (C a power
+// of two, 4 <= C <= 256): arch 1's image layer (GLI:222-223) and, reading the kernel transposed
+// and flipped, the data gradient of arch 1's 3-channel input layer (GLI:202, the WGAN-GP input
+// gradient).  As an implicit GEMM (N = NC) every MFMA would be >= 7/8 padding.  Here L = C / 4
+// lanes share a pixel, lane l owning channels 4 l .. 4 l + 3: it holds their 9 x 4 x NC weights
+// in registers for the whole wave, so a pixel costs each lane 9 float4 loads (the L lanes of a
+// tap read one contiguous C * 4-byte run) and 36 NC FMAs, after which a log2(L)-step xor
+// butterfly adds the lanes (a + b == b + a: every lane of a pixel holds the same sums) and lane
+// o mod L stores output o.  A wave walks `steps` groups of 64 / L pixels, two groups' loads in
+// flight together; waves are independent (no LDS, no barrier).  Round 6: a thread
+// per (pixel, quarter of the channels) ran 9 x C / 16 dependent load -> FMA steps at C4 (C =
+// 128), latency-bound at 14.1 us per call whatever the pixels per thread.
 constexpr int N3_MAXC = 256;
+constexpr int N3_WAVES = 4;  // waves per block
 template <int NC>
-__global__ __launch_bounds__(256) void conv3_narrow_out(NarrowArgs a) {
-  __shared__ float4 ws[9 * N3_MAXC];
-  const int C = a.C;
-  for (int i = threadIdx.x; i < 9 * C; i += 256) {
-    const int t = i / C, c = i - t * C, tw = a.w_flip ? 8 - t : t;
-    float v[4];
-#pragma unroll
-    for (int o = 0; o < 4; ++o) v[o] = o < NC ? a.w[(long long)o * a.w_sn + (long long)c * a.w_sc + tw] : 0.f;
-    ws[i] = make_float4(v[0], v[1], v[2], v[3]);
+__global__ __launch_bounds__(64 * N3_WAVES) void conv3_narrow_out(NarrowArgs a, int steps) {
+  extern __shared__ float wl[];  // [L][9][4][NC]: lane sl's weights contiguous
+  const int C = a.C, L = C >> 2, PW = 64 / L;
+  const int lc = __builtin_ctz(C);  // C is a power of two
+  for (int i = threadIdx.x; i < 9 * C * NC; i += 64 * N3_WAVES) {
+    const int o = i % NC, e = i / NC, c = e & (C - 1), t = e >> lc;  // reads: o fastest, then channel
+    wl[(((c >> 2) * 9 + t) * 4 + (c & 3)) * NC + o] =
+        a.w[o * (int)a.w_sn + c * (int)a.w_sc + (a.w_flip ? 8 - t : t)];
   }
   __syncthreads();
-  const int HW = a.Ho * a.Wo, P = a.B * HW;
-  const int pix = blockIdx.x * 64 + (threadIdx.x >> 2), q = threadIdx.x & 3;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  int b = 0, oh = 0, ow = 0;
-  if (pix < P) {
-    b = pix / HW;
-    const int r = pix - b * HW;
-    oh = r / a.Wo;
-    ow = r - oh * a.Wo;
-    const float* xb = a.x + (long long)b * a.xsb + 4 * q;
+  const int lane = threadIdx.x & 63, sl = lane & (L - 1);
+  const int HW = a.Ho * a.Wo, P = a.B * HW;  // < 2^31 (plan)
+  const int pix0 = (blockIdx.x * N3_WAVES + (threadIdx.x >> 6)) * steps * PW;
+  if (pix0 >= P) return;  // whole wave: no barrier below
+  float w[9][4][NC];
+  {
+    const float* src = wl + sl * 36 * NC;
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int o = 0; o < NC; ++o) w[t][k][o] = src[(t * 4 + k) * NC + o];
+  }
+  const float wsc = a.wscale ? a.wscale[0] : 1.f;
+  float bo[NC];
+#pragma unroll
+  for (int o = 0; o < NC; ++o) bo[o] = a.bias ? a.bias[o] : 0.f;
+  // x through a buffer descriptor: a tap outside the image (or a pixel past P) gets an offset
+  // past the extent and the load returns zeros -- every load unconditional, no branch (a
+  // conditional load is compiled into a branch that waits for it: one load in flight)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
+  const int xsb = 4 * (int)a.xsb, xsh = 4 * (int)a.xsh, xsw = 4 * (int)a.xsw;  // bytes
+  // the lane's pixel (b, oh, ow), advanced by PW per group without a division
+  int pix = pix0 + lane / L, b = pix / HW, r = pix - b * HW, oh = r / a.Wo, ow = r - oh * a.Wo;
+  auto advance = [&]() {
+    pix += PW;
+    ow += PW;
+    while (ow >= a.Wo) {
+      ow -= a.Wo;
+      if (++oh == a.Ho) { oh = 0; ++b; }
+    }
+  };
+  auto load = [&](u32x4 (&xv)[9]) {
+    const int base = b * xsb + (oh - a.pad) * xsh + (ow - a.pad) * xsw + 16 * sl;
+    const bool in = pix < P;
+    bool rok[3], cok[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      rok[k] = in & ((unsigned)(oh + k - a.pad) < (unsigned)a.H);
+      cok[k] = (unsigned)(ow + k - a.pad) < (unsigned)a.W;
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+      xv[t] = __builtin_amdgcn_raw_buffer_load_b128(
+          xr, (rok[t / 3] & cok[t % 3]) ? base + (t / 3) * xsh + (t % 3) * xsw : 0x7ffffff0, 0, 0);
+  };
+  auto finish = [&](const u32x4 (&xv)[9], int pb, int ob, int ohb, int owb) {
+    float acc[NC];
+#pragma unroll
+    for (int o = 0; o < NC; ++o) acc[o] = 0.f;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      const int ih = oh + t / 3 - a.pad, iw = ow + t % 3 - a.pad;
-      if ((unsigned)ih >= (unsigned)a.H || (unsigned)iw >= (unsigned)a.W) continue;
-      const float* xp = xb + (long long)ih * a.xsh + (long long)iw * a.xsw;
-      const float4* wp = ws + t * C + 4 * q;
-      for (int j = 0; j < C; j += 16) {
-        const float4 xv = *reinterpret_cast<const float4*>(xp + j);
-        const float4 w0 = wp[j], w1 = wp[j + 1], w2 = wp[j + 2], w3 = wp[j + 3];
-        acc[0] += xv.x * w0.x + xv.y * w1.x + xv.z * w2.x + xv.w * w3.x;
-        if (NC > 1) acc[1] += xv.x * w0.y + xv.y * w1.y + xv.z * w2.y + xv.w * w3.y;
-        if (NC > 2) acc[2] += xv.x * w0.z + xv.y * w1.z + xv.z * w2.z + xv.w * w3.z;
-        if (NC > 3) acc[3] += xv.x * w0.w + xv.y * w1.w + xv.z * w2.w + xv.w * w3.w;
-      }
+      const float x0 = __uint_as_float(xv[t].x), x1 = __uint_as_float(xv[t].y), x2 = __uint_as_float(xv[t].z),
+                  x3 = __uint_as_float(xv[t].w);
+#pragma unroll
+      for (int o = 0; o < NC; ++o) acc[o] += x0 * w[t][0][o] + x1 * w[t][1][o] + x2 * w[t][2][o] + x3 * w[t][3][o];
     }
-  }
+    for (int m = 1; m < L; m <<= 1)
 #pragma unroll
-  for (int o = 0; o < NC; ++o) {
-    acc[o] += __shfl_xor(acc[o], 1);
-    acc[o] += __shfl_xor(acc[o], 2);
-  }
-  if (pix < P && q == 0) {
-    const float wsc = a.wscale ? a.wscale[0] : 1.f;
-    float* yp = a.y + (long long)b * a.ysb + (long long)oh * a.ysh + (long long)ow * a.ysw;
+      for (int o = 0; o < NC; ++o) acc[o] += __shfl_xor(acc[o], m);
+    if (pb >= P) return;
+    float* yp = a.y + ob * a.ysb + (long long)ohb * a.ysh + (long long)owb * a.ysw;
+    if (L >= NC) {  // lane o stores output o: one activation per lane
+      if (sl < NC) {
+        float v = acc[0], bb = bo[0];
 #pragma unroll
-    for (int o = 0; o < NC; ++o)
-      yp[(long long)o * a.ysc] = act_fwd(acc[o] * wsc + (a.bias ? a.bias[o] : 0.f), a.act, a.alpha);
+        for (int o = 1; o < NC; ++o) {
+          v = sl == o ? acc[o] : v;
+          bb = sl == o ? bo[o] : bb;
+        }
+        yp[(long long)sl * a.ysc] = act_fwd(v * wsc + bb, a.act, a.alpha);
+      }
+    } else {
+#pragma unroll
+      for (int o = 0; o < NC; ++o)
+        if ((o & (L - 1)) == sl) yp[(long long)o * a.ysc] = act_fwd(acc[o] * wsc + bo[o], a.act, a.alpha);
+    }
+  };
+  // two pixel groups per pass: 18 loads in flight, the first group's FMAs waiting only on its own
+  for (int st = 0; st < steps; st += 2) {
+    u32x4 xa[9], xb[9];
+    load(xa);
+    const int pa = pix, ba = b, oha = oh, owa = ow;
+    advance();
+    if (st + 1 >= steps) pix = P;  // odd tail: the second group is empty
+    load(xb);
+    const int pb = pix, bb = b, ohb = oh, owb = ow;
+    advance();
+    finish(xa, pa, ba, oha, owa);
+    finish(xb, pb, bb, ohb, owb);
   }
 }
 
@@ -3092,7 +3150,8 @@ static bool plan_narrow3_out(Plan& p, int batch, const float* x, const long long
                              const float* w, long long w_sn, long long w_sc, int flip, int nc, float* y,
                              const long long* ys, int Ho, int Wo, int pad, const float* wscale, const float* bias,
                              int act, float alpha) {
-  if (nc > 4 || C % 16 != 0 || C > N3_MAXC || xs[1] != 1 || xs[0] % 4 || xs[2] % 4 || xs[3] % 4 || !aligned16(x))
+  if (nc > 4 || C < 4 || C > N3_MAXC || (C & (C - 1)) || xs[1] != 1 || xs[0] % 4 || xs[2] % 4 || xs[3] % 4 ||
+      !aligned16(x))
     return false;
   if (Ho != H + 2 * pad - 2 || Wo != W + 2 * pad - 2) return false;
   p.mode = MODE_NARROW3;
@@ -3103,6 +3162,14 @@ static bool plan_narrow3_out(Plan& p, int batch, const float* x, const long long
   a.y = y; a.ysb = ys[0]; a.ysc = ys[1]; a.ysh = ys[2]; a.ysw = ys[3];
   a.Ho = Ho; a.Wo = Wo; a.Cout = nc; a.stride = 1; a.pad = pad;
   a.bias = bias; a.wscale = wscale; a.act = act; a.alpha = alpha;
+  // pixels per wave: 64 / (C / 4) per step; enough steps to spread the per-wave weight loads,
+  // few enough to leave >= ~8 waves per CU
+  const long long P = (long long)batch * Ho * Wo, pw = 64 / (C / 4);
+  a.rows = (int)std::max(1LL, std::min(16LL, P / (pw * 2048)));
+  // 32-bit pixel indices and a buffer descriptor over x's extent
+  const long long ext = ((long long)(batch - 1) * xs[0] + (long long)(H - 1) * xs[2] + (long long)(W - 1) * xs[3] + C) * 4;
+  if (P + 64LL * (a.rows + 2) >= (1LL << 31) || ext >= 0x7ffffff0LL || xs[0] < 0 || xs[2] < 0 || xs[3] < 0) return false;
+  a.x_bytes = (int)ext;
   p.pack = false;
   return true;
 }
@@ -3496,7 +3563,7 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
     g_kernel_names[54] = "void rgan::gemm_post<1>(rgan::GemmArgs)";
     g_kernel_names[55] = "void rgan::gemm_post_bf16x6<0>(rgan::GemmArgs)";
     g_kernel_names[56] = "void rgan::gemm_post_bf16x6<1>(rgan::GemmArgs)";
-    g_kernel_names[57] = "void rgan::conv3_narrow_out<NC>(rgan::NarrowArgs)";
+    g_kernel_names[57] = "void rgan::conv3_narrow_out<NC>(rgan::NarrowArgs, int)";
     g_kernel_names[58] = "void rgan::wgrad3_narrow<NC>(rgan::NarrowArgs, int, int)";
     for (int m = 0; m < 3; ++m) {
       for (int a = 0; a < 2; ++a)
@@ -3583,12 +3650,14 @@ static int run_narrow(Plan& p, const float* packed, hipStream_t s) {
 static int run_narrow3(Plan& p, hipStream_t s) {
   NarrowArgs a = p.na;
   if (p.mode == MODE_NARROW3) {
-    const unsigned blocks = (unsigned)ceil_div((long long)a.B * a.Ho * a.Wo, 64LL);
+    const long long P = (long long)a.B * a.Ho * a.Wo, PW = 64 / (a.C / 4);
+    const int steps = a.rows;
+    const unsigned blocks = (unsigned)ceil_div(ceil_div(P, PW * steps), (long long)N3_WAVES);
     switch (a.Cout) {
-      case 1: conv3_narrow_out<1><<<blocks, 256, 0, s>>>(a); break;
-      case 2: conv3_narrow_out<2><<<blocks, 256, 0, s>>>(a); break;
-      case 3: conv3_narrow_out<3><<<blocks, 256, 0, s>>>(a); break;
-      default: conv3_narrow_out<4><<<blocks, 256, 0, s>>>(a); break;
+      case 1: conv3_narrow_out<1><<<blocks, 64 * N3_WAVES, 9 * a.C * 1 * 4, s>>>(a, steps); break;
+      case 2: conv3_narrow_out<2><<<blocks, 64 * N3_WAVES, 9 * a.C * 2 * 4, s>>>(a, steps); break;
+      case 3: conv3_narrow_out<3><<<blocks, 64 * N3_WAVES, 9 * a.C * 3 * 4, s>>>(a, steps); break;
+      default: conv3_narrow_out<4><<<blocks, 64 * N3_WAVES, 9 * a.C * 4 * 4, s>>>(a, steps); break;
     }
     return 0;
   }

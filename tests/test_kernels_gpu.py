@@ -1373,6 +1373,31 @@ def test_conv3x3_narrow_layers(K, nc, B, H):
     assert _rel(dw, w64.grad) < 3e-6
 
 
+# conv3_narrow_out's channel-lane layout (C / 4 lanes per pixel, 64 / (C / 4) pixels per wave
+# step, `steps` groups per wave): C = 4 / 8 (fewer lanes than outputs), 16, 128 (C4) and 256 (one
+# pixel per step), ragged pixel counts, pad 0; C = 48 is not a power of two and takes the GEMM.
+@pytest.mark.parametrize("C", [4, 8, 16, 48, 128, 256])
+@pytest.mark.parametrize("B,H,pad", [(3, 17, 1), (32, 32, 1), (2, 9, 0)])
+def test_conv3x3_narrow_channel_widths(K, C, B, H, pad):
+    g = K.ConvGeom(3, 1, pad, False)
+    Ho = H + 2 * pad - 2
+    s = torch.tensor([0.5], device=DEV)
+    for nc in (1, 3, 4):
+        torch.manual_seed(C * 10 + nc + B)
+        x = _nhwc(torch.randn(B, C, H, H, device=DEV))
+        w = torch.randn(nc, C, 3, 3, device=DEV) * 0.1
+        b = torch.randn(nc, device=DEV)
+        y = K.conv_fwd(x, w, g, bias=b, act="tanh", wscale=s, nchw_out=True)
+        assert _rel(y, torch.tanh(_ref_conv(x, w * 0.5, g, b))) < 3e-6, (nc, "fwd")
+        # the mirror: D's nc-channel input layer's data gradient (C-channel dy, flipped taps)
+        w_in = torch.randn(C, nc, 3, 3, device=DEV) * 0.1
+        dy = _nhwc(torch.randn(B, C, Ho, Ho, device=DEV))
+        x64 = torch.zeros(B, nc, H, H, dtype=torch.float64, requires_grad=True)
+        F.conv2d(x64, (w_in * 0.5).double().cpu(), padding=pad).backward(dy.double().cpu())
+        dx = K.conv_dgrad(dy, w_in, g, (B, nc, H, H), wscale=s)
+        assert _rel(dx, x64.grad) < 3e-6, (nc, "dgrad")
+
+
 @pytest.mark.parametrize("B,C,H", [(1, 16, 1), (3, 64, 5), (64, 512, 4), (32, 256, 8), (2, 64, 33), (64, 64, 8),
                                    (8, 20, 4), (64, 128, 16)])
 def test_channel_sum(K, B, C, H):
