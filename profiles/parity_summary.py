@@ -31,8 +31,15 @@ max|gpu - forced| / (RMS(forced) * tol) (must be <= ELEM_FACTOR = 10).
 def main(d, head="", rnd="4"):
     rows, tot, direct, forced = [], 0, 0, 0
     compact = {}
+    drift = []
     for f in sorted(glob.glob(os.path.join(d, "*.json"))):
         r = json.load(open(f))
+        if os.path.basename(f).startswith("drift_"):  # tests/test_drift_gpu.py: a trajectory report
+            worst = max(v["max_gap_over_bound"] for v in r["report"].values())
+            mean = max(v["gpu_mean_gap"] / v["ref_mean_spread"] for v in r["report"].values() if v["ref_mean_spread"])
+            drift.append(f"| {os.path.basename(f)[6:-5]} | {len(r['gpu'].get('errD', r['gpu']))} | "
+                         f"{r.get('threads', '-')} | {worst:.2f} | {mean:.2f} |")
+            continue
         assert r.get("FAIL", 0) == 0, f
         compact[r["config"]] = {k: r.get(k) for k in ("tensors", "direct", "forced", "envelope", "flip", "FAIL",
                                                       "premise_max_abs_over_rms", "worst_elem_vs_forced")}
@@ -49,6 +56,11 @@ def main(d, head="", rnd="4"):
     out = (HEAD.format(rnd=rnd, head=f", head {head}" if head else "") + "\n".join(rows) +
            f"\n\nTotal: {direct} of {tot} tensors direct ({100.0 * direct / tot:.1f} %), "
            f"{direct + forced} direct or against the mask-forced fp64 step ({100.0 * (direct + forced) / tot:.1f} %).\n")
+    if drift:
+        out += ("\nTrajectories vs the reference's thread envelope (tests/test_drift_gpu.py; bound: "
+                "3 x the 2-step-lagged spread of the reference's thread-count runs + 1e-4 scale, per step;"
+                " mean gap <= the mean spread):\n\n| config | iterations | reference threads | worst step "
+                "gap / bound | worst mean gap / mean spread |\n|---|---|---|---|---|\n" + "\n".join(drift) + "\n")
     open(os.path.join(d, "SUMMARY.md"), "w").write(out)
     # compact per-config counts (read by bench.py on the GPU box, where the audit dir is not sent)
     with open(os.path.join(os.path.dirname(os.path.abspath(d)), f"round{rnd}_parity_summary.json"), "w") as fh:
