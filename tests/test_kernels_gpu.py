@@ -243,6 +243,43 @@ def test_conv_dense_one_output(K, case):
     assert _rel(db, dy.double().cpu().sum((0, 2, 3))) < 1e-6
 
 
+@pytest.mark.parametrize("B,C,N", [(32, 128, 8192), (1, 4, 256), (64, 100, 300), (7, 512, 1024), (33, 20, 260)])
+def test_conv_dense_wide(K, B, C, N):
+    """A wide dense layer as a 1x1 conv over a 1x1 map (arch 1's G input Linear, GLI:205-207:
+    dense_wide_fwd / dense_wide_wgrad): fwd with bias, wscale and activation, wgrad + dbias
+    (written, accumulated, into the .grad given), through a weight view as arch 1 calls it,
+    vs torch fp64; ragged N (not a multiple of 32) and B (not of 8)."""
+    g = K.ConvGeom(1, 1, 0, False)
+    torch.manual_seed(B + C)
+    x = torch.randn(B, C, 1, 1, device=DEV)
+    p = torch.nn.Parameter(torch.randn(N, C, device=DEV) * 0.05)
+    w = p.view(N, C, 1, 1)
+    b = torch.randn(N, device=DEV)
+    ws = torch.tensor([0.7], device=DEV)
+    ref = F.conv2d(x.double().cpu(), w.detach().double().cpu() * 0.7, b.double().cpu())
+    for act, fn in [("none", lambda t: t), ("relu", F.relu), ("lrelu", lambda t: F.leaky_relu(t, 0.2))]:
+        y = K.conv_fwd(x, w, g, bias=b, act=act, alpha=0.2, wscale=ws, cache=True)
+        assert y.shape == (B, N, 1, 1)
+        assert _rel(y, fn(ref)) < 3e-6, act
+    dy = torch.randn(B, N, 1, 1, device=DEV)
+    w64 = w.detach().double().cpu().requires_grad_(True)
+    b64 = torch.zeros(N, dtype=torch.float64, requires_grad=True)
+    F.conv2d(x.double().cpu(), w64, b64).backward(dy.double().cpu())
+    dw, db = K.conv_wgrad(x, dy, g, w.shape, with_bias=True)
+    assert _rel(dw, w64.grad) < 2e-6
+    assert _rel(db, b64.grad) < 1e-6
+    dw0, db0 = torch.randn(N, C, 1, 1, device=DEV), torch.randn(N, device=DEV)
+    dwa, dba = dw0.clone(), db0.clone()
+    K.conv_wgrad(x, dy, g, w.shape, with_bias=True, out=dwa, out_bias=dba)
+    assert _rel(dwa, dw0.double().cpu() + w64.grad) < 1e-5
+    assert _rel(dba, db0.double().cpu() + b64.grad) < 1e-6
+    if B >= 2:  # bias over rows [B/2, B): the channel-sum path beside the wide weight gradient
+        dwr, dbr = dw0.clone(), db0.clone()
+        K.conv_wgrad(x, dy, g, w.shape, with_bias=True, out=dwr, out_bias=dbr, bias_row0=B // 2)
+        assert _rel(dwr, dw0.double().cpu() + w64.grad) < 1e-5
+        assert _rel(dbr, db0.double().cpu() + dy[B // 2:].double().cpu().sum((0, 2, 3))) < 1e-6
+
+
 @pytest.mark.parametrize("C", [1, 3, 4])
 @pytest.mark.parametrize("layout", ["nchw", "nhwc"])
 def test_image_layer_patches(K, C, layout):
