@@ -91,6 +91,7 @@ struct GemmArgs {
   float* slab;
   // FAST paths (raw buffer loads, scalar per-tile offsets): descriptor sizes in bytes
   int a_bytes, im_bytes, bw_bytes;
+  int im_buf;             // non-FAST WGRAD: the scalar im2col gathers through the im_bytes descriptor
   int vec_out;            // output n-quads contiguous and 16-B aligned (host-checked)
   int xgroup, nph;        // tile order (0: default; 2: blocks sharing weight columns on one XCD; 3: band order,
                           // each XCD a contiguous eighth of the m tiles); phases
@@ -555,28 +556,46 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
           rb[4 * i + 0] = v.x; rb[4 * i + 1] = v.y; rb[4 * i + 2] = v.z; rb[4 * i + 3] = v.w;
         }
       } else {
+        if (g.im_buf) {
+          // every gather unconditional, a tap outside the image at an offset past the
+          // descriptor (reads 0): a conditional load compiles into a branch that waits for it
+          // -- one gather in flight per thread (round 6: C4's input-layer weight gradient)
 #pragma unroll
-        for (int j = 0; j < B_ELEMS; ++j) {
-          int e = tid + 256 * j;
-          int row = e / BN, col = e - (e / BN) * BN;
-          int p = k0 + row, n = n0 + col;
-          float v = 0.f;
-          if (p < kend && n < g.N) {
-            uint32_t b = g.fghw.div(p);
-            uint32_t rem = p - b * g.fghw.d;
-            uint32_t oi = g.fgw.div(rem);
-            uint32_t oj = rem - oi * g.fgw.d;
-            uint32_t t = g.fC.div(n);
-            int ci = n - t * g.fC.d;
-            uint32_t kh = g.fKW.div(t);
-            int kw = t - kh * g.fKW.d;
-            int ih = (int)oi * g.stride - g.pad + (int)kh;
-            int iw = (int)oj * g.stride - g.pad + kw;
-            if ((unsigned)ih < (unsigned)g.im.H && (unsigned)iw < (unsigned)g.im.W)
-              v = g.im.p[(long long)b * g.im.sb + (long long)ih * g.im.sh + (long long)iw * g.im.sw +
-                         (long long)ci * g.im.sc];
+          for (int j = 0; j < B_ELEMS; ++j) {
+            const int e = tid + 256 * j, row = e / BN, col = e - row * BN, p = k0 + row, n = n0 + col;
+            const bool in = p < kend && n < g.N;
+            const uint32_t b = g.fghw.div(p), rem = p - b * g.fghw.d, oi = g.fgw.div(rem), oj = rem - oi * g.fgw.d;
+            const uint32_t t = g.fC.div(n), kh = g.fKW.div(t);
+            const int ci = n - t * g.fC.d, kw = t - kh * g.fKW.d;
+            const int ih = (int)oi * g.stride - g.pad + (int)kh, iw = (int)oj * g.stride - g.pad + kw;
+            const bool ok = in && (unsigned)ih < (unsigned)g.im.H && (unsigned)iw < (unsigned)g.im.W;
+            const int off = (int)b * (int)g.im.sb + ih * (int)g.im.sh + iw * (int)g.im.sw + ci * (int)g.im.sc;
+            rb[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brsrc, ok ? 4 * off : 0x7ffffff0, 0, 0));
           }
-          rb[j] = v;
+        } else {
+#pragma unroll
+          for (int j = 0; j < B_ELEMS; ++j) {
+            int e = tid + 256 * j;
+            int row = e / BN, col = e - (e / BN) * BN;
+            int p = k0 + row, n = n0 + col;
+            float v = 0.f;
+            if (p < kend && n < g.N) {
+              uint32_t b = g.fghw.div(p);
+              uint32_t rem = p - b * g.fghw.d;
+              uint32_t oi = g.fgw.div(rem);
+              uint32_t oj = rem - oi * g.fgw.d;
+              uint32_t t = g.fC.div(n);
+              int ci = n - t * g.fC.d;
+              uint32_t kh = g.fKW.div(t);
+              int kw = t - kh * g.fKW.d;
+              int ih = (int)oi * g.stride - g.pad + (int)kh;
+              int iw = (int)oj * g.stride - g.pad + kw;
+              if ((unsigned)ih < (unsigned)g.im.H && (unsigned)iw < (unsigned)g.im.W)
+                v = g.im.p[(long long)b * g.im.sb + (long long)ih * g.im.sh + (long long)iw * g.im.sw +
+                           (long long)ci * g.im.sc];
+            }
+            rb[j] = v;
+          }
         }
       }
     }
@@ -1086,6 +1105,29 @@ __device__ __forceinline__ void gemm_body(const GemmArgs& g) {
       const int col = n0 + cl;
       const float bv = (g.bias && col < g.N) ? g.bias[col] : 0.f;
       auto put = [&](auto actf) {
+        if constexpr (MODE == MODE_WGRAD) {
+          // accumulating: the 16 old values first, all in flight, through a descriptor over
+          // dW (rows outside the tile at an offset past it) -- the read-modify-write per
+          // element compiled into 16 dependent round trips
+          if (g.accum && (long long)g.M * g.N * 4 < 0x7ffffff0LL) {
+            const __amdgpu_buffer_rsrc_t crs =
+                __builtin_amdgcn_make_buffer_rsrc((void*)g.C, (short)0, (int)(4LL * g.M * g.N), 0x00020000);
+            float old[16];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rl = wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+              const bool ok = m0 + rl < g.M && col < g.N;
+              old[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                  crs, ok ? (int)(4 * (moff[rl] + noff[cl])) : 0x7ffffff0, 0, 0));
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int rl = wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+              if (m0 + rl < g.M && col < g.N) g.C[moff[rl] + noff[cl]] = old[r] + actf(acc[i][j][r] * wsc + bv);
+            }
+            return;
+          }
+        }
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int rl = wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
@@ -3133,6 +3175,14 @@ static long long img_span_bytes(const Img& im, int batch) {
 static void set_fast(Plan& p, int batch) {
   GemmArgs& g = p.g;
   p.fast = false;
+  g.im_buf = 0;
+  if (p.mode == MODE_WGRAD && !p.bv) {  // the scalar im2col gathers through a descriptor (element offsets < 2^29)
+    const long long im_bytes = img_span_bytes(g.im, batch);
+    if (im_bytes <= FAST_MAX_BYTES / 4 && g.im.sb >= 0 && g.im.sh >= 0 && g.im.sw >= 0 && g.im.sc >= 0) {
+      g.im_bytes = (int)im_bytes;
+      g.im_buf = 1;
+    }
+  }
   if (!p.av || !p.bv || g.K % BK != 0) return;
   int bm, bn;
   tile_dims(p.cfg, bm, bn);
