@@ -442,12 +442,17 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const float* __restrict__
 
 // apply-pass grid: pixel blocks per channel group, each thread at least `min_iter` pixel
 // rows (round-1 sweep with tools/bn_micro.py: 4096 blocks, 4 rows)
-static dim3 apply_grid(const BnGeo& g, long long P) {
-  constexpr long long blocks = 4096, min_iter = 4;
+static dim3 apply_grid(const BnGeo& g, long long P, long long blocks = 4096) {
+  constexpr long long min_iter = 4;
   const long long rb = std::max<long long>(
       1, std::min<long long>((P + g.rp * min_iter - 1) / (g.rp * min_iter), std::max<long long>(1, blocks / g.cgroups)));
   return dim3(g.cgroups, (unsigned)rb);
 }
+
+// the forward normalise + activation pass (2 streams: y in, a out) on twice the blocks: at
+// C3's largest layer (537 MB moved) 4.36-4.39 -> 4.68-4.72 TB/s (run r6m); the backward
+// passes (3-4 streams) measured slower there, and stay on 4096
+static dim3 fwd_apply_grid(const BnGeo& g, long long P) { return apply_grid(g, P, 8192); }
 
 extern "C" int rgan_bn_apply_segments(const float* y, long long P, int C, int nseg, const float* stats,
                                       const float* gamma, const float* beta, int act, float act_alpha, float* a,
@@ -459,10 +464,10 @@ extern "C" int rgan_bn_apply_segments(const float* y, long long P, int C, int ns
   BnGeo g = bn_geo(P, C, C, 1);
   RGAN_REQUIRE(g.vec && ((uintptr_t)y & 15) == 0 && ((uintptr_t)a & 15) == 0);
   if (nseg == 1)
-    bn_apply_kernel<4, 1><<<apply_grid(g, P), 256, 0, s>>>(y, P, C, C, 1, stats, gamma, beta, act, act_alpha, a, C,
+    bn_apply_kernel<4, 1><<<fwd_apply_grid(g, P), 256, 0, s>>>(y, P, C, C, 1, stats, gamma, beta, act, act_alpha, a, C,
                                                           1, g.tpr, 0);
   else
-    bn_apply_kernel<4, 2><<<apply_grid(g, P), 256, 0, s>>>(y, P, C, C, 1, stats, gamma, beta, act, act_alpha, a, C,
+    bn_apply_kernel<4, 2><<<fwd_apply_grid(g, P), 256, 0, s>>>(y, P, C, C, 1, stats, gamma, beta, act, act_alpha, a, C,
                                                           1, g.tpr, P / 2);
   RGAN_CHECK_LAUNCH();
   return 0;
@@ -478,10 +483,10 @@ extern "C" int rgan_bn_apply(const float* y, long long P, int C, long long sp, l
   const bool vec = g.vec && asc == 1 && asp == C && ((uintptr_t)y & 15) == 0 && ((uintptr_t)a & 15) == 0;
   if (!vec && g.vec) g = bn_geo(P, C, 1, 2);
   if (vec)
-    bn_apply_kernel<4><<<apply_grid(g, P), 256, 0, s>>>(y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, a,
+    bn_apply_kernel<4><<<fwd_apply_grid(g, P), 256, 0, s>>>(y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, a,
                                                        asp, asc, g.tpr);
   else
-    bn_apply_kernel<1><<<apply_grid(g, P), 256, 0, s>>>(y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, a,
+    bn_apply_kernel<1><<<fwd_apply_grid(g, P), 256, 0, s>>>(y, P, C, sp, sc, stats, gamma, beta, act, act_alpha, a,
                                                        asp, asc, g.tpr);
   RGAN_CHECK_LAUNCH();
   return 0;
