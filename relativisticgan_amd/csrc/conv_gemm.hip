@@ -1639,46 +1639,10 @@ __device__ __forceinline__ void dense_stage(float* dst, int ld, const float* __r
 }
 
 // A wide dense layer as a 1 x 1 conv over a 1 x 1 map (arch 1's G input Linear, z -> 4 x 4 x
-// 512, GLI:205-207): y[b][n] = act(wscale sum_k x[b][k] W[n][k] + bias[n]) for B <= 64 rows and
-// K <= 512.  As a GEMM it is M = B rows of a 128-row tile and N / 128 = 64 blocks of 4 k tiles
-// (18 us per C4 call, 3.8 TF/s).  Here a block stages x [B][K] and its DW_NT rows of W (each
-// read from HBM once) in LDS with every load in flight, then thread (feature n, row group q)
-// sums rows q, q + DW_BQ, ... from LDS (x broadcast, W rows padded against bank conflicts).
-constexpr int DW_NT = 32, DW_BQ = 8, DW_MAXB = 64, DW_MAXK = 512;
-__global__ __launch_bounds__(256) void dense_wide_fwd(DenseArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float dxs[];  // x [B][K], W [DW_NT][K + 4]
-  const int B = a.B, K = a.C, ldw = K + 4, n0 = blockIdx.x * DW_NT;
-  float* wl = dxs + B * K;
-  dense_stage(dxs, K, a.x, B, B, K, a.xsb, a.xsc);
-  dense_stage(wl, ldw, a.w + (long long)n0 * K, DW_NT, min(DW_NT, a.N - n0), K, K, 1);
-  __syncthreads();
-  const int j = (int)(threadIdx.x % DW_NT), q = (int)(threadIdx.x / DW_NT), n = n0 + j;
-  if (n >= a.N) return;
-  constexpr int RB = DW_MAXB / DW_BQ;
-  float acc[RB];
-#pragma unroll
-  for (int r = 0; r < RB; ++r) acc[r] = 0.f;
-  const float* wr = wl + j * ldw;
-  for (int k = 0; k < K; k += 4) {
-    const float4 w4 = *reinterpret_cast<const float4*>(wr + k);
-#pragma unroll
-    for (int r = 0; r < RB; ++r) {
-      const int b = q + r * DW_BQ;
-      if (b < B) {
-        const float4 x4 = *reinterpret_cast<const float4*>(dxs + b * K + k);
-        acc[r] += x4.x * w4.x + x4.y * w4.y + x4.z * w4.z + x4.w * w4.w;
-      }
-    }
-  }
-  const float wsc = a.wscale ? a.wscale[0] : 1.f, bn = a.bias ? a.bias[n] : 0.f;
-#pragma unroll
-  for (int r = 0; r < RB; ++r) {
-    const int b = q + r * DW_BQ;
-    if (b < B) a.y[(long long)b * a.ysb + (long long)n * a.ysc] = act_fwd(acc[r] * wsc + bn, a.act, a.alpha);
-  }
-}
-
-// Its weight (and bias) gradient: dW[n][k] (+)= sum_b dy[b][n] x[b][k], dbias[n] (+)= sum_b dy[b][n].
+// 512, GLI:205-207), B <= 64 rows, K <= 512 inputs, N >= 256 outputs: its forward runs on the
+// GEMM's 64 x 64 tiles (choose_tiling); its weight and bias gradient here.
+constexpr int DW_NT = 32, DW_MAXB = 64, DW_MAXK = 512;
+// dW[n][k] (+)= sum_b dy[b][n] x[b][k], dbias[n] (+)= sum_b dy[b][n].
 // As a GEMM: K = B = 32 pixel rows, 3.0 TF/s (22 us per C4 call).  A block owns DW_NT features:
 // x [B][K] and the dy columns [B][DW_NT] staged in LDS (loads in flight), thread (feature, k
 // quad) writes float4 runs of its feature's row (K * 4 contiguous bytes).
@@ -3096,6 +3060,11 @@ static void choose_tiling(Plan& p) {
   // the weight gradient of a thin input layer (N = taps x <= 3 channels <= 32, M = Cout <= 64:
   // arch 1's Conv3x3 3 -> 64, GLI:260): a 256-row tile would be >= 75 % empty rows (round 6)
   if (p.cfg == CFG_N && p.mode == MODE_WGRAD && g.M <= 64 && !emu_bf16x6()) p.cfg = CFG_S;
+  // a thin-M forward with many outputs (arch 1's G input Linear, z -> 4 x 4 x 512 as a 1 x 1 conv
+  // over a 1 x 1 map, M = B = 32): 64 x 64 tiles, 128 blocks instead of 64 half-empty 128 x 128
+  // ones -- 6.2 us per C4 call vs 15.8 (and vs 13.5 for a VALU kernel with LDS-staged rows,
+  // round 6, tools/dense_micro.py)
+  if (p.mode == MODE_CONV && g.M <= 64 && g.N >= 4096 && g.K <= 512 && !emu_bf16x6()) p.cfg = CFG_S;
   if (p.cfg == CFG_L) {
     const long long t = (long long)ceil_div(g.M, 128) * ceil_div(g.N, 128) * p.phases;
     const int nk = ceil_div(g.K, BK);
@@ -3415,18 +3384,16 @@ static bool plan_dense1(Plan& p, const RganConv* d, int op, const float* x, cons
   return true;
 }
 
-// a wide dense layer (a 1 x 1 conv over a 1 x 1 map, >= 256 outputs): dense_wide_fwd (op 3) /
-// dense_wide_wgrad (op 4), reading and writing torch layouts (no packed weight)
+// the weight (and bias) gradient of a wide dense layer (a 1 x 1 conv over a 1 x 1 map, >= 256
+// outputs): dense_wide_wgrad (op 4), torch layouts
 static bool plan_dense_wide(Plan& p, const RganConv* d, int op, const float* x, const float* w, const float* wscale,
                             const float* bias, float* y, float* out, int act, float alpha) {
   if (d->transposed || d->hin != 1 || d->win != 1 || d->kh != 1 || d->kw != 1 || d->hout != 1 || d->wout != 1 ||
       d->pad != 0 || d->stride != 1)
     return false;
   if (d->cout < 256 || d->cin % 4 || d->cin > DW_MAXK || d->batch > DW_MAXB || d->batch < 1) return false;
-  // LDS: x and the W rows (forward) / the dy columns (weight gradient)
-  if (((size_t)d->batch * d->cin + (size_t)DW_NT * (d->cin + 4) + (size_t)d->batch * DW_NT) * 4 > 64 * 1024) return false;
-  if (op == 3 && (!w || !aligned16(w))) return false;
-  if (op == 4 && (!out || !aligned16(out))) return false;
+  if (((size_t)d->batch * d->cin + (size_t)d->batch * DW_NT) * 4 > 64 * 1024) return false;  // LDS: x, the dy columns
+  if (op != 4 || !out || !aligned16(out)) return false;
   p.mode = MODE_DENSE1;
   p.dense_op = op;
   p.pack = false;
@@ -3450,7 +3417,6 @@ static int plan_fwd(const RganConv* d, const float* x, const float* w, const flo
     return 0;
   if (plan_narrow_in(p, d, x, w, wscale, bias, y, act, alpha)) return 0;
   if (plan_dense1(p, d, 0, x, w, wscale, bias, y, nullptr, act, alpha)) return 0;
-  if (plan_dense_wide(p, d, 3, x, w, wscale, bias, y, nullptr, act, alpha)) return 0;
   if (!d->transposed && d->kh == 3 && d->kw == 3 && d->stride == 1 && d->cout <= 4 &&
       plan_narrow3_out(p, d->batch, x, d->xs, d->hin, d->win, d->cin, w, (long long)d->cin * 9, 9, 0, d->cout, y,
                        d->ys, d->hout, d->wout, d->pad, wscale, bias, act, alpha))
@@ -3729,7 +3695,7 @@ static std::vector<ProfRec> g_recs;
 static std::vector<std::string> g_kernel_names;
 static double g_cur_flops = 0.0;
 
-constexpr int N_KERNEL_IDS = 76;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in + 2 bf16x6 + 2 post + 2 post bf16x6 + 2 narrow 3x3 + 12 (mode, av, bv) + 3 FAST (mode) of the 64x64 tile + 2 wide dense
+constexpr int N_KERNEL_IDS = 76;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in + 2 bf16x6 + 2 post + 2 post bf16x6 + 2 narrow 3x3 + 12 (mode, av, bv) + 3 FAST (mode) of the 64x64 tile + the wide dense weight gradient (75; 74 unused)
 
 static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
   if (cfg == CFG_S && mode <= MODE_WGRAD) {
@@ -3767,7 +3733,6 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
     g_kernel_names[47] = "void rgan::dense1_fwd<VEC>(rgan::DenseArgs)";
     g_kernel_names[48] = "void rgan::dense1_dgrad<VEC>(rgan::DenseArgs, rgan::FastDiv)";
     g_kernel_names[49] = "rgan::dense1_wgrad(rgan::DenseArgs)";
-    g_kernel_names[74] = "rgan::dense_wide_fwd(rgan::DenseArgs)";
     g_kernel_names[75] = "rgan::dense_wide_wgrad(rgan::DenseArgs)";
     g_kernel_names[50] = "void rgan::conv_img_in<CI, WT, ACT>(rgan::NarrowArgs)";
     g_kernel_names[51] = "void rgan::gemm_bf16x6<0>(rgan::GemmArgs)";
@@ -3897,10 +3862,6 @@ static int run_narrow3(Plan& p, hipStream_t s) {
 
 static void run_dense1(const Plan& p, const float* packed, hipStream_t s) {
   DenseArgs a = p.da;
-  if (p.dense_op == 3) {
-    dense_wide_fwd<<<ceil_div(a.N, DW_NT), 256, ((size_t)a.B * a.C + (size_t)DW_NT * (a.C + 4)) * 4, s>>>(a);
-    return;
-  }
   if (p.dense_op == 4) {
     dense_wide_wgrad<<<ceil_div(a.N, DW_NT), 256, ((size_t)a.B * a.C + (size_t)a.B * DW_NT) * 4, s>>>(a);
     return;

@@ -32,7 +32,7 @@ def main():
         dw, db = torch.zeros(N, C, 1, 1, device=DEV), torch.zeros(N, device=DEV)
 
         def fwd():
-            K.conv_fwd(x, w, g, bias=b, act="none", out=y)
+            K.conv_fwd(x, w, g, bias=b, act="none", out=y, cache=True)
 
         def wgrad():
             K.conv_wgrad(x, dy, g, w.shape, with_bias=True, out=dw, out_bias=db)
