@@ -1511,11 +1511,6 @@ struct DenseArgs {
   float alpha;
   int vec;
   int accum;                  // wgrad: add into out
-  // dense_wide_*: N outputs, y's channel stride, the fused bias gradient
-  int N = 0;
-  long long ysc = 0;
-  float* dbias = nullptr;
-  int db_accum = 0;
 };
 
 __device__ __forceinline__ long long dense_x_off(const DenseArgs& a, int e, int& widx) {
@@ -1595,101 +1590,6 @@ __global__ __launch_bounds__(256) void dense1_wgrad(DenseArgs a) {
 #pragma unroll 16
   for (int b = 0; b < a.B; ++b) acc = fmaf(a.y[(long long)b * a.ysb], a.x[(long long)b * a.xsb + xo], acc);
   a.out[wi] = a.accum ? a.out[wi] + acc : acc;
-}
-
-// dst[r * ld + c] = src[r * rs + c * cs] (r < rows, c < cols; rows past `valid` read as 0) by a
-// 256-thread block, DWS_UNR loads in flight per thread before their LDS stores (float4 when
-// the rows are contiguous and 16-B aligned): a loop of dependent load -> store pairs left one
-// load in flight per thread, ~0.5 us each
-constexpr int DWS_UNR = 8;
-__device__ __forceinline__ void dense_stage(float* dst, int ld, const float* __restrict__ src, int rows, int valid,
-                                            int cols, long long rs, long long cs) {
-  const bool vec = cs == 1 && (cols & 3) == 0 && (rs & 3) == 0 && (ld & 3) == 0 && ((uintptr_t)src & 15) == 0;
-  if (vec) {
-    const int cq = cols >> 2, n = rows * cq;
-    for (int i0 = threadIdx.x; i0 < n; i0 += 256 * DWS_UNR) {
-      float4 v[DWS_UNR];
-#pragma unroll
-      for (int u = 0; u < DWS_UNR; ++u) {
-        const int i = i0 + 256 * u, r = i / cq, c = 4 * (i - r * cq);
-        v[u] = i < n && r < valid ? *reinterpret_cast<const float4*>(src + r * rs + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int u = 0; u < DWS_UNR; ++u) {
-        const int i = i0 + 256 * u, r = i / cq, c = 4 * (i - r * cq);
-        if (i < n) *reinterpret_cast<float4*>(dst + r * ld + c) = v[u];
-      }
-    }
-  } else {
-    const int n = rows * cols;
-    for (int i0 = threadIdx.x; i0 < n; i0 += 256 * DWS_UNR) {
-      float v[DWS_UNR];
-#pragma unroll
-      for (int u = 0; u < DWS_UNR; ++u) {
-        const int i = i0 + 256 * u, r = i / cols, c = i - r * cols;
-        v[u] = i < n && r < valid ? src[r * rs + c * cs] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < DWS_UNR; ++u) {
-        const int i = i0 + 256 * u, r = i / cols, c = i - r * cols;
-        if (i < n) dst[r * ld + c] = v[u];
-      }
-    }
-  }
-}
-
-// A wide dense layer as a 1 x 1 conv over a 1 x 1 map (arch 1's G input Linear, z -> 4 x 4 x
-// 512, GLI:205-207), B <= 64 rows, K <= 512 inputs, N >= 256 outputs: its forward runs on the
-// GEMM's 64 x 64 tiles (choose_tiling); its weight and bias gradient here.
-constexpr int DW_NT = 32, DW_MAXB = 64, DW_MAXK = 512;
-// dW[n][k] (+)= sum_b dy[b][n] x[b][k], dbias[n] (+)= sum_b dy[b][n].
-// As a GEMM: K = B = 32 pixel rows, 3.0 TF/s (22 us per C4 call).  A block owns DW_NT features:
-// x [B][K] and the dy columns [B][DW_NT] staged in LDS (loads in flight), thread (feature, k
-// quad) writes float4 runs of its feature's row (K * 4 contiguous bytes).
-__global__ __launch_bounds__(256) void dense_wide_wgrad(DenseArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float dws[];  // x [B][K], dy [B][DW_NT]
-  const int B = a.B, K = a.C, n0 = blockIdx.x * DW_NT, nv = min(DW_NT, a.N - n0);
-  float* dys = dws + B * K;
-  dense_stage(dws, K, a.x, B, B, K, a.xsb, a.xsc);
-  // dy columns n0 .. n0 + nv - 1 as [B][DW_NT]: rows = b, cols = features (zero past nv)
-  for (int i0 = threadIdx.x; i0 < B * DW_NT; i0 += 256 * DWS_UNR) {
-    float v[DWS_UNR];
-#pragma unroll
-    for (int u = 0; u < DWS_UNR; ++u) {
-      const int i = i0 + 256 * u, b = i / DW_NT, jj = i - b * DW_NT;
-      v[u] = i < B * DW_NT && jj < nv ? a.y[(long long)b * a.ysb + (long long)(n0 + jj) * a.ysc] : 0.f;
-    }
-#pragma unroll
-    for (int u = 0; u < DWS_UNR; ++u)
-      if (i0 + 256 * u < B * DW_NT) dys[i0 + 256 * u] = v[u];
-  }
-  __syncthreads();
-  const int KQ = K >> 2;
-  for (int i = threadIdx.x; i < DW_NT * KQ; i += 256) {
-    const int j = i / KQ, kq = i - j * KQ, n = n0 + j;
-    if (j >= nv) continue;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int b = 0; b < B; ++b) {
-      const float g = dys[b * DW_NT + j];
-      const float4 x4 = *reinterpret_cast<const float4*>(dws + b * K + 4 * kq);
-      acc.x += g * x4.x;
-      acc.y += g * x4.y;
-      acc.z += g * x4.z;
-      acc.w += g * x4.w;
-    }
-    float4* dst = reinterpret_cast<float4*>(a.out + (long long)n * K + 4 * kq);
-    if (a.accum) {
-      const float4 o = *dst;
-      acc.x += o.x; acc.y += o.y; acc.z += o.z; acc.w += o.w;
-    }
-    *dst = acc;
-  }
-  if (a.dbias && (int)threadIdx.x < nv) {
-    float sb = 0.f;
-    for (int b = 0; b < B; ++b) sb += dys[b * DW_NT + threadIdx.x];
-    float* d = a.dbias + n0 + threadIdx.x;
-    *d = a.db_accum ? *d + sb : sb;
-  }
 }
 
 // WGRAD with 4x4 taps: the GEMM writes C[co][(tap, ci)] with whole-row float4 stores
@@ -3062,9 +2962,13 @@ static void choose_tiling(Plan& p) {
   if (p.cfg == CFG_N && p.mode == MODE_WGRAD && g.M <= 64 && !emu_bf16x6()) p.cfg = CFG_S;
   // a thin-M forward with many outputs (arch 1's G input Linear, z -> 4 x 4 x 512 as a 1 x 1 conv
   // over a 1 x 1 map, M = B = 32): 64 x 64 tiles, 128 blocks instead of 64 half-empty 128 x 128
-  // ones -- 6.2 us per C4 call vs 15.8 (and vs 13.5 for a VALU kernel with LDS-staged rows,
+  // ones -- 6.2 us per C4 call vs 15.8 (and vs 13.5 for a VALU kernel with LDS-staged rows;
   // round 6, tools/dense_micro.py)
   if (p.mode == MODE_CONV && g.M <= 64 && g.N >= 4096 && g.K <= 512 && !emu_bf16x6()) p.cfg = CFG_S;
+  // ... and its weight gradient (M = 8192 outputs, K = B = 32 pixel rows): 64 x 64 tiles, 256 blocks of
+  // one k tile instead of 64 -- 6.4 us per C4 call with the bias vs 19.5 (and vs 12.1 for a VALU
+  // kernel with LDS-staged rows, round 6)
+  if (p.mode == MODE_WGRAD && g.K <= 64 && g.M >= 4096 && !emu_bf16x6()) p.cfg = CFG_S;
   if (p.cfg == CFG_L) {
     const long long t = (long long)ceil_div(g.M, 128) * ceil_div(g.N, 128) * p.phases;
     const int nk = ceil_div(g.K, BK);
@@ -3384,27 +3288,6 @@ static bool plan_dense1(Plan& p, const RganConv* d, int op, const float* x, cons
   return true;
 }
 
-// the weight (and bias) gradient of a wide dense layer (a 1 x 1 conv over a 1 x 1 map, >= 256
-// outputs): dense_wide_wgrad (op 4), torch layouts
-static bool plan_dense_wide(Plan& p, const RganConv* d, int op, const float* x, const float* w, const float* wscale,
-                            const float* bias, float* y, float* out, int act, float alpha) {
-  if (d->transposed || d->hin != 1 || d->win != 1 || d->kh != 1 || d->kw != 1 || d->hout != 1 || d->wout != 1 ||
-      d->pad != 0 || d->stride != 1)
-    return false;
-  if (d->cout < 256 || d->cin % 4 || d->cin > DW_MAXK || d->batch > DW_MAXB || d->batch < 1) return false;
-  if (((size_t)d->batch * d->cin + (size_t)d->batch * DW_NT) * 4 > 64 * 1024) return false;  // LDS: x, the dy columns
-  if (op != 4 || !out || !aligned16(out)) return false;
-  p.mode = MODE_DENSE1;
-  p.dense_op = op;
-  p.pack = false;
-  DenseArgs& a = p.da;
-  a.x = x; a.xsb = d->xs[0]; a.xsc = d->xs[1]; a.xsh = d->xs[2]; a.xsw = d->xs[3];
-  a.w = w; a.wscale = wscale; a.bias = bias; a.y = y; a.ysb = d->ys[0]; a.ysc = d->ys[1]; a.out = out;
-  a.B = d->batch; a.C = d->cin; a.HW = 1; a.E = d->cin; a.N = d->cout;
-  a.act = act; a.alpha = alpha;
-  return true;
-}
-
 // forward GEMM over the conv's input x producing y (conv or transposed conv)
 static int plan_fwd(const RganConv* d, const float* x, const float* w, const float* wscale,
                     const float* bias, float* y, int act, float alpha, Plan& p) {
@@ -3553,7 +3436,6 @@ static int plan_dgrad(const RganConv* d, const float* dy, const float* w, const 
 static int plan_wgrad(const RganConv* d, const float* x, const float* dy, float* dw, Plan& p) {
   if (!desc_ok(d)) return RGAN_EINVAL;
   if (plan_dense1(p, d, 2, x, nullptr, nullptr, nullptr, const_cast<float*>(dy), dw, RGAN_ACT_NONE, 0.f)) return 0;
-  if (plan_dense_wide(p, d, 4, x, nullptr, nullptr, nullptr, const_cast<float*>(dy), dw, RGAN_ACT_NONE, 0.f)) return 0;
   if (plan_wgrad3_narrow(p, d, x, dy, dw)) return 0;
   GemmArgs& g = p.g;
   const int KK = d->kh * d->kw;
@@ -3695,7 +3577,7 @@ static std::vector<ProfRec> g_recs;
 static std::vector<std::string> g_kernel_names;
 static double g_cur_flops = 0.0;
 
-constexpr int N_KERNEL_IDS = 76;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in + 2 bf16x6 + 2 post + 2 post bf16x6 + 2 narrow 3x3 + 12 (mode, av, bv) + 3 FAST (mode) of the 64x64 tile + the wide dense weight gradient (75; 74 unused)
+constexpr int N_KERNEL_IDS = 74;  // 36 (mode, cfg, av, bv) + 9 FAST (mode, cfg) + 2 narrow + 3 dense + img_in + 2 bf16x6 + 2 post + 2 post bf16x6 + 2 narrow 3x3 + 12 (mode, av, bv) + 3 FAST (mode) of the 64x64 tile
 
 static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
   if (cfg == CFG_S && mode <= MODE_WGRAD) {
@@ -3704,7 +3586,7 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
   }
   const int id = mode == MODE_NARROW_T ? 45
                  : mode == MODE_NARROW_IN ? 46
-                 : mode == MODE_DENSE1 ? (cfg >= 3 ? 71 + cfg : 47 + cfg)
+                 : mode == MODE_DENSE1 ? 47 + cfg
                  : mode == MODE_NARROW3 ? 57
                  : mode == MODE_NARROW3W ? 58
                  : fast ? 36 + mode * 3 + cfg
@@ -3733,7 +3615,6 @@ static int kernel_id(int mode, int cfg, bool av, bool bv, bool fast = false) {
     g_kernel_names[47] = "void rgan::dense1_fwd<VEC>(rgan::DenseArgs)";
     g_kernel_names[48] = "void rgan::dense1_dgrad<VEC>(rgan::DenseArgs, rgan::FastDiv)";
     g_kernel_names[49] = "rgan::dense1_wgrad(rgan::DenseArgs)";
-    g_kernel_names[75] = "rgan::dense_wide_wgrad(rgan::DenseArgs)";
     g_kernel_names[50] = "void rgan::conv_img_in<CI, WT, ACT>(rgan::NarrowArgs)";
     g_kernel_names[51] = "void rgan::gemm_bf16x6<0>(rgan::GemmArgs)";
     g_kernel_names[52] = "void rgan::gemm_bf16x6<1>(rgan::GemmArgs)";
@@ -3862,10 +3743,6 @@ static int run_narrow3(Plan& p, hipStream_t s) {
 
 static void run_dense1(const Plan& p, const float* packed, hipStream_t s) {
   DenseArgs a = p.da;
-  if (p.dense_op == 4) {
-    dense_wide_wgrad<<<ceil_div(a.N, DW_NT), 256, ((size_t)a.B * a.C + (size_t)a.B * DW_NT) * 4, s>>>(a);
-    return;
-  }
   if (p.dense_op != 2) a.w = packed;
   if (p.dense_op != 2) {
     const float* t = p.dense_op == 0 ? a.x : a.out;
@@ -4448,11 +4325,6 @@ extern "C" int rgan_conv_wgrad_rows(const RganConv* d, const float* x, const flo
   const bool bias_fused = dbias && p.mode == MODE_WGRAD && p.fast && !d->transposed && ws_bytes >= plan_bytes &&
                           dbias_row0 % BK == 0 && dbias_row0 <= (long long)INT32_MAX &&
                           (p.g.splits == 1 || (size_t)p.g.splits * p.g.M * sizeof(double) <= ws_bytes - plan_bytes);
-  if (dbias && p.mode == MODE_DENSE1 && p.dense_op == 4 && dbias_row0 == 0) {  // dense_wide_wgrad sums it
-    p.da.dbias = dbias;
-    p.da.db_accum = accumulate ? 1 : 0;
-    return run_plan(p, ws, ws_bytes, (hipStream_t)stream);
-  }
   if (bias_fused) {
     p.g.dbias = dbias;
     p.g.db_accum = accumulate ? 1 : 0;

@@ -245,10 +245,10 @@ def test_conv_dense_one_output(K, case):
 
 @pytest.mark.parametrize("B,C,N", [(32, 128, 8192), (1, 4, 256), (64, 100, 300), (7, 512, 1024), (33, 20, 260)])
 def test_conv_dense_wide(K, B, C, N):
-    """A wide dense layer as a 1x1 conv over a 1x1 map (arch 1's G input Linear, GLI:205-207:
-    dense_wide_fwd / dense_wide_wgrad): fwd with bias, wscale and activation, wgrad + dbias
-    (written, accumulated, into the .grad given), through a weight view as arch 1 calls it,
-    vs torch fp64; ragged N (not a multiple of 32) and B (not of 8)."""
+    """A wide dense layer as a 1x1 conv over a 1x1 map (arch 1's G input Linear, GLI:205-207: the
+    GEMM's 64x64 tiles for the thin-M forward and the K <= 64 weight gradient): fwd with bias,
+    wscale and activation, wgrad + dbias (written, accumulated, the bias over a row range),
+    through a weight view as arch 1 calls it, vs torch fp64; ragged N and B."""
     g = K.ConvGeom(1, 1, 0, False)
     torch.manual_seed(B + C)
     x = torch.randn(B, C, 1, 1, device=DEV)
@@ -273,7 +273,7 @@ def test_conv_dense_wide(K, B, C, N):
     K.conv_wgrad(x, dy, g, w.shape, with_bias=True, out=dwa, out_bias=dba)
     assert _rel(dwa, dw0.double().cpu() + w64.grad) < 1e-5
     assert _rel(dba, db0.double().cpu() + b64.grad) < 1e-6
-    if B >= 2:  # bias over rows [B/2, B): the channel-sum path beside the wide weight gradient
+    if B >= 2:  # bias over rows [B/2, B) (rgan_conv_wgrad_rows)
         dwr, dbr = dw0.clone(), db0.clone()
         K.conv_wgrad(x, dy, g, w.shape, with_bias=True, out=dwr, out_bias=dbr, bias_row0=B // 2)
         assert _rel(dwr, dw0.double().cpu() + w64.grad) < 1e-5
